@@ -1,0 +1,323 @@
+#!/usr/bin/env python3
+"""Capture golden vectors from the REFERENCE BlueSky (build container only).
+
+Runs the reference's own numpy code from ``/root/reference`` (read-only; the
+numpy-2 shims below are the only changes, applied to the numpy module, not to
+the reference) on fixed synthetic / hand-made inputs and writes the inputs
+and outputs as small ``.npz`` files under ``tests/golden/``:
+
+* ``cd_<case>.npz``   -- ``StateBasedCD.detect`` (StateBasedCD.py:7-103)
+* ``mvp_<case>.npz``  -- ``MVP.resolve`` (MVP.py:14-143) for several switch sets
+* ``kin_<case>.npz``  -- ``Traffic.UpdateAirSpeed/GroundSpeed/Position``
+                         (traffic.py:425-483)
+
+It also runs the CPU restatement in ``oracle/`` on the same inputs and
+asserts bit-for-bit equality, so the oracle is pinned at capture time.
+The reference never leaves this container; only the vectors are committed.
+
+Usage:  python tools/make_golden.py   (takes ~1 min)
+"""
+import os
+import sys
+import types
+import zlib
+
+import numpy as np
+
+REF = '/root/reference'
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, 'tests', 'golden')
+
+# numpy-2 shims for the 2019 reference
+np.mat = np.asmatrix
+np.int = int
+np.float = float
+np.object = object
+np.str = str
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+sys.path.insert(0, REPO)
+
+from bluesky.traffic.asas import StateBasedCD, MVP          # noqa: E402
+from bluesky.traffic.traffic import Traffic as RefTraffic    # noqa: E402
+from bluesky.traffic.windsim import WindSim                  # noqa: E402
+from bluesky.tools.aero import ft, nm, kts, fpm              # noqa: E402
+
+from bluesky_amd import synth                                # noqa: E402
+from oracle import statebased as ocd                         # noqa: E402
+from oracle import mvp as omvp                               # noqa: E402
+from oracle import kinematics as okin                        # noqa: E402
+
+RPZ = 5.0 * nm
+HPZ = 1000.0 * ft
+TLA = 300.0
+
+
+def T(lat, lon, alt, trk, gs, vs):
+    return synth.Traffic(lat, lon, alt, trk, gs, vs)
+
+
+def edge_traffic():
+    rows = [
+        # lat,     lon,      alt,    trk,  gs,  vs
+        (52.0,     4.0,      10000., 90.,  200., 0.),    # 0
+        (52.0,     4.0,      10000., 90.,  200., 0.),    # 1 identical to 0
+        (52.0,     4.1,      10000., 270., 200., 0.),    # 2 head-on with 0/1
+        (52.0,     4.0,      10500., 90.,  200., 0.),    # 3 500 m above, level
+        (52.0,     4.0,      10200., 90.,  200., -5.),   # 4 vertical LoS
+        (0.0,      20.0,     9000.,  0.,   250., 0.),    # 5 lat == 0 exactly
+        (-0.01,    20.01,    9000.,  45.,  250., 0.),    # 6 southern hemisphere
+        (0.02,     20.0,     9000.,  180., 250., 0.),    # 7 northern, converging
+        (10.0,     179.95,   11000., 90.,  230., 0.),    # 8 antimeridian
+        (10.0,     -179.95,  11000., 270., 230., 0.),    # 9
+        (89.99,    0.0,      12000., 0.,   240., 0.),    # 10 near pole
+        (89.99,    180.0,    12000., 180., 240., 0.),    # 11
+        (52.0,     5.0,      10000., 0.,   0.,   0.),    # 12 zero speed
+        (52.0,     5.0,      10000., 0.,   0.,   0.),    # 13 zero speed, same pos
+        (52.05,    5.0,      10000., 180., 100., 0.),    # 14
+        (52.0,     6.0,      10000., 90.,  200., 0.),    # 15 parallel tracks
+        (52.01,    6.0,      10000., 90.,  200., 0.),    # 16
+        (52.0,     7.0,      5000.,  0.,   200., 10.),   # 17 climbing into 18
+        (52.0,     7.0,      6000.,  0.,   200., 0.),    # 18
+        (-30.0,    150.0,    10000., 0.,   200., 0.),    # 19 overtaking
+        (-30.05,   150.0,    10000., 0.,   220., 0.),    # 20
+        (-0.03,    20.02,    9100.,  300., 240., 3.),    # 21 southern, near 5-7
+        (0.0,      20.03,    9050.,  200., 260., -3.),   # 22 lat == 0 exactly
+    ]
+    a = np.array(rows, dtype=np.float64)
+    return T(*[a[:, k] for k in range(6)])
+
+
+def wrap_lon(t):
+    t.lon = ((t.lon + 180.0) % 360.0) - 180.0
+    return t
+
+
+def cd_cases():
+    cases = {}
+    cases['box64'] = (synth.box(64, 30.0, seed=1), None)
+    cases['box500'] = (synth.box(500, 150.0, seed=11), None)
+    cases['box2000'] = (synth.box(2000, 500.0, seed=7), None)
+    cases['equator1500'] = (synth.box(1500, 180.0, seed=5, lat0=0.0, lon0=-40.0), None)
+    cases['antimeridian800'] = (wrap_lon(synth.box(800, 200.0, seed=9, lat0=-20.0, lon0=180.0)), None)
+    cases['polar400'] = (synth.box(400, 60.0, seed=21, lat0=89.0, lon0=0.0), None)
+    cases['global3000'] = (synth.global_traffic(3000, seed=13), None)
+    cases['edge'] = (edge_traffic(), None)
+    own = synth.box(300, 60.0, seed=3, lat0=0.0, lon0=10.0)
+    intr = synth.box(300, 60.0, seed=4, lat0=0.0, lon0=10.0)
+    own.lat[::17] = 0.0
+    intr.lat[5::23] = 0.0
+    cases['own_ne_int300'] = (own, intr)
+    return cases
+
+
+def ids_to_idx(pairs, idmap):
+    if not pairs:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    a = np.array([(idmap[p], idmap[q]) for p, q in pairs], dtype=np.int64)
+    return a[:, 0], a[:, 1]
+
+
+def run_cd(name, own, intr):
+    intr_ = own if intr is None else intr
+    res = StateBasedCD.detect(own, intr_, RPZ, HPZ, TLA)
+    confpairs, lospairs, inconf, tcpamax, qdr, dist, tcpa, tin = res
+    idmap = {k: i for i, k in enumerate(own.id)}
+    ci, cj = ids_to_idx(confpairs, idmap)
+    li, lj = ids_to_idx(lospairs, idmap)
+    # oracle must be bitwise equal here
+    o = ocd.detect_arrays(own, intr_, RPZ, HPZ, TLA, budget_bytes=64 << 20)
+    for k, v in (('ci', ci), ('cj', cj), ('li', li), ('lj', lj),
+                 ('inconf', np.asarray(inconf)), ('tcpamax', np.asarray(tcpamax)),
+                 ('qdr', np.asarray(qdr)), ('dist', np.asarray(dist)),
+                 ('tcpa', np.asarray(tcpa)), ('tinconf', np.asarray(tin))):
+        ok = np.array_equal(o[k], v) if k != 'tcpamax' else np.all(o[k] == v)
+        assert ok, 'oracle != reference for %s/%s' % (name, k)
+    d = dict(lat=own.lat, lon=own.lon, alt=own.alt, trk=own.trk, gs=own.gs, vs=own.vs,
+             same=np.array(intr is None), rpz=RPZ, hpz=HPZ, tla=TLA,
+             ci=ci, cj=cj, li=li, lj=lj, inconf=np.asarray(inconf),
+             tcpamax=np.asarray(tcpamax), qdr=np.asarray(qdr), dist=np.asarray(dist),
+             tcpa=np.asarray(tcpa), tinconf=np.asarray(tin))
+    if intr is not None:
+        d.update(ilat=intr.lat, ilon=intr.lon, ialt=intr.alt, itrk=intr.trk,
+                 igs=intr.gs, ivs=intr.vs)
+    np.savez_compressed(os.path.join(OUT, 'cd_%s.npz' % name), **d)
+    print('cd_%-18s N=%5d conf=%6d los=%5d' % (name, own.ntraf, len(ci), len(li)))
+    return res
+
+
+# ---------------------------------------------------------------- MVP
+MVP_MODES = {
+    # name: (swresohoriz, swresospd, swresohdg, swresovert, swprio, priocode, noreso, resooff)
+    'default': (True, False, False, False, False, 'FF1', False, False),
+    'spd': (True, True, False, False, False, 'FF1', False, False),
+    'hdg': (True, False, True, False, False, 'FF1', False, False),
+    'vert': (False, False, False, True, False, 'FF1', False, False),
+    'hv': (False, False, False, False, False, 'FF1', False, False),
+    'ff1': (False, False, False, False, True, 'FF1', False, False),
+    'ff2': (False, False, False, False, True, 'FF2', False, False),
+    'ff3': (False, False, False, False, True, 'FF3', False, False),
+    'lay1': (False, False, False, False, True, 'LAY1', False, False),
+    'lay2': (False, False, False, False, True, 'LAY2', False, False),
+    'noreso': (False, False, False, False, False, 'FF1', True, False),
+    'resooff': (False, False, False, False, False, 'FF1', False, True),
+}
+
+
+def mvp_inputs(traf, seed):
+    rng = np.random.default_rng(seed)
+    n = traf.ntraf
+    gseast = traf.gs * np.sin(np.radians(traf.trk))
+    gsnorth = traf.gs * np.cos(np.radians(traf.trk))
+    selalt = traf.alt + rng.choice([0.0, 0.0, 2000.0 * ft, -2000.0 * ft, 150.0], n)
+    apvs = rng.choice([0.0, 1500.0 * fpm, 2500.0 * fpm], n)
+    asasalt = traf.alt + rng.choice([0.0, 1000.0 * ft, -1000.0 * ft], n)
+    return dict(gseast=gseast, gsnorth=gsnorth, selalt=selalt, apvs=apvs, asasalt=asasalt)
+
+
+def run_mvp(name, traf, cdres, mar=1.05):
+    confpairs, lospairs, inconf, tcpamax, qdr, dist, tcpa, tin = cdres
+    extra = mvp_inputs(traf, seed=zlib.crc32(name.encode()) % 1000)
+    ids = list(traf.id)
+    idmap = {k: i for i, k in enumerate(ids)}
+    ci, cj = ids_to_idx(confpairs, idmap)
+    noresolst = ids[::7]
+    resoofflst = ids[3::11]
+    out = dict(ci=ci, cj=cj, qdr=np.asarray(qdr), dist=np.asarray(dist),
+               tcpa=np.asarray(tcpa), tLOS=np.asarray(tin),
+               lat=traf.lat, lon=traf.lon, alt=traf.alt, trk=traf.trk, gs=traf.gs,
+               vs=traf.vs, mar=mar, rpz=RPZ, hpz=HPZ, tla=TLA,
+               noreso_idx=np.arange(0, len(ids), 7), resooff_idx=np.arange(3, len(ids), 11),
+               **extra)
+    for mode, sw in MVP_MODES.items():
+        asas, tr = make_ref_asas(traf, extra, confpairs, qdr, dist, tcpa, tin, mar, sw,
+                                 noresolst, resoofflst)
+        MVP.resolve(asas, tr)
+        # oracle must agree bitwise
+        o = omvp.resolve_arrays(
+            ci, cj, np.asarray(qdr), np.asarray(dist), np.asarray(tcpa), np.asarray(tin),
+            gseast=extra['gseast'], gsnorth=extra['gsnorth'], vs=traf.vs, alt=traf.alt,
+            trk=traf.trk, gs=traf.gs, selalt=extra['selalt'], apvs=extra['apvs'],
+            asasalt=extra['asasalt'].copy(), params=omvp.params_from_settings(
+                RPZ, HPZ, TLA, mar, *sw[:6]),
+            noreso=np.isin(np.arange(len(ids)), out['noreso_idx']) if sw[6] else None,
+            resooff=np.isin(np.arange(len(ids)), out['resooff_idx']) if sw[7] else None)
+        for k in ('trk', 'tas', 'vs', 'alt', 'asase', 'asasn'):
+            ref = np.asarray(getattr(asas, k))
+            assert np.array_equal(o[k], ref, equal_nan=True), \
+                'oracle != reference MVP %s/%s/%s' % (name, mode, k)
+        for k in ('trk', 'tas', 'vs', 'alt', 'asase', 'asasn'):
+            out['%s__%s' % (mode, k)] = np.asarray(getattr(asas, k))
+    np.savez_compressed(os.path.join(OUT, 'mvp_%s.npz' % name), **out)
+    print('mvp_%-17s N=%5d pairs=%6d modes=%d' % (name, traf.ntraf, len(ci), len(MVP_MODES)))
+
+
+def make_ref_asas(traf, extra, confpairs, qdr, dist, tcpa, tin, mar, sw,
+                  noresolst, resoofflst):
+    hz, spd, hdg, vert, prio, code, noreso, resooff = sw
+    asas = types.SimpleNamespace()
+    asas.swasas = True
+    asas.confpairs = list(confpairs)
+    asas.qdr, asas.dist, asas.tcpa, asas.tLOS = (np.asarray(qdr), np.asarray(dist),
+                                                  np.asarray(tcpa), np.asarray(tin))
+    asas.R = RPZ
+    asas.dh = HPZ
+    asas.mar = mar
+    asas.Rm = RPZ * mar
+    asas.dhm = HPZ * mar
+    asas.dtlookahead = TLA
+    asas.vmin = 200.0 * nm / 3600.
+    asas.vmax = 500.0 * nm / 3600.
+    asas.vsmin = -3000. / 60. * ft
+    asas.vsmax = 3000. / 60. * ft
+    asas.swresohoriz, asas.swresospd, asas.swresohdg, asas.swresovert = hz, spd, hdg, vert
+    asas.swprio, asas.priocode = prio, code
+    asas.swnoreso, asas.noresolst = noreso, list(noresolst)
+    asas.swresooff, asas.resoofflst = resooff, list(resoofflst)
+    asas.alt = extra['asasalt'].copy()
+    asas.asaseval = False
+    tr = types.SimpleNamespace()
+    tr.ntraf = traf.ntraf
+    tr.id = list(traf.id)
+    tr.alt, tr.vs, tr.trk, tr.gs = traf.alt, traf.vs, traf.trk, traf.gs
+    tr.gseast, tr.gsnorth = extra['gseast'], extra['gsnorth']
+    tr.selalt = extra['selalt']
+    tr.ap = types.SimpleNamespace(vs=extra['apvs'])
+    return asas, tr
+
+
+# ---------------------------------------------------------------- kinematics
+def kin_state(n, seed):
+    rng = np.random.default_rng(seed)
+    t = synth.box(n, 300.0, seed=seed)
+    s = {}
+    s['lat'], s['lon'], s['alt'] = t.lat.copy(), t.lon.copy(), t.alt.copy()
+    s['tas'] = t.gs.copy()
+    s['hdg'] = t.trk.copy()
+    s['vs'] = t.vs.copy()
+    # pilot targets: a mix of "already there", small and large deltas
+    s['ptas'] = s['tas'] + rng.choice([0.0, 0.3 * kts, 5.0, -12.0, 30.0], n)
+    s['phdg'] = (s['hdg'] + rng.choice([0.0, 0.05, 3.0, -90.0, 179.0, -181.0], n)) % 360.0
+    s['palt'] = s['alt'] + rng.choice([0.0, 2.0, 1000.0 * ft, -3000.0 * ft, 10.0 * ft], n)
+    s['pvs'] = rng.choice([0.0, 1500.0 * fpm, 3000.0 * fpm, 250.0 * fpm], n)
+    s['bank'] = np.full(n, np.radians(25.0))
+    s['eps'] = np.full(n, 0.01)
+    s['accel'] = np.where(rng.random(n) < 0.1, 2.0, 0.5)
+    # sprinkle edge values
+    s['tas'][:5] = [0.0, 0.001, 300.0, 120.0, 0.0]
+    s['vs'][5:8] = [0.0, 2.0, -12.0]
+    s['lat'][8] = 89.999
+    s['hdg'][9] = 359.99
+    s['phdg'][9] = 0.01
+    return s
+
+
+def run_kin(name, n, seed, dt, wind=None):
+    s = kin_state(n, seed)
+    fake = types.SimpleNamespace()
+    fake.pilot = types.SimpleNamespace(tas=s['ptas'].copy(), hdg=s['phdg'].copy(),
+                                       alt=s['palt'].copy(), vs=s['pvs'].copy())
+    fake.tas, fake.hdg, fake.alt, fake.vs = (s['tas'].copy(), s['hdg'].copy(),
+                                             s['alt'].copy(), s['vs'].copy())
+    fake.lat, fake.lon = s['lat'].copy(), s['lon'].copy()
+    fake.bank, fake.eps = s['bank'].copy(), s['eps'].copy()
+    acc = s['accel'].copy()
+    fake.perf = types.SimpleNamespace(acceleration=lambda: acc)
+    fake.wind = WindSim()
+    if wind is not None:
+        fake.wind.addpoint(52.0, 4.0, wind[0], wind[1])
+    RefTraffic.UpdateAirSpeed(fake, dt, 0.0)
+    RefTraffic.UpdateGroundSpeed(fake, dt)
+    RefTraffic.UpdatePosition(fake, dt)
+    keys = ('ax', 'delspd', 'tas', 'cas', 'M', 'hdg', 'swhdgsel', 'swaltsel', 'az', 'vs',
+            'gsnorth', 'gseast', 'gs', 'trk', 'alt', 'lat', 'lon', 'coslat')
+    ref = {k: np.asarray(getattr(fake, k)) for k in keys}
+    vn = ve = 0.0
+    if wind is not None:
+        vn_, ve_ = fake.wind.getdata(np.array([0.0]), np.array([0.0]), np.array([0.0]))
+        vn, ve = float(vn_[0]), float(ve_[0])
+    o = okin.step(s, dt, winddim=0 if wind is None else 1, windnorth=vn, windeast=ve)
+    for k in keys:
+        assert np.array_equal(o[k], ref[k], equal_nan=True), 'oracle != reference kin %s/%s' % (name, k)
+    out = dict(dt=dt, winddim=0 if wind is None else 1, windnorth=vn, windeast=ve, **s)
+    out.update({'out_' + k: v for k, v in ref.items()})
+    np.savez_compressed(os.path.join(OUT, 'kin_%s.npz' % name), **out)
+    print('kin_%-17s N=%5d dt=%g wind=%s' % (name, n, dt, wind))
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    cds = cd_cases()
+    results = {}
+    for name, (own, intr) in cds.items():
+        results[name] = run_cd(name, own, intr)
+    for name in ('box64', 'box500', 'box2000', 'edge', 'equator1500'):
+        run_mvp(name, cds[name][0], results[name])
+    run_kin('nowind2000', 2000, 31, 0.05)
+    run_kin('nowind_dt1', 500, 32, 1.0)
+    run_kin('wind1000', 1000, 33, 0.05, wind=(270.0, 25.0 * kts))
+
+
+if __name__ == '__main__':
+    main()
