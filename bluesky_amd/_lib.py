@@ -1,0 +1,271 @@
+"""ctypes binding of ``libbsaccel.so`` (declarations in ``include/bsaccel.h``).
+
+The HIP library is the ONLY compute path: if it is missing, or no HIP device
+is visible, every call raises ``AccelUnavailable`` -- there is deliberately no
+CPU fallback in the product path.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('BSACCEL_LIB', os.path.join(_HERE, 'libbsaccel.so'))
+
+ABI_VERSION = 1
+FLAG_WITH_DCPA = 1
+FLAG_NOPRUNE = 2
+
+_c_dp = ctypes.POINTER(ctypes.c_double)
+_c_fp = ctypes.POINTER(ctypes.c_float)
+_c_i32p = ctypes.POINTER(ctypes.c_int32)
+_c_u8p = ctypes.POINTER(ctypes.c_uint8)
+_c_i64p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+
+
+class AccelUnavailable(RuntimeError):
+    """libbsaccel.so could not be loaded or has no usable HIP device."""
+
+
+class AccelError(RuntimeError):
+    """A libbsaccel call returned an error status."""
+
+
+# name -> (restype, argtypes); must match include/bsaccel.h exactly
+SIGNATURES = {
+    'bsa_abi_version': (ctypes.c_int, []),
+    'bsa_device_count': (ctypes.c_int, []),
+    'bsa_create': (_vp, [ctypes.c_int]),
+    'bsa_destroy': (None, [_vp]),
+    'bsa_last_error': (ctypes.c_char_p, [_vp]),
+    'bsa_sync': (ctypes.c_int, [_vp]),
+    'bsa_set_state': (ctypes.c_int, [_vp, ctypes.c_int64] + [_c_dp] * 6),
+    'bsa_set_intruder': (ctypes.c_int, [_vp, ctypes.c_int64] + [_c_dp] * 6),
+    'bsa_detect': (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                  ctypes.c_int, ctypes.c_int64, ctypes.c_int64, _c_i64p, _c_i64p]),
+    'bsa_fetch_pairs': (ctypes.c_int, [_vp, _c_i32p, _c_i32p, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
+                                       _c_i32p, _c_i32p, _c_u8p, _c_dp]),
+    'bsa_last_candidates': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
+}
+
+PRIO_CODES = {'FF1': 1, 'FF2': 2, 'FF3': 3, 'LAY1': 4, 'LAY2': 5}
+
+
+class MvpParams(ctypes.Structure):
+    """bsa_mvp_params (include/bsaccel.h)."""
+    _fields_ = [('Rm', ctypes.c_double), ('dhm', ctypes.c_double),
+                ('dtlookahead', ctypes.c_double), ('vmin', ctypes.c_double),
+                ('vmax', ctypes.c_double), ('vsmin', ctypes.c_double), ('vsmax', ctypes.c_double),
+                ('swresohoriz', ctypes.c_int32), ('swresospd', ctypes.c_int32),
+                ('swresohdg', ctypes.c_int32), ('swresovert', ctypes.c_int32),
+                ('swprio', ctypes.c_int32), ('priocode', ctypes.c_int32),
+                ('swnoreso', ctypes.c_int32), ('swresooff', ctypes.c_int32)]
+
+
+class KinIO(ctypes.Structure):
+    """bsa_kin_io (include/bsaccel.h)."""
+    _fields_ = [(k, _c_dp) for k in ('ptas', 'phdg', 'palt', 'pvs', 'bank', 'eps', 'accel',
+                                     'tas', 'hdg', 'alt', 'vs', 'lat', 'lon', 'ax', 'delspd',
+                                     'cas', 'mach', 'gsnorth', 'gseast', 'gs', 'trk', 'coslat',
+                                     'az')] + [('swhdgsel', _c_u8p), ('swaltsel', _c_u8p)]
+
+
+SIGNATURES.update({
+    'bsa_set_pairs': (ctypes.c_int, [_vp, ctypes.c_int64, _c_i32p, _c_i32p, _c_dp, _c_dp, _c_dp,
+                                     _c_dp]),
+    'bsa_mvp': (ctypes.c_int, [_vp, ctypes.POINTER(MvpParams), _c_dp, _c_dp, _c_dp, _c_dp, _c_u8p,
+                               _c_u8p, _c_dp, _c_dp, _c_dp, _c_dp, _c_fp, _c_fp]),
+    'bsa_kinematics': (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_double, ctypes.c_int,
+                                      ctypes.c_double, ctypes.c_double, ctypes.POINTER(KinIO)]),
+})
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load(path=None):
+    """Load and type the library (idempotent).  Raises AccelUnavailable."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise AccelUnavailable('libbsaccel.so not built (%s); run `make -C bluesky_amd/csrc` '
+                                   'or __graft_entry__.build()' % p)
+        try:
+            lib = ctypes.CDLL(p)
+        except OSError as e:
+            raise AccelUnavailable('cannot load %s: %s' % (p, e))
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        v = lib.bsa_abi_version()
+        if v != ABI_VERSION:
+            raise AccelUnavailable('ABI mismatch: library %d, bindings %d' % (v, ABI_VERSION))
+        _lib = lib
+        return lib
+
+
+def ptr(a, ctype=_c_dp):
+    return None if a is None else a.ctypes.data_as(ctype)
+
+
+def f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Context:
+    """One HIP device + stream + its device buffers (bsa_ctx)."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        ndev = self.lib.bsa_device_count()
+        if ndev <= 0:
+            raise AccelUnavailable('no HIP device visible (bsa_device_count=%d)' % ndev)
+        h = self.lib.bsa_create(int(device))
+        if not h:
+            raise AccelUnavailable('bsa_create(%d) failed: %s'
+                                   % (device, self.lib.bsa_last_error(None).decode()))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.bsa_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, status, what):
+        if status != 0:
+            raise AccelError('%s: %s' % (what, self.lib.bsa_last_error(self.h).decode()))
+
+    # ---------------------------------------------------------------- state
+    def set_state(self, lat, lon, trk, gs, alt, vs):
+        arrs = [f64(x) for x in (lat, lon, trk, gs, alt, vs)]
+        n = len(arrs[0])
+        if any(len(a) != n for a in arrs):
+            raise ValueError('state arrays differ in length')
+        self.check(self.lib.bsa_set_state(self.h, n, *[ptr(a) for a in arrs]), 'bsa_set_state')
+        self.n = n
+
+    def set_intruder(self, lat=None, lon=None, trk=None, gs=None, alt=None, vs=None):
+        if lat is None:
+            self.check(self.lib.bsa_set_intruder(self.h, 0, *([None] * 6)), 'bsa_set_intruder')
+            return
+        arrs = [f64(x) for x in (lat, lon, trk, gs, alt, vs)]
+        self.check(self.lib.bsa_set_intruder(self.h, len(arrs[0]), *[ptr(a) for a in arrs]),
+                   'bsa_set_intruder')
+
+    # ---------------------------------------------------------------- detect
+    def detect(self, rpz, hpz, tla, flags=0, row_begin=0, row_end=-1):
+        nc = ctypes.c_int64()
+        nl = ctypes.c_int64()
+        self.check(self.lib.bsa_detect(self.h, float(rpz), float(hpz), float(tla), int(flags),
+                                       int(row_begin), int(row_end), ctypes.byref(nc),
+                                       ctypes.byref(nl)), 'bsa_detect')
+        self._rows = (row_begin, self.n if row_end is None or row_end < 0 else row_end)
+        return nc.value, nl.value
+
+    def fetch_pairs(self, n_conf, n_los, with_dcpa=False):
+        P, L = n_conf, n_los
+        R = self._rows[1] - self._rows[0]
+        o = dict(ci=np.empty(P, np.int32), cj=np.empty(P, np.int32), qdr=np.empty(P),
+                 dist=np.empty(P), tcpa=np.empty(P), tinconf=np.empty(P),
+                 dcpa=np.empty(P) if with_dcpa else None, li=np.empty(L, np.int32),
+                 lj=np.empty(L, np.int32), inconf=np.empty(R, np.uint8), tcpamax=np.empty(R))
+        self.check(self.lib.bsa_fetch_pairs(
+            self.h, ptr(o['ci'], _c_i32p), ptr(o['cj'], _c_i32p), ptr(o['qdr']), ptr(o['dist']),
+            ptr(o['tcpa']), ptr(o['tinconf']), ptr(o['dcpa']), ptr(o['li'], _c_i32p),
+            ptr(o['lj'], _c_i32p), ptr(o['inconf'], _c_u8p), ptr(o['tcpamax'])), 'bsa_fetch_pairs')
+        return o
+
+    def last_candidates(self):
+        v = ctypes.c_int64()
+        self.check(self.lib.bsa_last_candidates(self.h, ctypes.byref(v)), 'bsa_last_candidates')
+        return v.value
+
+    def last_timings(self):
+        t = np.zeros(5)
+        self.check(self.lib.bsa_last_timings(self.h, ptr(t)), 'bsa_last_timings')
+        return dict(prep=t[0], prefilter=t[1], exact=t[2], sort=t[3], total=t[4])
+
+    def sync(self):
+        self.check(self.lib.bsa_sync(self.h), 'bsa_sync')
+
+    # ---------------------------------------------------------------- MVP
+    def set_pairs(self, ci, cj, qdr, dist, tcpa, tlos):
+        """bsa_set_pairs: external confpairs (row-major) for bsa_mvp."""
+        ci = np.ascontiguousarray(ci, dtype=np.int32)
+        cj = np.ascontiguousarray(cj, dtype=np.int32)
+        arrs = [f64(x) for x in (qdr, dist, tcpa, tlos)]
+        self.check(self.lib.bsa_set_pairs(self.h, len(ci), ptr(ci, _c_i32p), ptr(cj, _c_i32p),
+                                          *[ptr(a) for a in arrs]), 'bsa_set_pairs')
+        self._rows = (0, self.n)
+
+    def mvp(self, params, gseast, gsnorth, selalt, apvs, asas_alt, noreso=None, resooff=None):
+        """bsa_mvp on the last detect's pairs; ``asas_alt`` (detect rows) is
+        updated in place.  Returns dict(trk, tas, vs, asase, asasn)."""
+        rows = self._rows[1] - self._rows[0]
+        ins = [f64(x) for x in (gseast, gsnorth, selalt, apvs)]
+        if asas_alt.dtype != np.float64 or not asas_alt.flags.c_contiguous or len(asas_alt) != rows:
+            raise ValueError('asas_alt must be a contiguous float64 array of the detect rows')
+        nr = None if noreso is None else np.ascontiguousarray(noreso, dtype=np.uint8)
+        ro = None if resooff is None else np.ascontiguousarray(resooff, dtype=np.uint8)
+        o = dict(trk=np.empty(rows), tas=np.empty(rows), vs=np.empty(rows),
+                 asase=np.empty(rows, np.float32), asasn=np.empty(rows, np.float32))
+        self.check(self.lib.bsa_mvp(self.h, ctypes.byref(params), *[ptr(a) for a in ins],
+                                    ptr(nr, _c_u8p), ptr(ro, _c_u8p), ptr(asas_alt), ptr(o['trk']),
+                                    ptr(o['tas']), ptr(o['vs']), ptr(o['asase'], _c_fp),
+                                    ptr(o['asasn'], _c_fp)), 'bsa_mvp')
+        return o
+
+    # ---------------------------------------------------------------- kinematics
+    KIN_OUT = ('ax', 'delspd', 'cas', 'mach', 'gsnorth', 'gseast', 'gs', 'trk', 'coslat', 'az')
+
+    def kinematics(self, simdt, state, inputs, winddim=0, windnorth=0.0, windeast=0.0):
+        """bsa_kinematics.  ``state``: dict of float64 arrays tas, hdg, alt, vs,
+        lat, lon (updated in place); ``inputs``: ptas, phdg, palt, pvs, bank,
+        eps, accel.  Returns the output dict (incl. swhdgsel/swaltsel bool)."""
+        n = len(state['tas'])
+        io = KinIO()
+        keep = []
+        for k in ('ptas', 'phdg', 'palt', 'pvs', 'bank', 'eps', 'accel'):
+            a = f64(inputs[k])
+            keep.append(a)
+            setattr(io, k, ptr(a))
+        for k in ('tas', 'hdg', 'alt', 'vs', 'lat', 'lon'):
+            a = state[k]
+            if a.dtype != np.float64 or not a.flags.c_contiguous or len(a) != n:
+                raise ValueError('state %s must be a contiguous float64 array' % k)
+            setattr(io, k, ptr(a))
+        out = {k: np.empty(n) for k in self.KIN_OUT}
+        for k in self.KIN_OUT:
+            setattr(io, k, ptr(out[k]))
+        sw = {k: np.empty(n, np.uint8) for k in ('swhdgsel', 'swaltsel')}
+        io.swhdgsel = ptr(sw['swhdgsel'], _c_u8p)
+        io.swaltsel = ptr(sw['swaltsel'], _c_u8p)
+        self.check(self.lib.bsa_kinematics(self.h, n, float(simdt), int(winddim), float(windnorth),
+                                           float(windeast), ctypes.byref(io)), 'bsa_kinematics')
+        out.update({k: v.astype(bool) for k, v in sw.items()})
+        return out
+
+
+_default = {}
+
+
+def default_context(device=0):
+    """Process-wide lazily created context per device (like the sim's single bs.traf)."""
+    ctx = _default.get(device)
+    if ctx is None:
+        ctx = _default[device] = Context(device)
+    return ctx

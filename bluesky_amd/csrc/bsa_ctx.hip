@@ -1,0 +1,239 @@
+// Context, device buffers, state upload and the C ABI entry points of
+// include/bsaccel.h.  No exception crosses the ABI: every entry point
+// returns a status and keeps its message in the context.
+#include <cstdarg>
+#include <new>
+
+#include "bsa_internal.h"
+
+namespace bsa {
+
+static thread_local std::string g_create_error;
+
+int fail(Ctx *c, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf; else g_create_error = buf;
+  return -1;
+}
+
+bool ensure(Ctx *c, DevBuf &b, size_t bytes, const char *what) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return true;
+  if (b.p) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      fail(c, "sync before realloc of %s: %s", what, hipGetErrorString(e));
+      return false;
+    }
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  // round up to 2 MiB to limit reallocation churn
+  size_t rounded = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+  hipError_t e = hipMalloc(&b.p, rounded);
+  if (e != hipSuccess) {
+    b.p = nullptr;
+    fail(c, "hipMalloc(%zu) for %s failed: %s", rounded, what, hipGetErrorString(e));
+    return false;
+  }
+  b.bytes = rounded;
+  return true;
+}
+
+void release(DevBuf &b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+static int upload6(Ctx *c, DevBuf *dst, int64_t n, const double *const src[6]) {
+  static const char *names[6] = {"lat", "lon", "trk", "gs", "alt", "vs"};
+  for (int k = 0; k < 6; ++k) {
+    if (!src[k]) return fail(c, "NULL %s array", names[k]);
+    if (!ensure(c, dst[k], (size_t)n * 8, names[k])) return -1;
+    if (n) BSA_HIP(c, hipMemcpyAsync(dst[k].p, src[k], (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  return 0;
+}
+
+}  // namespace bsa
+
+using bsa::Ctx;
+
+struct bsa_ctx : Ctx {};
+
+extern "C" {
+
+int bsa_abi_version(void) { return BSA_ABI_VERSION; }
+
+int bsa_device_count(void) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e == hipErrorNoDevice) return 0;
+  if (e != hipSuccess) return -1;
+  return n;
+}
+
+bsa_ctx *bsa_create(int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    bsa::fail(nullptr, "no HIP device available (%s)", hipGetErrorString(e));
+    return nullptr;
+  }
+  if (device < 0 || device >= n) {
+    bsa::fail(nullptr, "device %d out of range [0, %d)", device, n);
+    return nullptr;
+  }
+  e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    bsa::fail(nullptr, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    return nullptr;
+  }
+  bsa_ctx *c = new (std::nothrow) bsa_ctx();
+  if (!c) {
+    bsa::fail(nullptr, "out of host memory");
+    return nullptr;
+  }
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    bsa::fail(nullptr, "hipStreamCreate: %s", hipGetErrorString(e));
+    delete c;
+    return nullptr;
+  }
+  for (int k = 0; k < 5; ++k) {
+    e = hipEventCreate(&c->ev[k]);
+    if (e != hipSuccess) {
+      bsa::fail(nullptr, "hipEventCreate: %s", hipGetErrorString(e));
+      delete c;
+      return nullptr;
+    }
+  }
+  return c;
+}
+
+void bsa_destroy(bsa_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  bsa::DevBuf *all[] = {&c->rowrec, &c->colrec, &c->pfrow, &c->pfcol, &c->counters, &c->cand,
+                        &c->ckey, &c->cval, &c->ckey2, &c->cval2, &c->cpay, &c->lkey, &c->lkey2,
+                        &c->out_ci, &c->out_cj, &c->out_li, &c->out_lj, &c->out_pay, &c->inconf,
+                        &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage};
+  for (auto *b : all) bsa::release(*b);
+  for (int k = 0; k < 6; ++k) {
+    bsa::release(c->own[k]);
+    bsa::release(c->intr[k]);
+  }
+  for (int k = 0; k < 5; ++k)
+    if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char *bsa_last_error(const bsa_ctx *c) {
+  return c ? c->err.c_str() : bsa::g_create_error.c_str();
+}
+
+int bsa_sync(bsa_ctx *c) {
+  if (!c) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int bsa_set_state(bsa_ctx *c, int64_t n, const double *lat, const double *lon, const double *trk,
+                  const double *gs, const double *alt, const double *vs) {
+  if (!c) return -1;
+  if (n < 0) return bsa::fail(c, "negative n");
+  BSA_HIP(c, hipSetDevice(c->device));
+  const double *src[6] = {lat, lon, trk, gs, alt, vs};
+  if (n == 0) {
+    c->n = 0;
+    c->has_intruder = false;
+    c->have_pairs = false;
+    return 0;
+  }
+  if (bsa::upload6(c, c->own, n, src)) return -1;
+  c->n = n;
+  c->has_intruder = false;
+  c->have_pairs = false;
+  return 0;
+}
+
+int bsa_set_intruder(bsa_ctx *c, int64_t n, const double *lat, const double *lon, const double *trk,
+                     const double *gs, const double *alt, const double *vs) {
+  if (!c) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (n == 0) {
+    c->has_intruder = false;
+    return 0;
+  }
+  if (n != c->n) return bsa::fail(c, "intruder n=%lld != ownship n=%lld", (long long)n, (long long)c->n);
+  const double *src[6] = {lat, lon, trk, gs, alt, vs};
+  if (bsa::upload6(c, c->intr, n, src)) return -1;
+  c->has_intruder = true;
+  c->have_pairs = false;
+  return 0;
+}
+
+int bsa_detect(bsa_ctx *c, double rpz, double hpz, double tla, int flags, int64_t row_begin,
+               int64_t row_end, int64_t *n_conf, int64_t *n_los) {
+  if (!c) return -1;
+  if (!n_conf || !n_los) return bsa::fail(c, "NULL count pointer");
+  BSA_HIP(c, hipSetDevice(c->device));
+  return bsa::detect(c, rpz, hpz, tla, flags, row_begin, row_end, n_conf, n_los);
+}
+
+int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *dist, double *tcpa,
+                    double *tinconf, double *dcpa, int32_t *li, int32_t *lj, uint8_t *inconf,
+                    double *tcpamax) {
+  if (!c) return -1;
+  if (!c->have_pairs) return bsa::fail(c, "no detect results to fetch");
+  BSA_HIP(c, hipSetDevice(c->device));
+  const int64_t P = c->last_conf, L = c->last_los, R = c->last_re - c->last_rb;
+  auto cp = [&](void *dst, const void *src, size_t bytes) -> int {
+    if (dst && bytes) BSA_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  };
+  const double *pay = (const double *)c->out_pay.p;
+  if (cp(ci, c->out_ci.p, P * 4) || cp(cj, c->out_cj.p, P * 4) || cp(qdr, pay + 0 * P, P * 8) ||
+      cp(dist, pay + 1 * P, P * 8) || cp(tcpa, pay + 2 * P, P * 8) || cp(tinconf, pay + 3 * P, P * 8) ||
+      cp(li, c->out_li.p, L * 4) || cp(lj, c->out_lj.p, L * 4) || cp(inconf, c->inconf.p, R) ||
+      cp(tcpamax, c->tcpamax.p, R * 8))
+    return -1;
+  if (dcpa) {
+    if (!(c->last_flags & BSA_FLAG_WITH_DCPA)) return bsa::fail(c, "dcpa requested without BSA_FLAG_WITH_DCPA");
+    if (cp(dcpa, pay + 4 * P, P * 8)) return -1;
+  }
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int bsa_last_candidates(bsa_ctx *c, int64_t *n_candidates) {
+  if (!c || !n_candidates) return -1;
+  *n_candidates = c->last_cand;
+  return 0;
+}
+
+int bsa_last_timings(bsa_ctx *c, double *ms5) {
+  if (!c || !ms5) return -1;
+  if (!c->ev_valid) return bsa::fail(c, "no timed detect yet");
+  BSA_HIP(c, hipEventSynchronize(c->ev[4]));
+  float t;
+  for (int k = 0; k < 4; ++k) {
+    BSA_HIP(c, hipEventElapsedTime(&t, c->ev[k], c->ev[k + 1]));
+    ms5[k] = t;
+  }
+  BSA_HIP(c, hipEventElapsedTime(&t, c->ev[0], c->ev[4]));
+  ms5[4] = t;
+  return 0;
+}
+
+}  // extern "C"

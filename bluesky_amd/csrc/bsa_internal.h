@@ -1,0 +1,157 @@
+// Internal runtime of libbsaccel: context, device buffers, error plumbing.
+// gfx950 (MI355X) only; compiled with -ffp-contract=off so every fp64
+// expression rounds exactly like numpy's (one rounding per operation).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/bsaccel.h"
+
+namespace bsa {
+
+// ---------------------------------------------------------------- constants
+// bluesky/tools/aero.py:11-28, bluesky/tools/geo.py:7,38-39
+constexpr double kNM = 1852.0;
+constexpr double kFT = 0.3048;
+constexpr double kKTS = 0.514444;
+constexpr double kWGS84_A = 6378137.0;
+constexpr double kWGS84_B = 6356752.314245;
+constexpr double kPI = 3.14159265358979323846;  // NPY_PI
+constexpr double kD2R = kPI / 180.0;            // numpy deg2rad / radians factor
+constexpr double kR2D = 180.0 / kPI;            // numpy rad2deg / degrees factor
+
+// ---------------------------------------------------------------- records
+// Per-index fp64 records gathered by the exact pair kernel (128 B = one
+// cache line each).  Orientation follows StateBasedCD.py: for pair (i, j)
+// the geometry row is ownship i and the column is intruder j, while the
+// velocity / altitude differences are own[j] - intruder[i]
+// (StateBasedCD.py:39-40,65-69).  So the ROW record i carries own[i]'s
+// position and intruder[i]'s velocity; the COLUMN record j carries
+// intruder[j]'s position and own[j]'s velocity.
+struct alignas(16) RowRec {
+  double lat, lon;        // own[i] [deg]
+  double sinlat, coslat;  // sin/cos(radians(own.lat[i]))          geo.py:137-140
+  double hemA;            // |lat| * (rwgs84(lat) + a)              geo.py:127
+  double u, v;            // int.gs[i] * sin/cos(radians(int.trk[i]))  StateBasedCD.py:35-37
+  double alt, vs;         // int.alt[i], int.vs[i]
+  double pad[7];
+};
+struct alignas(16) ColRec {
+  double lat, lon;        // int[j]
+  double sinlat, coslat;
+  double hemA;
+  double u, v;            // own.gs[j] * sin/cos(radians(own.trk[j]))  StateBasedCD.py:30-32
+  double alt, vs;         // own.alt[j], own.vs[j]
+  double eps;             // (own.lat[j] == 0.) * 1e-6                geo.py:128
+  double pad[6];
+};
+static_assert(sizeof(RowRec) == 128, "RowRec must be one cache line");
+static_assert(sizeof(ColRec) == 128, "ColRec must be one cache line");
+
+// fp32 prefilter record (32 B): unit-sphere position + conservative
+// horizontal / vertical reach terms (see DESIGN.md "exact-safe prefilter").
+struct alignas(16) PFRec {
+  float x, y, z;   // unit vector of the position
+  float s;         // horizontal reach, chord units (half of the pair bound)
+  float alt;       // altitude [m]
+  float h;         // vertical reach [m] (half of the pair bound)
+  float pad0, pad1;
+};
+static_assert(sizeof(PFRec) == 32, "PFRec must be 32 B");
+
+// counters block on the device (one cache line)
+struct Counters {
+  unsigned long long cand;
+  unsigned long long conf;
+  unsigned long long los;
+  unsigned long long pad[5];
+};
+
+// ---------------------------------------------------------------- buffers
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+
+struct Ctx;
+bool ensure(Ctx *c, DevBuf &b, size_t bytes, const char *what);
+void release(DevBuf &b);
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // state
+  int64_t n = 0;
+  bool has_intruder = false;
+  DevBuf own[6];   // lat lon trk gs alt vs
+  DevBuf intr[6];
+  DevBuf rowrec, colrec, pfrow, pfcol;
+
+  // detect buffers
+  DevBuf counters;           // Counters
+  DevBuf cand;               // uint2 (i, j)
+  unsigned long long cand_cap = 0;
+  DevBuf ckey, cval, ckey2, cval2;  // conflict keys / slot ids (+ sorted)
+  DevBuf cpay;               // 5 x cap doubles: qdr dist tcpa tin dcpa (slot order)
+  unsigned long long conf_cap = 0;
+  DevBuf lkey, lkey2;        // LoS keys (+ sorted)
+  unsigned long long los_cap = 0;
+  DevBuf out_ci, out_cj, out_li, out_lj;  // int32 sorted
+  DevBuf out_pay;            // 5 x n_conf doubles, sorted
+  DevBuf inconf, tcpamax;    // per row of the last detect
+  DevBuf sort_tmp;
+
+  // last detect
+  int64_t last_rb = 0, last_re = 0;
+  int64_t last_conf = 0, last_los = 0, last_cand = 0;
+  int last_flags = 0;
+  bool have_pairs = false;
+
+  hipEvent_t ev[5] = {};
+  bool ev_valid = false;
+
+  // MVP / kinematics staging (host-buffer entry points)
+  DevBuf seg, mvp_stage, kin_stage;
+};
+
+// device pointers for the MVP kernel (full-N traffic arrays, per-row outputs)
+struct MvpDev {
+  const double *gseast, *gsnorth, *vs, *alt, *trk, *gs, *selalt, *apvs;
+  const uint8_t *noreso, *resooff;
+  double *asas_alt, *o_trk, *o_tas, *o_vs;
+  float *o_asase, *o_asasn;
+  double *o_tsolv;
+};
+int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d);
+
+// device pointers for the fused kinematics kernel
+struct KinDev {
+  const double *ptas, *phdg, *palt, *pvs, *bank, *eps, *accel;
+  double *tas, *hdg, *alt, *vs, *lat, *lon;
+  double *ax, *delspd, *cas, *mach, *gsnorth, *gseast, *gs, *trk, *coslat, *az;
+  uint8_t *swhdgsel, *swaltsel;
+};
+int kin_device(Ctx *c, int64_t n, double simdt, int winddim, double vn, double ve, const KinDev &d);
+
+// error helpers
+int fail(Ctx *c, const char *fmt, ...);
+#define BSA_HIP(c, call)                                                              \
+  do {                                                                                \
+    hipError_t e_ = (call);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return ::bsa::fail((c), "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                         __FILE__, __LINE__);                                         \
+  } while (0)
+
+// detect entry (bsa_cd.hip)
+int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
+           int64_t *n_conf, int64_t *n_los);
+int prep_records(Ctx *c, double rpz, double hpz, double tla);
+
+}  // namespace bsa

@@ -1,0 +1,117 @@
+"""GPU parity: bsa_detect (HIP, gfx950) against the reference's golden vectors
+and the oracle restatement; exact pair sets, reals within 1e-9 relative."""
+import numpy as np
+import pytest
+
+from bluesky_amd import statebased, synth
+from oracle import statebased as ocd
+from tests import util
+
+pytestmark = pytest.mark.gpu
+
+CD = util.golden('cd_*.npz')
+RPZ, HPZ, TLA = synth.RPZ, synth.HPZ, synth.TLOOKAHEAD
+
+
+@pytest.mark.parametrize('path', CD, ids=[util.case_name(p) for p in CD])
+def test_detect_matches_reference_golden(ctx, path):
+    own, intr, z = util.load_cd(path)
+    got = statebased.detect_indices(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']), ctx=ctx)
+    util.assert_detect_equal(got, z, float(z['rpz']), float(z['tla']))
+
+
+@pytest.mark.parametrize('path', CD, ids=[util.case_name(p) for p in CD])
+def test_prefilter_is_exact_safe_on_golden(ctx, path):
+    """Pruned and unpruned (every pair evaluated) runs give identical results."""
+    own, intr, z = util.load_cd(path)
+    a = statebased.detect_indices(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']), ctx=ctx)
+    b = statebased.detect_indices(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']),
+                                  ctx=ctx, noprune=True)
+    for k in a:
+        if a[k] is not None:
+            assert np.array_equal(a[k], b[k]), k
+
+
+def test_tuple_contract(ctx):
+    own, intr, z = util.load_cd(util.golden('cd_box500.npz')[0])
+    res = statebased.detect(own, own, RPZ, HPZ, TLA)
+    assert len(res) == 8
+    confpairs, lospairs, inconf, tcpamax, qdr, dist, tcpa, tin = res
+    assert isinstance(confpairs, list) and isinstance(confpairs[0], tuple)
+    assert confpairs == [(own.id[i], own.id[j]) for i, j in zip(z['ci'], z['cj'])]
+    assert lospairs == [(own.id[i], own.id[j]) for i, j in zip(z['li'], z['lj'])]
+    assert inconf.dtype == bool and inconf.shape == (own.ntraf,)
+    res9 = statebased.detect(own, own, RPZ, HPZ, TLA, with_dcpa=True)
+    assert len(res9) == 9 and len(res9[6]) == len(confpairs)
+    ref = ocd.detect_arrays(own, own, RPZ, HPZ, TLA, want_dcpa=True)
+    ok, msg = util.close(res9[6], ref['dcpa'], RPZ)
+    assert ok, msg
+
+
+@pytest.mark.parametrize('n', [0, 1, 2, 3, 63, 64, 65, 511, 512, 513, 1025])
+def test_ragged_sizes(ctx, n):
+    t = synth.box(n, 20.0 + n / 10.0, seed=100 + n)
+    got = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx)
+    if n == 0:   # the reference's np.max over an empty axis raises; the GPU returns empties
+        assert all(len(v) == 0 for v in got.values() if v is not None)
+        return
+    exp = ocd.detect_arrays(t, t, RPZ, HPZ, TLA)
+    util.assert_detect_equal(got, exp, RPZ, TLA)
+
+
+@pytest.mark.parametrize('seed,n,L', [(7, 4000, 500.0), (11, 3000, 120.0), (13, 2500, 40.0)])
+def test_random_boxes_vs_oracle(ctx, seed, n, L):
+    t = synth.box(n, L, seed=seed)
+    got = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx)
+    exp = ocd.detect_arrays(t, t, RPZ, HPZ, TLA)
+    util.assert_detect_equal(got, exp, RPZ, TLA)
+
+
+def test_global_vs_oracle(ctx):
+    t = synth.global_traffic(4000, seed=3)
+    got = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx)
+    exp = ocd.detect_arrays(t, t, RPZ, HPZ, TLA)
+    util.assert_detect_equal(got, exp, RPZ, TLA)
+
+
+def test_row_range_is_a_slice(ctx):
+    t = synth.box(3000, 150.0, seed=5)
+    full = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx)
+    parts = [statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx, row_begin=a, row_end=b)
+             for a, b in ((0, 1000), (1000, 1001), (1001, 3000))]
+    for k in ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'li', 'lj', 'inconf', 'tcpamax'):
+        assert np.array_equal(np.concatenate([p[k] for p in parts]), full[k]), k
+
+
+def test_other_lookahead_and_zones(ctx):
+    t = synth.box(2000, 100.0, seed=17)
+    for rpz, hpz, tla in ((3 * 1852.0, 600.0, 120.0), (8 * 1852.0, 1000 * 0.3048, 600.0),
+                          (5 * 1852.0, 304.8, 0.0), (5 * 1852.0, 304.8, -10.0)):
+        got = statebased.detect_indices(t, t, rpz, hpz, tla, ctx=ctx)
+        exp = ocd.detect_arrays(t, t, rpz, hpz, tla)
+        util.assert_detect_equal(got, exp, rpz, max(tla, 1.0))
+
+
+@pytest.mark.slow
+def test_full_size_100k_row_sample(ctx):
+    """BASELINE size (100k, density-matched box): every GPU pair of 48 sampled
+    rows equals the oracle over all 100k columns; the output is sorted and
+    consistent with inconf."""
+    t = synth.workload('box100k')
+    got = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx)
+    key = got['ci'].astype(np.int64) * t.ntraf + got['cj']
+    assert np.all(np.diff(key) > 0)
+    lkey = got['li'].astype(np.int64) * t.ntraf + got['lj']
+    assert np.all(np.diff(lkey) > 0)
+    assert np.array_equal(np.unique(got['ci']), np.flatnonzero(got['inconf']))
+    rows = np.random.default_rng(1).choice(t.ntraf, 48, replace=False)
+    rows.sort()
+    exp = ocd.detect_arrays(t, t, RPZ, HPZ, TLA, rows=rows, budget_bytes=512 << 20)
+    sel = np.isin(got['ci'], rows)
+    lsel = np.isin(got['li'], rows)
+    sub = dict(ci=got['ci'][sel], cj=got['cj'][sel], li=got['li'][lsel], lj=got['lj'][lsel],
+               qdr=got['qdr'][sel], dist=got['dist'][sel], tcpa=got['tcpa'][sel],
+               tinconf=got['tinconf'][sel], inconf=got['inconf'][rows], tcpamax=got['tcpamax'][rows])
+    util.assert_detect_equal(sub, exp, RPZ, TLA)
+    # density-matched box: ~1.4 conflict pairs per aircraft
+    assert 0.5 * t.ntraf < len(got['ci']) < 3.0 * t.ntraf

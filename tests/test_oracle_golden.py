@@ -1,0 +1,91 @@
+"""CPU: the oracle restatement against the reference's golden vectors.
+
+The vectors were captured by running the reference itself (tools/make_golden.py,
+which also asserted bitwise equality at capture time).  Here the check is
+exact for index sets and <= 1e-12 relative for reals, so it also holds on a
+host whose numpy/libm dispatch differs by an ULP from the capture host.
+"""
+import numpy as np
+import pytest
+
+from oracle import kinematics as okin
+from oracle import mvp as omvp
+from oracle import statebased as ocd
+from tests import util
+
+CD = util.golden('cd_*.npz')
+MVP = util.golden('mvp_*.npz')
+KIN = util.golden('kin_*.npz')
+
+
+def test_fixtures_present():
+    assert len(CD) >= 9 and len(MVP) >= 5 and len(KIN) >= 3
+
+
+@pytest.mark.parametrize('path', CD, ids=[util.case_name(p) for p in CD])
+def test_oracle_detect_matches_reference(path):
+    own, intr, z = util.load_cd(path)
+    o = ocd.detect_arrays(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']),
+                          budget_bytes=256 << 20)
+    for k in ('ci', 'cj', 'li', 'lj'):
+        assert np.array_equal(o[k], z[k]), k
+    assert np.array_equal(o['inconf'], z['inconf'])
+    for k, s in (('qdr', 360.0), ('dist', 1e4), ('tcpa', 300.0), ('tinconf', 300.0),
+                 ('tcpamax', 300.0)):
+        ok, msg = util.close(o[k], z[k], s, rtol=1e-12)
+        assert ok, '%s: %s' % (k, msg)
+
+
+def test_oracle_tuple_contract():
+    own, intr, z = util.load_cd(util.golden('cd_box64.npz')[0])
+    res = ocd.detect(own.as_dict(), own.as_dict(), float(z['rpz']), float(z['hpz']), float(z['tla']))
+    assert len(res) == 8
+    confpairs, lospairs = res[0], res[1]
+    assert confpairs and isinstance(confpairs[0], tuple) and isinstance(confpairs[0][0], str)
+    assert [(own.id.index(a), own.id.index(b)) for a, b in confpairs] == list(zip(z['ci'], z['cj']))
+
+
+MODES = ['default', 'spd', 'hdg', 'vert', 'hv', 'ff1', 'ff2', 'ff3', 'lay1', 'lay2', 'noreso', 'resooff']
+MODE_SW = {
+    'default': (True, False, False, False, False, 'FF1'), 'spd': (True, True, False, False, False, 'FF1'),
+    'hdg': (True, False, True, False, False, 'FF1'), 'vert': (False, False, False, True, False, 'FF1'),
+    'hv': (False, False, False, False, False, 'FF1'), 'ff1': (False, False, False, False, True, 'FF1'),
+    'ff2': (False, False, False, False, True, 'FF2'), 'ff3': (False, False, False, False, True, 'FF3'),
+    'lay1': (False, False, False, False, True, 'LAY1'), 'lay2': (False, False, False, False, True, 'LAY2'),
+    'noreso': (False, False, False, False, False, 'FF1'), 'resooff': (False, False, False, False, False, 'FF1'),
+}
+
+
+def mvp_args(z, mode):
+    n = len(z['alt'])
+    p = omvp.params_from_settings(float(z['rpz']), float(z['hpz']), float(z['tla']), float(z['mar']),
+                                  *MODE_SW[mode])
+    noreso = np.isin(np.arange(n), z['noreso_idx']) if mode == 'noreso' else None
+    resooff = np.isin(np.arange(n), z['resooff_idx']) if mode == 'resooff' else None
+    return p, noreso, resooff
+
+
+@pytest.mark.parametrize('path', MVP, ids=[util.case_name(p) for p in MVP])
+def test_oracle_mvp_matches_reference(path):
+    z = dict(np.load(path, allow_pickle=False))
+    for mode in MODES:
+        p, noreso, resooff = mvp_args(z, mode)
+        o = omvp.resolve_arrays(z['ci'], z['cj'], z['qdr'], z['dist'], z['tcpa'], z['tLOS'],
+                                z['gseast'], z['gsnorth'], z['vs'], z['alt'], z['trk'], z['gs'],
+                                z['selalt'], z['apvs'], z['asasalt'].copy(), p, noreso, resooff)
+        for k in ('trk', 'tas', 'vs', 'alt', 'asase', 'asasn'):
+            ok, msg = util.close(o[k], z['%s__%s' % (mode, k)], 1.0, rtol=1e-12)
+            assert ok, '%s/%s: %s' % (mode, k, msg)
+
+
+@pytest.mark.parametrize('path', KIN, ids=[util.case_name(p) for p in KIN])
+def test_oracle_kinematics_matches_reference(path):
+    z = dict(np.load(path, allow_pickle=False))
+    s = {k: z[k] for k in ('lat', 'lon', 'alt', 'tas', 'hdg', 'vs', 'ptas', 'phdg', 'palt', 'pvs',
+                           'bank', 'eps', 'accel')}
+    o = okin.step(s, float(z['dt']), int(z['winddim']), float(z['windnorth']), float(z['windeast']))
+    for k in ('ax', 'delspd', 'tas', 'cas', 'M', 'hdg', 'swhdgsel', 'swaltsel', 'az', 'vs',
+              'gsnorth', 'gseast', 'gs', 'trk', 'alt', 'lat', 'lon', 'coslat'):
+        ok, msg = util.close(np.asarray(o[k], dtype=np.float64),
+                             np.asarray(z['out_' + k], dtype=np.float64), 1.0, rtol=1e-12)
+        assert ok, '%s: %s' % (k, msg)
