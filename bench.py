@@ -87,9 +87,9 @@ def main():
                            rpz_m=synth.RPZ, hpz_m=synth.HPZ, tlookahead_s=synth.TLOOKAHEAD,
                            parallelism='dp%d-rows' % args.gpus),
                roofline=roof,
-               kernels_ms=dict(prep=np.mean([m['prep'] for m in ms]), prefilter=pf * 1e3,
+               kernels_ms=dict(order_prep_cull=np.mean([m['prep'] for m in ms]), prefilter=pf * 1e3,
                                exact=ex * 1e3, sort=np.mean([m['sort'] for m in ms])),
-               n_conf=nc, n_los=nl, n_candidates=ncand,
+               n_conf=nc, n_los=nl, n_candidates=ncand, tile_pairs=ctx.last_tiles(),
                exact_fp64=dict(achieved_tflops=ncand * OPS_PER_PAIR / ex / 1e12 if ex > 0 else None,
                                peak=FP64_PEAK_TFLOPS),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12))

@@ -1,23 +1,28 @@
-// K0 prep, K1a prefilter, K1b exact pair evaluation, K2 canonical sort.
+// StateBased conflict detection for gfx950:
+//   StateBasedCD.detect (bluesky/traffic/asas/StateBasedCD.py:7-103) with
+//   geo.qdrdist_matrix (bluesky/tools/geo.py:110-162) fused in.
 //
-// StateBasedCD.detect (bluesky/traffic/asas/StateBasedCD.py:7-103) with
-// geo.qdrdist_matrix (bluesky/tools/geo.py:110-162) fused in, for gfx950.
-//
-// Structure:
-//   K0 prep        one thread per aircraft: per-index fp64 records (the
-//                  per-aircraft factors of the reference's N x N broadcasts)
-//                  and fp32 prefilter records.
-//   K1a prefilter  N-body tiled sweep over all (i, j): lane = ownship row
-//                  (2 rows per lane), intruder tiles in LDS, broadcast reads.
-//                  A conservative fp32 bound keeps every pair that could be a
-//                  conflict or a loss of separation (proof in DESIGN.md);
-//                  survivors are compacted through a per-wave LDS queue with
-//                  ballot/mbcnt and one atomic per flush.
+// Pipeline, all on one stream, one host sync:
+//   K0a keys       Morton code of each position's unit vector (rows = own,
+//                  columns = intruder), then hipcub radix sort -> spatial order.
+//   K0b prep       per sorted index: fp64 records (the per-aircraft factors of
+//                  the reference's N x N broadcasts) + fp32 prefilter records.
+//   K0c tilebox    bounds of every 512-row block / 512-column tile.
+//   K0d tilepairs  (row block, column tile) pairs whose bounds can contain a
+//                  kept pair; all others are skipped without touching a pair.
+//   K1a prefilter  N-body sweep of the surviving tile pairs: lane = ownship
+//                  row (2 per lane), column tile in LDS (broadcast reads);
+//                  stage 1 conservative reach test, stage 2 conservative
+//                  fp32 closest-approach refine (exact-safe proofs);
+//                  survivors compacted per wave (ballot/mbcnt, 1 atomic/flush).
 //   K1b exact      one lane per candidate: the reference's fp64 expression
-//                  sequence, op for op (-ffp-contract=off), conflict / LoS
-//                  outputs appended with one atomic per wave.
-//   K2 sort        hipcub radix sort on key = (i << 32 | j), i.e. the
-//                  reference's row-major np.where order, then a gather.
+//                  sequence op for op (-ffp-contract=off), outputs appended
+//                  with one atomic per wave.
+//   K2  sort       radix sort on (i << 32 | j) = the reference's row-major
+//                  np.where order, then a gather.
+// Neither the spatial order nor the culling changes any result: every stage
+// before K1b only removes pairs that provably cannot be a conflict or a loss
+// of separation, and K1b evaluates the survivors exactly.
 #include <hipcub/hipcub.hpp>
 
 #include "bsa_internal.h"
@@ -52,131 +57,362 @@ __device__ __forceinline__ double rwgs84(double latd) {
   return sqrt((anan + bnbn) / (adad + bdbd));
 }
 
-// ------------------------------------------------------------------ K0 prep
+// ------------------------------------------------------------------ K0a keys
+__device__ __forceinline__ unsigned expand10(unsigned v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+__device__ __forceinline__ unsigned morton_latlon(double latd, double lond) {
+  const double la = latd * kD2R, lo = lond * kD2R;
+  const double cl = cos(la);
+  const double p[3] = {cl * cos(lo), cl * sin(lo), sin(la)};
+  unsigned key = 0;
+  for (int k = 0; k < 3; ++k) {
+    if (!(p[k] == p[k]) || isinf(p[k])) return 0xffffffffu;
+    int q = (int)((p[k] + 1.0) * 512.0);
+    q = q < 0 ? 0 : (q > 1023 ? 1023 : q);
+    key |= expand10((unsigned)q) << (2 - k);
+  }
+  return key;
+}
+
+__global__ __launch_bounds__(256) void k_keys(int cnt, int base, const double *__restrict__ lat,
+                                              const double *__restrict__ lon,
+                                              unsigned *__restrict__ key,
+                                              unsigned *__restrict__ idx) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= cnt) return;
+  const int o = base + k;
+  key[k] = morton_latlon(lat[o], lon[o]);
+  idx[k] = (unsigned)o;
+}
+
+// ------------------------------------------------------------------ K0b prep
 __device__ __forceinline__ float reach_h(double rpz, double gs, double tlap) {
-  // horizontal half-bound in unit-sphere chord units: the pair keeps iff
-  // chord < s_i + s_j, s = ((R/2 + (|gs| + 0.5e-3) tla)(1 + 1e-5)) / 6.3e6 + 1e-6
-  double s = ((0.5 * rpz + (fabs(gs) + 0.5e-3) * tlap) * (1.0 + 1e-5)) / 6.3e6 + 1e-6;
+  // horizontal half-bound in unit-sphere chord units: a pair is kept iff
+  // chord < s_i + s_j,  s = ((R/2 + (|gs| + 0.5e-3) tla)(1 + 1e-5)) / 6.3e6 + 1e-6
+  const double s = ((0.5 * rpz + (fabs(gs) + 0.5e-3) * tlap) * (1.0 + 1e-5)) / 6.3e6 + 1e-6;
   return isfinite(s) ? (float)s : INFINITY;
 }
 __device__ __forceinline__ float reach_v(double hpz, double vs, double alt, double tlap) {
-  double h = (0.5 * hpz + (fabs(vs) + 0.5e-6) * tlap) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(alt);
+  const double h = (0.5 * hpz + (fabs(vs) + 0.5e-6) * tlap) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(alt);
   return isfinite(h) ? (float)h : INFINITY;
 }
 
-__global__ __launch_bounds__(256) void k_prep(
-    int n, const double *__restrict__ olat, const double *__restrict__ olon,
-    const double *__restrict__ otrk, const double *__restrict__ ogs,
-    const double *__restrict__ oalt, const double *__restrict__ ovs,
-    const double *__restrict__ ilat, const double *__restrict__ ilon,
-    const double *__restrict__ itrk, const double *__restrict__ igs,
-    const double *__restrict__ ialt, const double *__restrict__ ivs, int distinct,
-    double rpz, double hpz, double tla, RowRec *__restrict__ R, ColRec *__restrict__ C,
-    PFRec *__restrict__ PR, PFRec *__restrict__ PC) {
+struct SoA6 {
+  const double *lat, *lon, *trk, *gs, *alt, *vs;
+};
+
+// Row records, sorted position k -> original row perm[k]: own[i] geometry,
+// intruder[i] velocity / altitude (StateBasedCD.py:39-40,65-69 orientation).
+__global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__restrict__ perm,
+                                                   SoA6 own, SoA6 intr, double rpz, double hpz,
+                                                   double tla, RowRec *__restrict__ R,
+                                                   PFRec *__restrict__ PR, PFAux *__restrict__ PA) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const double a = kWGS84_A;
+  if (k >= cnt) return;
+  const int o = (int)perm[k];
   const double tlap = tla > 0.0 ? tla : 0.0;
-
-  // ownship k: row geometry, column velocity
-  const double la_o = olat[k], lo_o = olon[k];
-  const double rad_o = la_o * kD2R;
-  const double sin_o = sin(rad_o), cos_o = cos(rad_o);
-  const double trk_o = otrk[k] * kD2R;
-  const double u_o = ogs[k] * sin(trk_o), v_o = ogs[k] * cos(trk_o);
-  // intruder k: column geometry, row velocity
-  double la_i = la_o, lo_i = lo_o, sin_i = sin_o, cos_i = cos_o, u_i = u_o, v_i = v_o;
-  double alt_i = oalt[k], vs_i = ovs[k], gs_i = ogs[k];
-  if (distinct) {
-    la_i = ilat[k];
-    lo_i = ilon[k];
-    const double rad_i = la_i * kD2R;
-    sin_i = sin(rad_i);
-    cos_i = cos(rad_i);
-    const double trk_i = itrk[k] * kD2R;
-    gs_i = igs[k];
-    u_i = gs_i * sin(trk_i);
-    v_i = gs_i * cos(trk_i);
-    alt_i = ialt[k];
-    vs_i = ivs[k];
-  }
-
+  const double la = own.lat[o], lo = own.lon[o];
+  const double rad = la * kD2R;
+  const double sinl = sin(rad), cosl = cos(rad);
+  const double trk = intr.trk[o] * kD2R;
+  const double gs = intr.gs[o];
   RowRec r;
-  r.lat = la_o;
-  r.lon = lo_o;
-  r.sinlat = sin_o;
-  r.coslat = cos_o;
-  r.hemA = fabs(la_o) * (rwgs84(la_o) + a);
-  r.u = u_i;
-  r.v = v_i;
-  r.alt = alt_i;
-  r.vs = vs_i;
+  r.lat = la;
+  r.lon = lo;
+  r.sinlat = sinl;
+  r.coslat = cosl;
+  r.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);  // geo.py:127
+  r.u = gs * sin(trk);                           // StateBasedCD.py:36-37
+  r.v = gs * cos(trk);
+  r.alt = intr.alt[o];
+  r.vs = intr.vs[o];
   for (int q = 0; q < 7; ++q) r.pad[q] = 0.0;
   R[k] = r;
+  const double lor = lo * kD2R;
+  PFRec p;
+  p.x = (float)(cosl * cos(lor));
+  p.y = (float)(cosl * sin(lor));
+  p.z = (float)sinl;
+  p.s = reach_h(rpz, gs, tlap);
+  p.alt = (float)r.alt;
+  p.h = reach_v(hpz, r.vs, r.alt, tlap);
+  p.u = (float)r.u;
+  p.v = (float)r.v;
+  PFAux a;
+  a.vs = (float)r.vs;
+  a.flags = 0;
+  if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
+    p.s = INFINITY;
+    a.flags = 1;
+  }
+  PR[k] = p;
+  PA[k] = a;
+}
 
+// Column records: intruder[j] geometry, own[j] velocity / altitude.
+__global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__restrict__ perm,
+                                                   SoA6 own, SoA6 intr, int distinct, double rpz,
+                                                   double hpz, double tla, ColRec *__restrict__ C,
+                                                   PFRec *__restrict__ PC, PFAux *__restrict__ PA) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= cnt) return;
+  const int o = (int)perm[k];
+  const double tlap = tla > 0.0 ? tla : 0.0;
+  const double la = intr.lat[o], lo = intr.lon[o];
+  const double rad = la * kD2R;
+  const double sinl = sin(rad), cosl = cos(rad);
+  const double trk = own.trk[o] * kD2R;
+  const double gs = own.gs[o];
+  const double olat = own.lat[o];
   ColRec c;
-  c.lat = la_i;
-  c.lon = lo_i;
-  c.sinlat = sin_i;
-  c.coslat = cos_i;
-  c.hemA = distinct ? fabs(la_i) * (rwgs84(la_i) + a) : r.hemA;
-  c.u = u_o;
-  c.v = v_o;
-  c.alt = oalt[k];
-  c.vs = ovs[k];
-  c.eps = (la_o == 0.0) ? 0.000001 : 0.0;
+  c.lat = la;
+  c.lon = lo;
+  c.sinlat = sinl;
+  c.coslat = cosl;
+  c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);
+  c.u = gs * sin(trk);                           // StateBasedCD.py:31-32
+  c.v = gs * cos(trk);
+  c.alt = own.alt[o];
+  c.vs = own.vs[o];
+  c.eps = (olat == 0.0) ? 0.000001 : 0.0;       // geo.py:128 (column-indexed)
   for (int q = 0; q < 6; ++q) c.pad[q] = 0.0;
   C[k] = c;
+  const double lor = lo * kD2R;
+  PFRec p;
+  p.x = (float)(cosl * cos(lor));
+  p.y = (float)(cosl * sin(lor));
+  p.z = (float)sinl;
+  p.s = reach_h(rpz, gs, tlap);
+  p.alt = (float)c.alt;
+  p.h = reach_v(hpz, c.vs, c.alt, tlap);
+  p.u = (float)c.u;
+  p.v = (float)c.v;
+  PFAux a;
+  a.vs = (float)c.vs;
+  a.flags = 0;
+  // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
+  // when own != intruder (geo.py:128): never prune or refine such a column.
+  if ((distinct && olat == 0.0) || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
+    p.s = INFINITY;
+    a.flags = 1;
+  }
+  PC[k] = p;
+  PA[k] = a;
+}
 
-  // fp32 prefilter records (accuracy is covered by the margins in reach_*)
-  PFRec pr, pc;
-  const double lon_or = lo_o * kD2R, lon_ir = lo_i * kD2R;
-  pr.x = (float)(cos_o * cos(lon_or));
-  pr.y = (float)(cos_o * sin(lon_or));
-  pr.z = (float)sin_o;
-  pr.s = reach_h(rpz, gs_i, tlap);
-  pr.alt = (float)alt_i;
-  pr.h = reach_v(hpz, vs_i, alt_i, tlap);
-  pr.pad0 = pr.pad1 = 0.f;
-  pc.x = (float)(cos_i * cos(lon_ir));
-  pc.y = (float)(cos_i * sin(lon_ir));
-  pc.z = (float)sin_i;
-  // (own.lat[j] == 0) makes the different-hemisphere radius unbounded below
-  // when own != intruder (geo.py:128): never prune such a column.
-  pc.s = (distinct && la_o == 0.0) ? INFINITY : reach_h(rpz, ogs[k], tlap);
-  pc.alt = (float)oalt[k];
-  pc.h = reach_v(hpz, ovs[k], oalt[k], tlap);
-  pc.pad0 = pc.pad1 = 0.f;
-  if (!(isfinite(pr.x) && isfinite(pr.y) && isfinite(pr.z))) pr.s = INFINITY;
-  if (!(isfinite(pc.x) && isfinite(pc.y) && isfinite(pc.z))) pc.s = INFINITY;
-  PR[k] = pr;
-  PC[k] = pc;
+// ------------------------------------------------------------------ K0c tile boxes
+__device__ __forceinline__ float wmin(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wmax(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// one 256-thread block per tile of kTile consecutive sorted records
+__global__ __launch_bounds__(256) void k_tilebox(int cnt, const PFRec *__restrict__ P,
+                                                 TileBox *__restrict__ box) {
+  __shared__ float red[4][10];
+  const int t = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  float v[10];
+  for (int q = 0; q < 5; ++q) {
+    v[q] = INFINITY;        // minima: x y z alt (+1 spare)
+    v[5 + q] = -INFINITY;   // maxima: x y z alt s/h
+  }
+  float smax = 0.f, hmax = 0.f;
+  const int b0 = t * kTile, b1 = min(cnt, b0 + kTile);
+  for (int k = b0 + tid; k < b1; k += 256) {
+    const PFRec p = P[k];
+    v[0] = fminf(v[0], p.x); v[5] = fmaxf(v[5], p.x);
+    v[1] = fminf(v[1], p.y); v[6] = fmaxf(v[6], p.y);
+    v[2] = fminf(v[2], p.z); v[7] = fmaxf(v[7], p.z);
+    v[3] = fminf(v[3], p.alt); v[8] = fmaxf(v[8], p.alt);
+    smax = fmaxf(smax, p.s == p.s ? p.s : INFINITY);
+    hmax = fmaxf(hmax, p.h == p.h ? p.h : INFINITY);
+  }
+  v[4] = -smax;  // store as minima of negatives
+  v[9] = hmax;
+  for (int q = 0; q < 5; ++q) v[q] = wmin(v[q]);
+  for (int q = 5; q < 10; ++q) v[q] = wmax(v[q]);
+  if (lane == 0)
+    for (int q = 0; q < 10; ++q) red[w][q] = v[q];
+  __syncthreads();
+  if (tid == 0) {
+    for (int ww = 1; ww < 4; ++ww) {
+      for (int q = 0; q < 5; ++q) v[q] = fminf(v[q], red[ww][q]);
+      for (int q = 5; q < 10; ++q) v[q] = fmaxf(v[q], red[ww][q]);
+    }
+    TileBox b;
+    for (int q = 0; q < 3; ++q) {
+      b.lo[q] = v[q];
+      b.hi[q] = v[5 + q];
+    }
+    b.altlo = v[3];
+    b.althi = v[8];
+    b.smax = -v[4];
+    b.hmax = v[9];
+    b.count = b1 - b0;
+    b.pad = 0;
+    box[t] = b;
+  }
+}
+
+// ------------------------------------------------------------------ K0d tile pairs
+__device__ __forceinline__ float gap(float alo, float ahi, float blo, float bhi) {
+  return fmaxf(0.f, fmaxf(alo - bhi, blo - ahi));
+}
+
+__global__ __launch_bounds__(256) void k_tilepairs(int nrt, int nct, const TileBox *__restrict__ rb,
+                                                   const TileBox *__restrict__ cb, int noprune,
+                                                   uint2 *__restrict__ out,
+                                                   unsigned long long *__restrict__ count) {
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = id < (long long)nrt * nct;
+  bool keep = false;
+  int rt = 0, ct = 0;
+  if (valid) {
+    rt = (int)(id / nct);
+    ct = (int)(id % nct);
+    if (noprune) {
+      keep = true;
+    } else {
+      const TileBox a = rb[rt], b = cb[ct];
+      const float gx = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]);
+      const float gy = gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]);
+      const float gz = gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]);
+      const float d2 = gx * gx + gy * gy + gz * gz;
+      const float st = (a.smax + b.smax) * 1.00001f + 1e-6f;
+      const float ga = gap(a.altlo, a.althi, b.altlo, b.althi);
+      // a pair inside can pass only if its chord < s_i + s_j <= smax_a + smax_b
+      // and |dalt| < h_i + h_j <= hmax_a + hmax_b; the gaps bound chord/dalt below
+      keep = !(d2 >= st * st) && !(ga >= (a.hmax + b.hmax) * 1.00001f + 1e-3f);
+    }
+  }
+  const unsigned long long m = __ballot(keep);
+  if (m) {
+    const int lane = threadIdx.x & 63;
+    const int leader = __builtin_ctzll(m);
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader);
+    if (keep) {
+      const unsigned pos = (unsigned)(base + __builtin_amdgcn_mbcnt_hi(
+                                                 (unsigned)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)));
+      out[pos] = make_uint2((unsigned)rt, (unsigned)ct);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ K1a prefilter
 constexpr int PF_BLOCK = 256;
-constexpr int PF_RPT = 2;                    // ownship rows per lane
-constexpr int PF_ROWS = PF_BLOCK * PF_RPT;   // rows per workgroup
-constexpr int PF_TILE = 512;                 // intruder columns per LDS tile (16 KiB)
-constexpr int PF_QCAP = 1024;                // per-wave candidate queue (8 KiB)
+constexpr int PF_QCAP = 512;                 // per-wave candidate queue (4 KiB)
 constexpr int PF_WAVES = PF_BLOCK / 64;
+static_assert(kTile == 2 * PF_BLOCK, "2 rows per lane");
+
+struct RefineParams {
+  float R;      // rpz [m]
+  float H;      // hpz [m]
+  float T;      // max(tla, 0) [s]
+  float lim2;   // ((R + EABS) / (1 - E1))^2
+};
+constexpr float kRS = 6371000.f;   // scale of the unit-sphere chord to metres
+constexpr float kE1 = 0.012f;      // bound on |log(reference dist / estimated dist)|
+constexpr float kEABS = 50.f;      // absolute position error budget [m]
 
 __device__ __forceinline__ unsigned lane_prefix(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
-
 __device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long v) {
-  unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
   return ((unsigned long long)hi << 32) | lo;
 }
 
-__device__ __forceinline__ bool pf_keep(const PFRec &a, const PFRec &c) {
+// one ownship row held in registers for the sweep
+struct RowPF {
+  PFRec p;
+  float ex, ey, nx, ny, nz;  // local east / north basis at the row position
+  float vs;
+  bool refine;               // basis well conditioned and no quirk flag
+};
+
+__device__ __forceinline__ RowPF load_row(const PFRec *__restrict__ P, const PFAux *__restrict__ A,
+                                          int k, int cnt) {
+  RowPF r;
+  if (k < cnt) {
+    r.p = P[k];
+    const PFAux a = A[k];
+    r.vs = a.vs;
+    const float rho = sqrtf(r.p.x * r.p.x + r.p.y * r.p.y);
+    r.refine = (a.flags == 0) && rho > 1e-2f;
+    const float ir = r.refine ? 1.f / rho : 0.f;
+    r.ex = -r.p.y * ir;
+    r.ey = r.p.x * ir;
+    r.nx = -r.p.z * r.p.x * ir;
+    r.ny = -r.p.z * r.p.y * ir;
+    r.nz = rho;
+  } else {
+    const float qnan = __builtin_nanf("");
+    r.p.x = r.p.y = r.p.z = qnan;   // NaN never passes a test
+    r.p.s = r.p.alt = r.p.h = r.p.u = r.p.v = 0.f;
+    r.vs = 0.f;
+    r.refine = false;
+    r.ex = r.ey = r.nx = r.ny = r.nz = 0.f;
+  }
+  return r;
+}
+
+// stage 1: conservative reach test (keeps every pair that can be a conflict
+// or a loss of separation; proof in DESIGN.md)
+__device__ __forceinline__ bool pf_reach(const PFRec &a, const PFRec &c) {
   const float dx = c.x - a.x, dy = c.y - a.y, dz = c.z - a.z;
   const float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
   const float st = a.s + c.s;
   const float dh = __builtin_fabsf(c.alt - a.alt);
   return (d2 < st * st) & (dh < a.h + c.h);
+}
+
+// stage 2: conservative closest-approach refine.  Returns false only when no
+// t in [0, max(tla,0)] can lie in both the vertical and horizontal windows of
+// the reference's geometry (DESIGN.md "CPA refine"); NaN keeps the pair.
+__device__ __forceinline__ bool pf_refine(const RowPF &r, const PFRec &c, float cvs, unsigned cflags,
+                                          const RefineParams &rp) {
+  if (!r.refine || cflags) return true;
+  const float dx = c.x - r.p.x, dy = c.y - r.p.y, dz = c.z - r.p.z;
+  if (dx * dx + dy * dy + dz * dz > 0.04f) return true;   // > ~1270 km: keep, no refine
+  const float pe = (dx * r.ex + dy * r.ey) * kRS;
+  const float pn = (dx * r.nx + dy * r.ny + dz * r.nz) * kRS;
+  const float ve = c.u - r.p.u, vn = c.v - r.p.v;          // own.u[j] - int.u[i]
+  const float vv = ve * ve + vn * vn;
+  if (!(vv >= 4e-6f)) return true;                         // reference may clamp dv2
+  const float dalt = c.alt - r.p.alt;                      // own.alt[j] - int.alt[i]
+  const float dvs = cvs - r.vs;
+  const float adv = __builtin_fabsf(dvs);
+  float t0 = 0.f, t1 = rp.T;
+  if (adv < 1e-3f) {
+    if (__builtin_fabsf(dalt) >= rp.H + 1e-3f * rp.T + 2.f + 1e-5f * __builtin_fabsf(dalt)) return false;
+  } else {
+    const float ta = (-rp.H - dalt) / dvs, tb = (rp.H - dalt) / dvs;
+    const float lo = fminf(ta, tb), hi = fmaxf(ta, tb);
+    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + rp.H)) / adv +
+                    1e-4f * fmaxf(__builtin_fabsf(lo), __builtin_fabsf(hi));
+    t0 = fmaxf(lo - d, 0.f);
+    t1 = fminf(hi + d, rp.T);
+    if (t0 > t1) return false;
+  }
+  const float tl = t0 * (1.f - kE1), th = t1 * (1.f + 2.f * kE1);
+  float ts = -(pe * ve + pn * vn) / vv;
+  ts = fminf(fmaxf(ts, tl), th);
+  const float qe = pe + ve * ts, qn = pn + vn * ts;
+  return !(qe * qe + qn * qn > rp.lim2);
 }
 
 __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 *__restrict__ cand,
@@ -192,35 +428,49 @@ __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 
 }
 
 __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
-    const PFRec *__restrict__ prow, const PFRec *__restrict__ pcol, int rb, int re, int ncols,
-    int cols_per_split, int noprune, uint2 *__restrict__ cand,
+    const PFRec *__restrict__ prow, const PFAux *__restrict__ arow, int nrows,
+    const PFRec *__restrict__ pcol, const PFAux *__restrict__ acol, int ncols,
+    const uint2 *__restrict__ tiles, const unsigned long long *__restrict__ ntiles_p,
+    RefineParams rp, int noprune, uint2 *__restrict__ cand,
     unsigned long long *__restrict__ cand_count, unsigned long long cap) {
-  __shared__ PFRec tile[PF_TILE];
+  __shared__ PFRec tile[kTile];
+  __shared__ PFAux aux[kTile];
   __shared__ uint2 queue[PF_WAVES][PF_QCAP];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int r0 = rb + blockIdx.x * PF_ROWS + tid;
-  const int r1 = r0 + PF_BLOCK;
-  PFRec a, b;
-  const float qnan = __builtin_nanf("");
-  if (r0 < re) a = prow[r0]; else { a.x = a.y = a.z = qnan; a.s = a.alt = a.h = 0.f; }
-  if (r1 < re) b = prow[r1]; else { b.x = b.y = b.z = qnan; b.s = b.alt = b.h = 0.f; }
-  const bool va = r0 < re, vb = r1 < re;
-  const int c0 = blockIdx.y * cols_per_split;
-  const int c1 = min(ncols, c0 + cols_per_split);
+  const unsigned long long ntiles = *ntiles_p;
   uint2 *q = queue[w];
   unsigned qn = 0;  // wave-uniform queue fill
-  for (int t0 = c0; t0 < c1; t0 += PF_TILE) {
-    const int nt = min(PF_TILE, c1 - t0);
+  for (unsigned long long tp = blockIdx.x; tp < ntiles; tp += gridDim.x) {
+    const uint2 rc = tiles[tp];
+    const int r0 = (int)rc.x * kTile + tid, r1 = r0 + PF_BLOCK;
+    const RowPF a = load_row(prow, arow, r0, nrows);
+    const RowPF b = load_row(prow, arow, r1, nrows);
+    const int c0 = (int)rc.y * kTile;
+    const int nt = min(kTile, ncols - c0);
     __syncthreads();
-    for (int k = tid; k < nt; k += PF_BLOCK) tile[k] = pcol[t0 + k];
+    for (int k = tid; k < nt; k += PF_BLOCK) {
+      tile[k] = pcol[c0 + k];
+      aux[k] = acol[c0 + k];
+    }
     __syncthreads();
     for (int jj = 0; jj < nt; ++jj) {
       const PFRec c = tile[jj];
-      const bool ka = noprune ? va : pf_keep(a, c);
-      const bool kb = noprune ? vb : pf_keep(b, c);
+      bool ka, kb;
+      if (noprune) {
+        ka = r0 < nrows;
+        kb = r1 < nrows;
+      } else {
+        ka = pf_reach(a.p, c);
+        kb = pf_reach(b.p, c);
+        if (__ballot(ka | kb)) {
+          const PFAux ca = aux[jj];
+          if (ka) ka = pf_refine(a, c, ca.vs, ca.flags, rp);
+          if (kb) kb = pf_refine(b, c, ca.vs, ca.flags, rp);
+        }
+      }
       const unsigned long long ma = __ballot(ka), mb = __ballot(kb);
       if (ma | mb) {
-        const unsigned j = (unsigned)(t0 + jj);
+        const unsigned j = (unsigned)(c0 + jj);
         if (ka) q[qn + lane_prefix(ma)] = make_uint2((unsigned)r0, j);
         qn += (unsigned)__popcll(ma);
         if (kb) q[qn + lane_prefix(mb)] = make_uint2((unsigned)r1, j);
@@ -312,26 +562,29 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
 }
 
 __global__ __launch_bounds__(256) void k_exact(
-    const RowRec *__restrict__ R, const ColRec *__restrict__ C, const uint2 *__restrict__ cand,
-    unsigned long long ncand, double rpz, double hpz, double tla, int rb,
-    unsigned long long *__restrict__ ckey, unsigned *__restrict__ cval,
-    double *__restrict__ cpay, unsigned long long conf_cap,
-    unsigned long long *__restrict__ lkey, unsigned long long los_cap,
+    const RowRec *__restrict__ R, const ColRec *__restrict__ C,
+    const unsigned *__restrict__ perm_r, const unsigned *__restrict__ perm_c,
+    const uint2 *__restrict__ cand, const unsigned long long *__restrict__ ncand_p,
+    unsigned long long cand_cap, double rpz, double hpz, double tla, int rb,
+    unsigned long long *__restrict__ ckey, unsigned *__restrict__ cval, double *__restrict__ cpay,
+    unsigned long long conf_cap, unsigned long long *__restrict__ lkey, unsigned long long los_cap,
     Counters *__restrict__ cnt, unsigned char *__restrict__ inconf,
     unsigned long long *__restrict__ tcpamax_bits) {
   const int lane = threadIdx.x & 63;
+  const unsigned long long ncand = min(*ncand_p, cand_cap);
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long idx = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
        idx < ncand; idx += stride) {
     const uint2 p = cand[idx];
+    const unsigned oi = perm_r[p.x], oj = perm_c[p.y];
     bool conf = false, los = false;
     PairResult o;
-    if (p.x != p.y) {
+    if (oi != oj) {
       o = eval_pair(R[p.x], C[p.y], rpz, hpz, tla);
       conf = o.conf;
       los = o.los;
     }
-    const unsigned long long key = ((unsigned long long)p.x << 32) | p.y;
+    const unsigned long long key = ((unsigned long long)oi << 32) | oj;
     const unsigned long long mc = __ballot(conf);
     if (mc) {
       const int leader = __builtin_ctzll(mc);
@@ -349,11 +602,12 @@ __global__ __launch_bounds__(256) void k_exact(
           cpay[3 * conf_cap + slot] = o.tin;
           cpay[4 * conf_cap + slot] = o.dcpa;
         }
-        const int row = (int)p.x - rb;
+        const int row = (int)oi - rb;
         inconf[row] = 1;
         // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
         // positive tcpa can raise it, and positive doubles order as integers.
-        if (o.tcpa > 0.0) atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
+        if (o.tcpa > 0.0)
+          atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
       }
     }
     const unsigned long long ml = __ballot(los);
@@ -397,23 +651,30 @@ __global__ __launch_bounds__(256) void k_split_los(int64_t L, const unsigned lon
 // ------------------------------------------------------------------ host side
 static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-int prep_records(Ctx *c, double rpz, double hpz, double tla) {
-  const int64_t n = c->n;
-  if (!ensure(c, c->rowrec, n * sizeof(RowRec), "row records") ||
-      !ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
-      !ensure(c, c->pfrow, n * sizeof(PFRec), "prefilter rows") ||
-      !ensure(c, c->pfcol, n * sizeof(PFRec), "prefilter columns"))
+static int bitwidth(int64_t n) {
+  int b = 1;
+  while ((int64_t(1) << b) < n) ++b;
+  return b;
+}
+
+// spatial sort of cnt positions starting at original index base -> perm
+static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const double *lon,
+                         DevBuf &key, DevBuf &idx, DevBuf &key2, DevBuf &perm) {
+  if (!ensure(c, key, (size_t)cnt * 4, "keys") || !ensure(c, idx, (size_t)cnt * 4, "key idx") ||
+      !ensure(c, key2, (size_t)cnt * 4, "sorted keys") || !ensure(c, perm, (size_t)cnt * 4, "perm"))
     return -1;
-  DevBuf *I = c->has_intruder ? c->intr : c->own;
-  hipLaunchKernelGGL(k_prep, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n,
-                     (const double *)c->own[0].p, (const double *)c->own[1].p,
-                     (const double *)c->own[2].p, (const double *)c->own[3].p,
-                     (const double *)c->own[4].p, (const double *)c->own[5].p,
-                     (const double *)I[0].p, (const double *)I[1].p, (const double *)I[2].p,
-                     (const double *)I[3].p, (const double *)I[4].p, (const double *)I[5].p,
-                     c->has_intruder ? 1 : 0, rpz, hpz, tla, (RowRec *)c->rowrec.p,
-                     (ColRec *)c->colrec.p, (PFRec *)c->pfrow.p, (PFRec *)c->pfcol.p);
+  hipLaunchKernelGGL(k_keys, dim3(blocks_for(cnt, 256)), dim3(256), 0, c->stream, cnt, base, lat, lon,
+                     (unsigned *)key.p, (unsigned *)idx.p);
   BSA_HIP(c, hipGetLastError());
+  size_t tmp = 0;
+  BSA_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (unsigned *)key.p, (unsigned *)key2.p,
+                                                (unsigned *)idx.p, (unsigned *)perm.p, cnt, 0, 30,
+                                                c->stream));
+  if (!ensure(c, c->sort_tmp, std::max<size_t>(tmp, 16), "sort scratch")) return -1;
+  tmp = c->sort_tmp.bytes;
+  BSA_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, (unsigned *)key.p,
+                                                (unsigned *)key2.p, (unsigned *)idx.p,
+                                                (unsigned *)perm.p, cnt, 0, 30, c->stream));
   return 0;
 }
 
@@ -423,18 +684,12 @@ static int read_counters(Ctx *c, Counters *h) {
   return 0;
 }
 
-static int bitwidth(int64_t n) {
-  int b = 1;
-  while ((int64_t(1) << b) < n) ++b;
-  return b;
-}
-
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
            int64_t *n_conf, int64_t *n_los) {
   const int64_t n = c->n;
   if (re <= 0) re = n;
-  if (rb < 0 || rb > re || re > n) return fail(c, "bad row range [%lld, %lld) for n=%lld",
-                                                 (long long)rb, (long long)re, (long long)n);
+  if (rb < 0 || rb > re || re > n)
+    return fail(c, "bad row range [%lld, %lld) for n=%lld", (long long)rb, (long long)re, (long long)n);
   if (n > (int64_t)0x7fffffff) return fail(c, "n=%lld exceeds 2^31-1", (long long)n);
   const int64_t nrows = re - rb;
   c->have_pairs = false;
@@ -454,63 +709,99 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
     *n_conf = *n_los = 0;
     return 0;
   }
-  if (prep_records(c, rpz, hpz, tla)) return -1;
+  const int noprune = (flags & BSA_FLAG_NOPRUNE) ? 1 : 0;
+  const bool distinct = c->has_intruder;
+  DevBuf *I = distinct ? c->intr : c->own;
+  SoA6 own{(const double *)c->own[0].p, (const double *)c->own[1].p, (const double *)c->own[2].p,
+           (const double *)c->own[3].p, (const double *)c->own[4].p, (const double *)c->own[5].p};
+  SoA6 intr{(const double *)I[0].p, (const double *)I[1].p, (const double *)I[2].p,
+            (const double *)I[3].p, (const double *)I[4].p, (const double *)I[5].p};
+
+  // ---- K0a spatial order (rows: own positions of [rb, re); columns: intruder positions)
+  if (spatial_order(c, (int)nrows, (int)rb, own.lat, own.lon, c->key_r, c->idx_r, c->key_r2, c->perm_r) ||
+      spatial_order(c, (int)n, 0, intr.lat, intr.lon, c->key_c, c->idx_c, c->key_c2, c->perm_c))
+    return -1;
+  // ---- K0b records in sorted order
+  if (!ensure(c, c->rowrec, nrows * sizeof(RowRec), "row records") ||
+      !ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
+      !ensure(c, c->pfrow, nrows * sizeof(PFRec), "prefilter rows") ||
+      !ensure(c, c->pfcol, n * sizeof(PFRec), "prefilter columns") ||
+      !ensure(c, c->pfauxrow, nrows * sizeof(PFAux), "prefilter row aux") ||
+      !ensure(c, c->pfauxcol, n * sizeof(PFAux), "prefilter column aux"))
+    return -1;
+  hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows,
+                     (const unsigned *)c->perm_r.p, own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p,
+                     (PFRec *)c->pfrow.p, (PFAux *)c->pfauxrow.p);
+  BSA_HIP(c, hipGetLastError());
+  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n,
+                     (const unsigned *)c->perm_c.p, own, intr, distinct ? 1 : 0, rpz, hpz, tla,
+                     (ColRec *)c->colrec.p, (PFRec *)c->pfcol.p, (PFAux *)c->pfauxcol.p);
+  BSA_HIP(c, hipGetLastError());
+  // ---- K0c/K0d tile culling
+  const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
+  const long long ntp = (long long)nrt * nct;
+  if (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
+      !ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
+      !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
+    return -1;
+  hipLaunchKernelGGL(k_tilebox, dim3(nrt), dim3(256), 0, c->stream, (int)nrows, (const PFRec *)c->pfrow.p,
+                     (TileBox *)c->tbox_r.p);
+  hipLaunchKernelGGL(k_tilebox, dim3(nct), dim3(256), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
+                     (TileBox *)c->tbox_c.p);
+  BSA_HIP(c, hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
+  Counters *dcnt = (Counters *)c->counters.p;
+  hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + 255) / 256)), dim3(256), 0, c->stream, nrt, nct,
+                     (const TileBox *)c->tbox_r.p, (const TileBox *)c->tbox_c.p, noprune,
+                     (uint2 *)c->tilepairs.p, &dcnt->tiles);
+  BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(c->ev[1], c->stream));
 
-  // ---- K1a prefilter (retry with a larger candidate buffer on overflow)
-  if (c->cand_cap == 0) c->cand_cap = (unsigned long long)std::max<int64_t>(1 << 20, 64 * nrows);
-  const int noprune = (flags & BSA_FLAG_NOPRUNE) ? 1 : 0;
-  const unsigned rowblocks = blocks_for(nrows, PF_ROWS);
-  unsigned splits = (unsigned)std::max<int64_t>(1, (4096 + rowblocks - 1) / rowblocks);
-  splits = (unsigned)std::min<int64_t>(splits, std::max<int64_t>(1, n / PF_TILE));
-  const int cols_per_split = (int)((n + splits - 1) / splits);
-  Counters h;
-  for (int attempt = 0;; ++attempt) {
-    if (!ensure(c, c->cand, c->cand_cap * sizeof(uint2), "candidate pairs")) return -1;
-    BSA_HIP(c, hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-    hipLaunchKernelGGL(k_prefilter, dim3(rowblocks, splits), dim3(PF_BLOCK), 0, c->stream,
-                       (const PFRec *)c->pfrow.p, (const PFRec *)c->pfcol.p, (int)rb, (int)re,
-                       (int)n, cols_per_split, noprune, (uint2 *)c->cand.p,
-                       &((Counters *)c->counters.p)->cand, c->cand_cap);
-    BSA_HIP(c, hipGetLastError());
-    if (read_counters(c, &h)) return -1;
-    if (h.cand <= c->cand_cap) break;
-    if (attempt > 3) return fail(c, "candidate buffer overflow (%llu)", h.cand);
-    c->cand_cap = h.cand + h.cand / 4 + 1024;
-  }
-  BSA_HIP(c, hipEventRecord(c->ev[2], c->stream));
-  c->last_cand = (int64_t)h.cand;
-
-  // ---- K1b exact evaluation (retry with larger outputs on overflow)
+  if (c->cand_cap == 0) c->cand_cap = (unsigned long long)std::max<int64_t>(1 << 20, 16 * nrows);
   if (c->conf_cap == 0) c->conf_cap = (unsigned long long)std::max<int64_t>(1 << 16, 8 * nrows);
   if (c->los_cap == 0) c->los_cap = (unsigned long long)std::max<int64_t>(1 << 16, 4 * nrows);
-  const unsigned long long ncand = h.cand;
+  const float T = (float)(tla > 0.0 ? tla : 0.0);
+  const float lim = (float)((rpz + kEABS) / (1.0 - kE1));
+  const RefineParams rp{(float)rpz, (float)hpz, T, lim * lim};
+  Counters h;
   for (int attempt = 0;; ++attempt) {
-    if (!ensure(c, c->ckey, c->conf_cap * 8, "conflict keys") ||
+    if (!ensure(c, c->cand, c->cand_cap * sizeof(uint2), "candidate pairs") ||
+        !ensure(c, c->ckey, c->conf_cap * 8, "conflict keys") ||
         !ensure(c, c->cval, c->conf_cap * 4, "conflict slots") ||
         !ensure(c, c->cpay, c->conf_cap * 5 * 8, "conflict payload") ||
         !ensure(c, c->lkey, c->los_cap * 8, "los keys"))
       return -1;
-    BSA_HIP(c, hipMemsetAsync(&((Counters *)c->counters.p)->conf, 0, 16, c->stream));
+    // ---- K1a prefilter over surviving tile pairs (persistent grid, count read on device)
+    BSA_HIP(c, hipMemsetAsync(&dcnt->cand, 0, 24, c->stream));  // cand, conf, los
     BSA_HIP(c, hipMemsetAsync(c->inconf.p, 0, nrows, c->stream));
     BSA_HIP(c, hipMemsetAsync(c->tcpamax.p, 0, nrows * 8, c->stream));
-    if (ncand) {
-      const unsigned grid = (unsigned)std::min<unsigned long long>((ncand + 255) / 256, 1u << 16);
-      hipLaunchKernelGGL(k_exact, dim3(grid), dim3(256), 0, c->stream, (const RowRec *)c->rowrec.p,
-                         (const ColRec *)c->colrec.p, (const uint2 *)c->cand.p, ncand, rpz, hpz, tla,
-                         (int)rb, (unsigned long long *)c->ckey.p, (unsigned *)c->cval.p,
-                         (double *)c->cpay.p, c->conf_cap, (unsigned long long *)c->lkey.p,
-                         c->los_cap, (Counters *)c->counters.p, (unsigned char *)c->inconf.p,
-                         (unsigned long long *)c->tcpamax.p);
-      BSA_HIP(c, hipGetLastError());
-    }
+    const unsigned pf_grid = (unsigned)std::min<long long>(ntp, 256 * 6);
+    hipLaunchKernelGGL(k_prefilter, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
+                       (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
+                       (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
+                       (const uint2 *)c->tilepairs.p, &dcnt->tiles, rp, noprune, (uint2 *)c->cand.p,
+                       &dcnt->cand, c->cand_cap);
+    BSA_HIP(c, hipGetLastError());
+    BSA_HIP(c, hipEventRecord(c->ev[2], c->stream));
+    // ---- K1b exact evaluation (grid-stride, count read on device)
+    hipLaunchKernelGGL(k_exact, dim3(256 * 16), dim3(256), 0, c->stream, (const RowRec *)c->rowrec.p,
+                       (const ColRec *)c->colrec.p, (const unsigned *)c->perm_r.p,
+                       (const unsigned *)c->perm_c.p, (const uint2 *)c->cand.p, &dcnt->cand,
+                       c->cand_cap, rpz, hpz, tla, (int)rb, (unsigned long long *)c->ckey.p,
+                       (unsigned *)c->cval.p, (double *)c->cpay.p, c->conf_cap,
+                       (unsigned long long *)c->lkey.p, c->los_cap, dcnt, (unsigned char *)c->inconf.p,
+                       (unsigned long long *)c->tcpamax.p);
+    BSA_HIP(c, hipGetLastError());
+    BSA_HIP(c, hipEventRecord(c->ev[3], c->stream));
     if (read_counters(c, &h)) return -1;
-    if (h.conf <= c->conf_cap && h.los <= c->los_cap) break;
-    if (attempt > 3) return fail(c, "pair buffer overflow (conf %llu, los %llu)", h.conf, h.los);
+    if (h.cand <= c->cand_cap && h.conf <= c->conf_cap && h.los <= c->los_cap) break;
+    if (attempt > 3) return fail(c, "pair buffer overflow (cand %llu conf %llu los %llu)", h.cand, h.conf, h.los);
+    if (h.cand > c->cand_cap) c->cand_cap = h.cand + h.cand / 4 + 1024;
     if (h.conf > c->conf_cap) c->conf_cap = h.conf + h.conf / 4 + 1024;
     if (h.los > c->los_cap) c->los_cap = h.los + h.los / 4 + 1024;
   }
-  BSA_HIP(c, hipEventRecord(c->ev[3], c->stream));
+  c->last_cand = (int64_t)h.cand;
+  c->last_tiles = (int64_t)h.tiles;
+  c->last_tiles_total = ntp;
 
   // ---- K2 canonical row-major order
   const int64_t P = (int64_t)h.conf, L = (int64_t)h.los;
@@ -532,9 +823,9 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   BSA_HIP(c, hipcub::DeviceRadixSort::SortKeys(nullptr, t2, (unsigned long long *)nullptr,
                                                (unsigned long long *)nullptr,
                                                (int)std::max<int64_t>(L, 1), 0, end_bit, c->stream));
-  size_t tmp = std::max(t1, t2);
-  if (!ensure(c, c->sort_tmp, std::max<size_t>(tmp, 16), "sort scratch")) return -1;
+  if (!ensure(c, c->sort_tmp, std::max<size_t>(std::max(t1, t2), 16), "sort scratch")) return -1;
   if (P > 0) {
+    size_t tmp = c->sort_tmp.bytes;
     BSA_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, (unsigned long long *)c->ckey.p,
                                                   (unsigned long long *)c->ckey2.p, (unsigned *)c->cval.p,
                                                   (unsigned *)c->cval2.p, (int)P, 0, end_bit, c->stream));
@@ -545,7 +836,7 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
     BSA_HIP(c, hipGetLastError());
   }
   if (L > 0) {
-    tmp = std::max(t1, t2);
+    size_t tmp = c->sort_tmp.bytes;
     BSA_HIP(c, hipcub::DeviceRadixSort::SortKeys(c->sort_tmp.p, tmp, (unsigned long long *)c->lkey.p,
                                                  (unsigned long long *)c->lkey2.p, (int)L, 0, end_bit,
                                                  c->stream));

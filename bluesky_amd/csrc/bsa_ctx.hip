@@ -125,7 +125,10 @@ void bsa_destroy(bsa_ctx *c) {
   bsa::DevBuf *all[] = {&c->rowrec, &c->colrec, &c->pfrow, &c->pfcol, &c->counters, &c->cand,
                         &c->ckey, &c->cval, &c->ckey2, &c->cval2, &c->cpay, &c->lkey, &c->lkey2,
                         &c->out_ci, &c->out_cj, &c->out_li, &c->out_lj, &c->out_pay, &c->inconf,
-                        &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage};
+                        &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage,
+                        &c->pfauxrow, &c->pfauxcol, &c->key_r, &c->idx_r, &c->key_r2, &c->perm_r,
+                        &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
+                        &c->tilepairs};
   for (auto *b : all) bsa::release(*b);
   for (int k = 0; k < 6; ++k) {
     bsa::release(c->own[k]);
@@ -219,6 +222,13 @@ int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *d
 int bsa_last_candidates(bsa_ctx *c, int64_t *n_candidates) {
   if (!c || !n_candidates) return -1;
   *n_candidates = c->last_cand;
+  return 0;
+}
+
+int bsa_last_tiles(bsa_ctx *c, int64_t *kept, int64_t *total) {
+  if (!c || !kept || !total) return -1;
+  *kept = c->last_tiles;
+  *total = c->last_tiles_total;
   return 0;
 }
 

@@ -59,16 +59,33 @@ struct alignas(16) PFRec {
   float s;         // horizontal reach, chord units (half of the pair bound)
   float alt;       // altitude [m]
   float h;         // vertical reach [m] (half of the pair bound)
-  float pad0, pad1;
+  float u, v;      // east / north velocity [m/s] (same orientation as RowRec/ColRec)
 };
 static_assert(sizeof(PFRec) == 32, "PFRec must be 32 B");
+
+// cold part of the prefilter record, read only by the CPA refine
+struct alignas(8) PFAux {
+  float vs;        // vertical speed [m/s]
+  unsigned flags;  // bit 0: never refine this index (unbounded radius quirk / non-finite)
+};
+
+// axis-aligned bounds of one tile of sorted PFRecs (tile culling)
+struct alignas(16) TileBox {
+  float lo[3], hi[3];
+  float altlo, althi;
+  float smax, hmax;
+  int count, pad;
+};
+
+constexpr int kTile = 512;  // rows per row block == columns per column tile
 
 // counters block on the device (one cache line)
 struct Counters {
   unsigned long long cand;
   unsigned long long conf;
   unsigned long long los;
-  unsigned long long pad[5];
+  unsigned long long tiles;
+  unsigned long long pad[4];
 };
 
 // ---------------------------------------------------------------- buffers
@@ -91,7 +108,10 @@ struct Ctx {
   bool has_intruder = false;
   DevBuf own[6];   // lat lon trk gs alt vs
   DevBuf intr[6];
-  DevBuf rowrec, colrec, pfrow, pfcol;
+  DevBuf rowrec, colrec, pfrow, pfcol, pfauxrow, pfauxcol;
+  // spatial order: Morton keys and the sorted-position -> original-index maps
+  DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
+  DevBuf tbox_r, tbox_c, tilepairs;
 
   // detect buffers
   DevBuf counters;           // Counters
@@ -109,7 +129,7 @@ struct Ctx {
 
   // last detect
   int64_t last_rb = 0, last_re = 0;
-  int64_t last_conf = 0, last_los = 0, last_cand = 0;
+  int64_t last_conf = 0, last_los = 0, last_cand = 0, last_tiles = 0, last_tiles_total = 0;
   int last_flags = 0;
   bool have_pairs = false;
 
@@ -152,6 +172,5 @@ int fail(Ctx *c, const char *fmt, ...);
 // detect entry (bsa_cd.hip)
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
            int64_t *n_conf, int64_t *n_los);
-int prep_records(Ctx *c, double rpz, double hpz, double tla);
 
 }  // namespace bsa

@@ -103,9 +103,13 @@ int bsa_fetch_pairs(bsa_ctx *ctx,
  * conservative prefilter and were evaluated exactly in fp64). */
 int bsa_last_candidates(bsa_ctx *ctx, int64_t *n_candidates);
 
-/* Device time of the last detect's kernels in milliseconds, measured with
- * HIP events on the context stream: [0] prep, [1] prefilter, [2] exact,
- * [3] sort+gather, [4] whole detect (first event to last). */
+/* Tile pairs (512 rows x 512 columns) of the last detect that survived the
+ * bounding-box cull, and the total number of tile pairs. */
+int bsa_last_tiles(bsa_ctx *ctx, int64_t *kept, int64_t *total);
+
+/* Device time of the last detect's stages in milliseconds, measured with
+ * HIP events on the context stream: [0] spatial order + records + tile cull,
+ * [1] prefilter, [2] exact, [3] sort+gather, [4] whole detect. */
 int bsa_last_timings(bsa_ctx *ctx, double *ms5);
 
 /* ---------------------------------------------------------------- MVP
