@@ -83,6 +83,44 @@ SIGNATURES.update({
                                       ctypes.c_double, ctypes.c_double, ctypes.POINTER(KinIO)]),
 })
 
+class SimParams(ctypes.Structure):
+    """bsa_sim_params (include/bsaccel.h)."""
+    _fields_ = [('simdt', ctypes.c_double), ('rpz', ctypes.c_double), ('hpz', ctypes.c_double),
+                ('tla', ctypes.c_double), ('cd_every', ctypes.c_int32), ('reso', ctypes.c_int32),
+                ('mvp', MvpParams)]
+
+
+SIM_STATE_FIELDS = ('lat', 'lon', 'alt', 'tas', 'hdg', 'vs', 'gs', 'trk', 'gseast', 'gsnorth',
+                    'ap_trk', 'ap_tas', 'ap_alt', 'ap_vs', 'selalt', 'bank', 'eps', 'accel',
+                    'asas_alt')
+SIM_OUT_FIELDS = ('lat', 'lon', 'alt', 'tas', 'hdg', 'vs', 'gs', 'trk', 'gseast', 'gsnorth',
+                  'asas_trk', 'asas_tas', 'asas_vs', 'asas_alt')
+
+
+class SimState(ctypes.Structure):
+    """bsa_sim_state (include/bsaccel.h)."""
+    _fields_ = [(k, _c_dp) for k in SIM_STATE_FIELDS]
+
+
+class SimOut(ctypes.Structure):
+    """bsa_sim_out (include/bsaccel.h)."""
+    _fields_ = [(k, _c_dp) for k in SIM_OUT_FIELDS] + [('active', _c_u8p)]
+
+
+SIGNATURES.update({
+    'bsa_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
+    'bsa_comm_init': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+    'bsa_comm_allreduce_max': (ctypes.c_int, [_vp, _c_dp, ctypes.c_int]),
+    'bsa_comm_allreduce_sum': (ctypes.c_int, [_vp, _c_dp, ctypes.c_int]),
+    'bsa_sim_init': (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.POINTER(SimState),
+                                    ctypes.POINTER(SimParams)]),
+    'bsa_sim_step': (ctypes.c_int, [_vp, ctypes.c_int]),
+    'bsa_sim_read': (ctypes.c_int, [_vp, ctypes.POINTER(SimOut)]),
+    'bsa_sim_stats': (ctypes.c_int, [_vp, _c_i64p]),
+})
+
+UNIQUE_ID_BYTES = 128
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -110,6 +148,15 @@ def load(path=None):
             raise AccelUnavailable('ABI mismatch: library %d, bindings %d' % (v, ABI_VERSION))
         _lib = lib
         return lib
+
+
+def comm_unique_id():
+    """128-byte RCCL communicator id (create on one rank, ship to the others)."""
+    lib = load()
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    if lib.bsa_comm_unique_id(buf) != 0:
+        raise AccelError('bsa_comm_unique_id failed')
+    return buf.raw
 
 
 def ptr(a, ctype=_c_dp):
@@ -236,8 +283,54 @@ class Context:
                                     ptr(o['asasn'], _c_fp)), 'bsa_mvp')
         return o
 
+    # ---------------------------------------------------------------- multi-GPU
+    def comm_init(self, nranks, rank, uid):
+        if len(uid) != UNIQUE_ID_BYTES:
+            raise ValueError('unique id must be %d bytes' % UNIQUE_ID_BYTES)
+        self.check(self.lib.bsa_comm_init(self.h, int(nranks), int(rank), uid), 'bsa_comm_init')
+
+    def allreduce_max(self, values):
+        v = np.array(values, dtype=np.float64, copy=True).ravel()
+        self.check(self.lib.bsa_comm_allreduce_max(self.h, ptr(v), len(v)), 'bsa_comm_allreduce_max')
+        return v
+
+    def allreduce_sum(self, values):
+        v = np.array(values, dtype=np.float64, copy=True).ravel()
+        self.check(self.lib.bsa_comm_allreduce_sum(self.h, ptr(v), len(v)), 'bsa_comm_allreduce_sum')
+        return v
+
+    # ---------------------------------------------------------------- resident sim
+    def sim_init(self, state, params):
+        n = len(state['lat'])
+        keep = {k: f64(state[k]) for k in SIM_STATE_FIELDS}
+        for k, a in keep.items():
+            if len(a) != n:
+                raise ValueError('sim state %s has length %d != %d' % (k, len(a), n))
+        st = SimState(**{k: ptr(a) for k, a in keep.items()})
+        self.check(self.lib.bsa_sim_init(self.h, n, ctypes.byref(st), ctypes.byref(params)),
+                   'bsa_sim_init')
+        self.n = n
+
+    def sim_step(self, nsteps=1):
+        self.check(self.lib.bsa_sim_step(self.h, int(nsteps)), 'bsa_sim_step')
+
+    def sim_read(self):
+        n = self.n
+        o = {k: np.empty(n) for k in SIM_OUT_FIELDS}
+        o['active'] = np.empty(n, np.uint8)
+        so = SimOut(**{k: ptr(o[k]) for k in SIM_OUT_FIELDS}, active=ptr(o['active'], _c_u8p))
+        self.check(self.lib.bsa_sim_read(self.h, ctypes.byref(so)), 'bsa_sim_read')
+        o['active'] = o['active'].astype(bool)
+        return o
+
+    def sim_stats(self):
+        v = np.zeros(6, np.int64)
+        self.check(self.lib.bsa_sim_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_stats')
+        return dict(steps=int(v[0]), cd_calls=int(v[1]), n_conf=int(v[2]), n_los=int(v[3]),
+                    row_begin=int(v[4]), row_end=int(v[5]))
+
     # ---------------------------------------------------------------- kinematics
-    KIN_OUT = ('ax', 'delspd', 'cas', 'mach', 'gsnorth', 'gseast', 'gs', 'trk', 'coslat', 'az')
+    KIN_OUT =('ax', 'delspd', 'cas', 'mach', 'gsnorth', 'gseast', 'gs', 'trk', 'coslat', 'az')
 
     def kinematics(self, simdt, state, inputs, winddim=0, windnorth=0.0, windeast=0.0):
         """bsa_kinematics.  ``state``: dict of float64 arrays tas, hdg, alt, vs,

@@ -130,6 +130,7 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
                         &c->tilepairs};
   for (auto *b : all) bsa::release(*b);
+  bsa::sim_release(c);
   for (int k = 0; k < 6; ++k) {
     bsa::release(c->own[k]);
     bsa::release(c->intr[k]);
@@ -156,6 +157,7 @@ int bsa_set_state(bsa_ctx *c, int64_t n, const double *lat, const double *lon, c
   if (!c) return -1;
   if (n < 0) return bsa::fail(c, "negative n");
   BSA_HIP(c, hipSetDevice(c->device));
+  c->sim_ready = false;  // a new state replaces any resident sim
   const double *src[6] = {lat, lon, trk, gs, alt, vs};
   if (n == 0) {
     c->n = 0;

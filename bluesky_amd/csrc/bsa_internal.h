@@ -138,6 +138,22 @@ struct Ctx {
 
   // MVP / kinematics staging (host-buffer entry points)
   DevBuf seg, mvp_stage, kin_stage;
+
+  // multi-GPU (RCCL); comm is an ncclComm_t
+  void *comm = nullptr;
+  int nranks = 1, rank = 0;
+  DevBuf red;  // small reduction scratch
+
+  // GPU-resident sim (bsa_sim.hip)
+  bool sim_ready = false;
+  bsa_sim_params simp{};
+  int64_t sim_steps = 0, sim_cd_calls = 0, sim_rb = 0, sim_re = 0, sim_rpr = 0;
+  int64_t sim_last_conf = 0, sim_last_los = 0;
+  bool sim_gathered = true;  // replicas consistent with every rank's rows
+  DevBuf s_tas, s_hdg, s_gse, s_gsn;                        // traffic state besides own[]
+  DevBuf s_aptrk, s_aptas, s_apalt, s_apvs, s_selalt, s_bank, s_eps, s_accel;  // frozen
+  DevBuf s_atrk, s_atas, s_avs, s_aalt, s_ase, s_asn, s_active;  // ASAS (full n)
+  DevBuf g_send, g_recv;                                    // all-gather staging
 };
 
 // device pointers for the MVP kernel (full-N traffic arrays, per-row outputs)
@@ -168,6 +184,9 @@ int fail(Ctx *c, const char *fmt, ...);
       return ::bsa::fail((c), "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
                          __FILE__, __LINE__);                                         \
   } while (0)
+
+// sim / comm teardown (bsa_sim.hip)
+void sim_release(Ctx *c);
 
 // detect entry (bsa_cd.hip)
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,

@@ -1,120 +1,50 @@
-// K4: fused kinematic integration of one sim step, one lane per aircraft.
-//
-// Traffic.UpdateAirSpeed   bluesky/traffic/traffic.py:425-454
-// Traffic.UpdateGroundSpeed bluesky/traffic/traffic.py:456-476 (winddim 0/1)
-// Traffic.UpdatePosition   bluesky/traffic/traffic.py:478-483
-// with aero.vatmos / vtas2cas / vtas2mach (bluesky/tools/aero.py:62-147)
-// inlined.  HBM-bound: 13 fp64 reads + 16 fp64 + 2 byte writes per aircraft
-// (234 B); every expression keeps numpy's evaluation order.
-#include "bsa_internal.h"
+// K4: fused kinematic integration of one sim step, one lane per aircraft
+// (math in bsa_kin_math.h: traffic.py:425-483 + aero.py:62-147).
+// HBM-bound: 13 fp64 reads + 16 fp64 + 2 byte writes per aircraft
+// (234 B).
+#include "bsa_kin_math.h"
 
 #pragma clang fp contract(off)
 
 namespace bsa {
 
-namespace {
-constexpr double kG0 = 9.80665;        // aero.py:18
-constexpr double kRgas = 287.05287;    // aero.py:19
-constexpr double kP0 = 101325.;        // aero.py:20
-constexpr double kRho0 = 1.225;        // aero.py:21
-constexpr double kTstrat = 216.65;     // aero.py:23
-constexpr double kGamma = 1.40;        // aero.py:24
-constexpr double kRearth = 6371000.;   // aero.py:28
-constexpr double kFPM = kFT / 60.;     // aero.py:13
-
-__device__ __forceinline__ double npmax(double a, double b) { return (a >= b || a != a) ? a : b; }
-__device__ __forceinline__ double npsign(double x) {
-  return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x));
-}
-__device__ __forceinline__ double nprem(double a, double b) {
-  double mod = fmod(a, b);
-  if (mod != 0.0) {
-    if ((b < 0) != (mod < 0)) mod += b;
-  } else {
-    mod = copysign(0.0, b);
-  }
-  return mod;
-}
-}  // namespace
-
 __global__ __launch_bounds__(256) void k_kinematics(int n, double simdt, int winddim, double wn,
                                                     double we, KinDev d) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const double tas0 = d.tas[k], hdg0 = d.hdg[k], alt0 = d.alt[k], vs0 = d.vs[k];
-  const double ptas = d.ptas[k], phdg = d.phdg[k], palt = d.palt[k], pvs = d.pvs[k];
-
-  // ---- UpdateAirSpeed: speed
-  const double delta_spd = ptas - tas0;
-  const double need_ax = fabs(delta_spd) > kKTS ? 1.0 : 0.0;
-  const double ax = need_ax * npsign(delta_spd) * d.accel[k];
-  const double tas = tas0 + ax * simdt;
-  // vatmos(alt) (aero.py:62-74) shared by vtas2cas and vtas2mach
-  const double T = npmax(288.15 - 0.0065 * alt0, kTstrat);
-  const double rhotrop = 1.225 * pow(T / 288.15, 4.256848030018761);
-  const double dhstrat = npmax(0., alt0 - 11000.);
-  const double rho = rhotrop * exp(-dhstrat / 6341.552161);
-  const double p = rho * kRgas * T;
-  const double qdyn = p * (pow(1. + rho * tas * tas / (7. * p), 3.5) - 1.);
-  double cas = sqrt(7. * kP0 / kRho0 * (pow(qdyn / kP0 + 1., 2. / 7.) - 1.));
-  cas = tas < 0 ? -1 * cas : cas;
-  const double a = sqrt(kGamma * kRgas * T);
-  const double mach = tas / a;
-  // turning
-  const double turnrate = (kG0 * tan(d.bank[k]) / npmax(tas, d.eps[k])) * kR2D;
-  const double delhdg = nprem(phdg - hdg0 + 180, 360) - 180;
-  const bool swhdgsel = fabs(delhdg) > fabs(2 * simdt * turnrate);
-  const double hdg = nprem(hdg0 + simdt * turnrate * (swhdgsel ? 1.0 : 0.0) * npsign(delhdg), 360.);
-  // vertical speed
-  const double delta_alt = palt - alt0;
-  const bool swaltsel = fabs(delta_alt) > npmax(10 * kFT, fabs(2 * simdt * fabs(vs0)));
-  const double target_vs = (swaltsel ? 1.0 : 0.0) * npsign(delta_alt) * fabs(pvs);
-  const double delta_vs = target_vs - vs0;
-  const bool need_az = fabs(delta_vs) > 300 * kFPM;
-  const double az = (need_az ? 1.0 : 0.0) * npsign(delta_vs) * (300 * kFPM);
-  double vs = need_az ? vs0 + az * simdt : target_vs;
-  vs = isfinite(vs) ? vs : 0;
-
-  // ---- UpdateGroundSpeed
-  double gsnorth, gseast, gs, trk;
-  if (winddim == 0) {
-    gsnorth = tas * cos(hdg * kD2R);
-    gseast = tas * sin(hdg * kD2R);
-    gs = tas;
-    trk = hdg;
-  } else {
-    const double aw = alt0 > 50. * kFT ? 1.0 : 0.0;
-    const double naw = 1.0 - aw;
-    gsnorth = tas * cos(hdg * kD2R) + wn * aw;
-    gseast = tas * sin(hdg * kD2R) + we * aw;
-    gs = naw * tas + aw * sqrt(gsnorth * gsnorth + gseast * gseast);
-    trk = naw * hdg + nprem(aw * (atan2(gseast, gsnorth) * kR2D), 360.);
-  }
-
-  // ---- UpdatePosition
-  const double alt = swaltsel ? alt0 + vs * simdt : palt;
-  const double lat = d.lat[k] + (simdt * gsnorth / kRearth) * kR2D;
-  const double coslat = cos(lat * kD2R);
-  const double lon = d.lon[k] + (simdt * gseast / coslat / kRearth) * kR2D;
-
-  d.tas[k] = tas;
-  d.hdg[k] = hdg;
-  d.alt[k] = alt;
-  d.vs[k] = vs;
-  d.lat[k] = lat;
-  d.lon[k] = lon;
-  if (d.ax) d.ax[k] = ax;
-  if (d.delspd) d.delspd[k] = delta_spd;
-  if (d.cas) d.cas[k] = cas;
-  if (d.mach) d.mach[k] = mach;
-  if (d.gsnorth) d.gsnorth[k] = gsnorth;
-  if (d.gseast) d.gseast[k] = gseast;
-  if (d.gs) d.gs[k] = gs;
-  if (d.trk) d.trk[k] = trk;
-  if (d.coslat) d.coslat[k] = coslat;
-  if (d.az) d.az[k] = az;
-  if (d.swhdgsel) d.swhdgsel[k] = swhdgsel;
-  if (d.swaltsel) d.swaltsel[k] = swaltsel;
+  kin::In s;
+  s.tas = d.tas[k];
+  s.hdg = d.hdg[k];
+  s.alt = d.alt[k];
+  s.vs = d.vs[k];
+  s.lat = d.lat[k];
+  s.lon = d.lon[k];
+  s.ptas = d.ptas[k];
+  s.phdg = d.phdg[k];
+  s.palt = d.palt[k];
+  s.pvs = d.pvs[k];
+  s.bank = d.bank[k];
+  s.eps = d.eps[k];
+  s.accel = d.accel[k];
+  const kin::Out o = kin::step(s, simdt, winddim, wn, we);
+  d.tas[k] = o.tas;
+  d.hdg[k] = o.hdg;
+  d.alt[k] = o.alt;
+  d.vs[k] = o.vs;
+  d.lat[k] = o.lat;
+  d.lon[k] = o.lon;
+  if (d.ax) d.ax[k] = o.ax;
+  if (d.delspd) d.delspd[k] = o.delspd;
+  if (d.cas) d.cas[k] = o.cas;
+  if (d.mach) d.mach[k] = o.mach;
+  if (d.gsnorth) d.gsnorth[k] = o.gsnorth;
+  if (d.gseast) d.gseast[k] = o.gseast;
+  if (d.gs) d.gs[k] = o.gs;
+  if (d.trk) d.trk[k] = o.trk;
+  if (d.coslat) d.coslat[k] = o.coslat;
+  if (d.az) d.az[k] = o.az;
+  if (d.swhdgsel) d.swhdgsel[k] = o.swhdgsel;
+  if (d.swaltsel) d.swaltsel[k] = o.swaltsel;
 }
 
 int kin_device(Ctx *c, int64_t n, double simdt, int winddim, double vn, double ve, const KinDev &d) {

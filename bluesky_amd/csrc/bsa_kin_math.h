@@ -1,0 +1,111 @@
+// Device-side math of one aircraft's kinematic step, shared by the host-API
+// kernel (bsa_kin.hip) and the GPU-resident sim step (bsa_sim.hip).
+//
+// Traffic.UpdateAirSpeed    bluesky/traffic/traffic.py:425-454
+// Traffic.UpdateGroundSpeed bluesky/traffic/traffic.py:456-476 (winddim 0/1)
+// Traffic.UpdatePosition    bluesky/traffic/traffic.py:478-483
+// aero.vatmos / vtas2cas / vtas2mach  bluesky/tools/aero.py:62-147
+// Every expression keeps numpy's evaluation order (compile with
+// -ffp-contract=off).
+#pragma once
+#include "bsa_internal.h"
+
+namespace bsa {
+namespace kin {
+
+constexpr double kG0 = 9.80665;        // aero.py:18
+constexpr double kRgas = 287.05287;    // aero.py:19
+constexpr double kP0 = 101325.;        // aero.py:20
+constexpr double kRho0 = 1.225;        // aero.py:21
+constexpr double kTstrat = 216.65;     // aero.py:23
+constexpr double kGamma = 1.40;        // aero.py:24
+constexpr double kRearth = 6371000.;   // aero.py:28
+constexpr double kFPM = kFT / 60.;     // aero.py:13
+
+__device__ __forceinline__ double npmax(double a, double b) { return (a >= b || a != a) ? a : b; }
+__device__ __forceinline__ double npsign(double x) {
+  return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x));
+}
+// numpy.remainder for float64 (npy_divmod semantics)
+__device__ __forceinline__ double nprem(double a, double b) {
+  double mod = fmod(a, b);
+  if (mod != 0.0) {
+    if ((b < 0) != (mod < 0)) mod += b;
+  } else {
+    mod = copysign(0.0, b);
+  }
+  return mod;
+}
+
+struct In {
+  double tas, hdg, alt, vs, lat, lon;       // state before the step
+  double ptas, phdg, palt, pvs;             // pilot targets
+  double bank, eps, accel;
+};
+struct Out {
+  double tas, hdg, alt, vs, lat, lon;       // state after the step
+  double ax, delspd, cas, mach, gsnorth, gseast, gs, trk, coslat, az;
+  bool swhdgsel, swaltsel;
+};
+
+__device__ __forceinline__ Out step(const In &s, double simdt, int winddim, double wn, double we) {
+  Out o;
+  // ---- UpdateAirSpeed: speed (traffic.py:427-435)
+  const double delta_spd = s.ptas - s.tas;
+  const double need_ax = fabs(delta_spd) > kKTS ? 1.0 : 0.0;
+  o.ax = need_ax * npsign(delta_spd) * s.accel;
+  o.delspd = delta_spd;
+  const double tas = s.tas + o.ax * simdt;
+  // vatmos(alt) (aero.py:62-74), shared by vtas2cas and vtas2mach
+  const double T = npmax(288.15 - 0.0065 * s.alt, kTstrat);
+  const double rhotrop = 1.225 * pow(T / 288.15, 4.256848030018761);
+  const double dhstrat = npmax(0., s.alt - 11000.);
+  const double rho = rhotrop * exp(-dhstrat / 6341.552161);
+  const double p = rho * kRgas * T;
+  const double qdyn = p * (pow(1. + rho * tas * tas / (7. * p), 3.5) - 1.);
+  double cas = sqrt(7. * kP0 / kRho0 * (pow(qdyn / kP0 + 1., 2. / 7.) - 1.));
+  o.cas = tas < 0 ? -1 * cas : cas;
+  o.mach = tas / sqrt(kGamma * kRgas * T);
+  // turning (traffic.py:438-444)
+  const double turnrate = (kG0 * tan(s.bank) / npmax(tas, s.eps)) * kR2D;
+  const double delhdg = nprem(s.phdg - s.hdg + 180, 360) - 180;
+  o.swhdgsel = fabs(delhdg) > fabs(2 * simdt * turnrate);
+  const double hdg = nprem(s.hdg + simdt * turnrate * (o.swhdgsel ? 1.0 : 0.0) * npsign(delhdg), 360.);
+  // vertical speed (traffic.py:447-454)
+  const double delta_alt = s.palt - s.alt;
+  o.swaltsel = fabs(delta_alt) > npmax(10 * kFT, fabs(2 * simdt * fabs(s.vs)));
+  const double target_vs = (o.swaltsel ? 1.0 : 0.0) * npsign(delta_alt) * fabs(s.pvs);
+  const double delta_vs = target_vs - s.vs;
+  const bool need_az = fabs(delta_vs) > 300 * kFPM;
+  o.az = (need_az ? 1.0 : 0.0) * npsign(delta_vs) * (300 * kFPM);
+  double vs = need_az ? s.vs + o.az * simdt : target_vs;
+  vs = isfinite(vs) ? vs : 0;
+
+  // ---- UpdateGroundSpeed (traffic.py:456-476)
+  if (winddim == 0) {
+    o.gsnorth = tas * cos(hdg * kD2R);
+    o.gseast = tas * sin(hdg * kD2R);
+    o.gs = tas;
+    o.trk = hdg;
+  } else {
+    const double aw = s.alt > 50. * kFT ? 1.0 : 0.0;
+    const double naw = 1.0 - aw;
+    o.gsnorth = tas * cos(hdg * kD2R) + wn * aw;
+    o.gseast = tas * sin(hdg * kD2R) + we * aw;
+    o.gs = naw * tas + aw * sqrt(o.gsnorth * o.gsnorth + o.gseast * o.gseast);
+    o.trk = naw * hdg + nprem(aw * (atan2(o.gseast, o.gsnorth) * kR2D), 360.);
+  }
+
+  // ---- UpdatePosition (traffic.py:480-483)
+  o.alt = o.swaltsel ? s.alt + vs * simdt : s.palt;
+  o.lat = s.lat + (simdt * o.gsnorth / kRearth) * kR2D;
+  o.coslat = cos(o.lat * kD2R);
+  o.lon = s.lon + (simdt * o.gseast / o.coslat / kRearth) * kR2D;
+  o.tas = tas;
+  o.hdg = hdg;
+  o.vs = vs;
+  return o;
+}
+
+}  // namespace kin
+}  // namespace bsa

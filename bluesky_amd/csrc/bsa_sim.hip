@@ -1,0 +1,380 @@
+// GPU-resident sim step and the RCCL row-sharded multi-GPU mode.
+//
+// One step, rows [rb, re) owned by this rank:
+//   every cd_every steps:
+//     C1  all-gather of the 8 state arrays CD/MVP read for other rows
+//         (lat lon trk gs alt vs gseast gsnorth) over xGMI, one RCCL call
+//     K0-K2 detect(own rows x all columns)          asas.py:481-483
+//     K3  MVP on the own rows' pairs, only when some rank has a conflict
+//         (asas.py:486-487 `if self.confpairs`), then asas.active = inconf
+//   every step:
+//     K4' Pilot.APorASAS (no wind, pilot.py:41-63) fused with the kinematic
+//         update (traffic.py:425-483) of the own rows
+#include <rccl/rccl.h>
+
+#include "bsa_kin_math.h"
+
+#pragma clang fp contract(off)
+
+namespace bsa {
+
+#define BSA_NCCL(c, call)                                                                     \
+  do {                                                                                        \
+    ncclResult_t r_ = (call);                                                                 \
+    if (r_ != ncclSuccess)                                                                    \
+      return ::bsa::fail((c), "%s failed: %s (%s:%d)", #call, ncclGetErrorString(r_), __FILE__, \
+                         __LINE__);                                                           \
+  } while (0)
+
+struct SimDev {
+  double *lat, *lon, *trk, *gs, *alt, *vs, *tas, *hdg, *gse, *gsn;
+  const double *aptrk, *aptas, *apalt, *apvs, *bank, *eps, *accel;
+  const double *atrk, *atas, *avs, *aalt;
+  const uint8_t *active;
+};
+
+// Pilot.APorASAS (winddim 0) + UpdateAirSpeed/GroundSpeed/Position, rows [rb, re)
+__global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, SimDev d) {
+  const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= re) return;
+  const bool act = d.active[k] != 0;
+  const double ptrk = act ? d.atrk[k] : d.aptrk[k];   // pilot.py:41
+  kin::In s;
+  s.ptas = act ? d.atas[k] : d.aptas[k];              // pilot.py:38,42
+  s.palt = act ? d.aalt[k] : d.apalt[k];              // pilot.py:43
+  s.pvs = fabs(act ? d.avs[k] : d.apvs[k]);           // pilot.py:44,48
+  s.phdg = kin::nprem(ptrk, 360.);                    // pilot.py:63
+  s.tas = d.tas[k];
+  s.hdg = d.hdg[k];
+  s.alt = d.alt[k];
+  s.vs = d.vs[k];
+  s.lat = d.lat[k];
+  s.lon = d.lon[k];
+  s.bank = d.bank[k];
+  s.eps = d.eps[k];
+  s.accel = d.accel[k];
+  const kin::Out o = kin::step(s, simdt, 0, 0.0, 0.0);
+  d.tas[k] = o.tas;
+  d.hdg[k] = o.hdg;
+  d.alt[k] = o.alt;
+  d.vs[k] = o.vs;
+  d.lat[k] = o.lat;
+  d.lon[k] = o.lon;
+  d.gs[k] = o.gs;
+  d.trk[k] = o.trk;
+  d.gse[k] = o.gseast;
+  d.gsn[k] = o.gsnorth;
+}
+
+__global__ __launch_bounds__(256) void k_copy_active(int nrows, const uint8_t *__restrict__ inconf,
+                                                     uint8_t *__restrict__ active) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < nrows) active[r] = inconf[r];
+}
+
+// field list of one all-gather: fp64 arrays (full n) + optionally one uint8 array
+struct Fields {
+  double *f[8];
+  int nf;
+  uint8_t *u8;  // transported as 0.0 / 1.0 in one extra slot (may be NULL)
+};
+
+__global__ __launch_bounds__(256) void k_pack(int rb, int re, int rpr, Fields fl, double *__restrict__ send) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rpr) return;
+  const int k = rb + r;
+  const bool v = k < re;
+  for (int f = 0; f < fl.nf; ++f) send[(size_t)f * rpr + r] = v ? fl.f[f][k] : 0.0;
+  if (fl.u8) send[(size_t)fl.nf * rpr + r] = v ? (double)fl.u8[k] : 0.0;
+}
+
+__global__ __launch_bounds__(256) void k_unpack(int n, int rpr, int self, Fields fl, int slots,
+                                                const double *__restrict__ recv) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int q = k / rpr, r = k - q * rpr;
+  if (q == self) return;
+  const double *blk = recv + (size_t)q * slots * rpr;
+  for (int f = 0; f < fl.nf; ++f) fl.f[f][k] = blk[(size_t)f * rpr + r];
+  if (fl.u8) fl.u8[k] = blk[(size_t)fl.nf * rpr + r] != 0.0;
+}
+
+static SimDev sim_dev(Ctx *c) {
+  SimDev d;
+  d.lat = (double *)c->own[0].p;
+  d.lon = (double *)c->own[1].p;
+  d.trk = (double *)c->own[2].p;
+  d.gs = (double *)c->own[3].p;
+  d.alt = (double *)c->own[4].p;
+  d.vs = (double *)c->own[5].p;
+  d.tas = (double *)c->s_tas.p;
+  d.hdg = (double *)c->s_hdg.p;
+  d.gse = (double *)c->s_gse.p;
+  d.gsn = (double *)c->s_gsn.p;
+  d.aptrk = (const double *)c->s_aptrk.p;
+  d.aptas = (const double *)c->s_aptas.p;
+  d.apalt = (const double *)c->s_apalt.p;
+  d.apvs = (const double *)c->s_apvs.p;
+  d.bank = (const double *)c->s_bank.p;
+  d.eps = (const double *)c->s_eps.p;
+  d.accel = (const double *)c->s_accel.p;
+  d.atrk = (const double *)c->s_atrk.p;
+  d.atas = (const double *)c->s_atas.p;
+  d.avs = (const double *)c->s_avs.p;
+  d.aalt = (const double *)c->s_aalt.p;
+  d.active = (const uint8_t *)c->s_active.p;
+  return d;
+}
+
+static int allreduce(Ctx *c, double *v, int count, ncclRedOp_t op) {
+  if (!c->comm || c->nranks == 1 || count <= 0) return 0;
+  if (!ensure(c, c->red, (size_t)count * 8, "reduction scratch")) return -1;
+  BSA_HIP(c, hipMemcpyAsync(c->red.p, v, (size_t)count * 8, hipMemcpyHostToDevice, c->stream));
+  BSA_NCCL(c, ncclAllReduce(c->red.p, c->red.p, (size_t)count, ncclDouble, op, (ncclComm_t)c->comm,
+                            c->stream));
+  BSA_HIP(c, hipMemcpyAsync(v, c->red.p, (size_t)count * 8, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// one RCCL all-gather of the listed arrays' rows [sim_rb, sim_re) of every rank
+static int gather_fields(Ctx *c, const Fields &fl) {
+  const int64_t rpr = c->sim_rpr, n = c->n;
+  const int slots = fl.nf + (fl.u8 ? 1 : 0);
+  const size_t blk = (size_t)slots * rpr;
+  if (!ensure(c, c->g_send, blk * 8, "gather send") ||
+      !ensure(c, c->g_recv, blk * 8 * c->nranks, "gather recv"))
+    return -1;
+  hipLaunchKernelGGL(k_pack, dim3((unsigned)((rpr + 255) / 256)), dim3(256), 0, c->stream, (int)c->sim_rb,
+                     (int)c->sim_re, (int)rpr, fl, (double *)c->g_send.p);
+  BSA_HIP(c, hipGetLastError());
+  BSA_NCCL(c, ncclAllGather(c->g_send.p, c->g_recv.p, blk, ncclDouble, (ncclComm_t)c->comm, c->stream));
+  hipLaunchKernelGGL(k_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, (int)n,
+                     (int)rpr, c->rank, fl, slots, (const double *)c->g_recv.p);
+  BSA_HIP(c, hipGetLastError());
+  return 0;
+}
+
+// C1: replicate every rank's rows of the 8 arrays CD and MVP read for any row
+static int sim_gather(Ctx *c) {
+  if (c->nranks == 1 || c->sim_gathered) {
+    c->sim_gathered = true;
+    return 0;
+  }
+  SimDev d = sim_dev(c);
+  Fields fl{{d.lat, d.lon, d.trk, d.gs, d.alt, d.vs, d.gse, d.gsn}, 8, nullptr};
+  if (gather_fields(c, fl)) return -1;
+  c->sim_gathered = true;
+  return 0;
+}
+
+// read-time gather of the per-rank ASAS outputs (only own rows are computed)
+static int sim_gather_asas(Ctx *c) {
+  if (c->nranks == 1) return 0;
+  Fields fl{{(double *)c->s_atrk.p, (double *)c->s_atas.p, (double *)c->s_avs.p, (double *)c->s_aalt.p,
+             (double *)c->s_tas.p, (double *)c->s_hdg.p, nullptr, nullptr},
+            6, (uint8_t *)c->s_active.p};
+  return gather_fields(c, fl);
+}
+
+void sim_release(Ctx *c) {
+  DevBuf *all[] = {&c->red, &c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
+                   &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
+                   &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
+                   &c->s_active, &c->g_send, &c->g_recv};
+  for (auto *b : all) release(*b);
+  if (c->comm) {
+    ncclCommDestroy((ncclComm_t)c->comm);
+    c->comm = nullptr;
+  }
+}
+
+static int sim_cd(Ctx *c) {
+  const bsa_sim_params &p = c->simp;
+  int64_t nc = 0, nl = 0;
+  if (sim_gather(c)) return -1;
+  if (detect(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, &nc, &nl)) return -1;
+  c->sim_last_conf = nc;
+  c->sim_last_los = nl;
+  c->sim_cd_calls++;
+  if (!p.reso) return 0;
+  // asas.py:486-487: resolve only if confpairs is non-empty (globally)
+  double any = (double)nc;
+  if (allreduce(c, &any, 1, ncclSum)) return -1;
+  const int64_t rb = c->sim_rb, nrows = c->sim_re - c->sim_rb;
+  if (any > 0.0) {
+    MvpDev d;
+    d.gseast = (const double *)c->s_gse.p;
+    d.gsnorth = (const double *)c->s_gsn.p;
+    d.vs = (const double *)c->own[5].p;
+    d.alt = (const double *)c->own[4].p;
+    d.trk = (const double *)c->own[2].p;
+    d.gs = (const double *)c->own[3].p;
+    d.selalt = (const double *)c->s_selalt.p;
+    d.apvs = (const double *)c->s_apvs.p;
+    d.noreso = nullptr;
+    d.resooff = nullptr;
+    d.asas_alt = (double *)c->s_aalt.p + rb;
+    d.o_trk = (double *)c->s_atrk.p + rb;
+    d.o_tas = (double *)c->s_atas.p + rb;
+    d.o_vs = (double *)c->s_avs.p + rb;
+    d.o_asase = (float *)c->s_ase.p + rb;
+    d.o_asasn = (float *)c->s_asn.p + rb;
+    d.o_tsolv = nullptr;
+    if (mvp_device(c, p.mvp, d)) return -1;
+  }
+  // asas.active = inconf (build-defined stand-in for ResumeNav)
+  hipLaunchKernelGGL(k_copy_active, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, c->stream,
+                     (int)nrows, (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p + rb);
+  BSA_HIP(c, hipGetLastError());
+  return 0;
+}
+
+}  // namespace bsa
+
+using bsa::Ctx;
+
+extern "C" {
+
+int bsa_comm_unique_id(char *id128) {
+  if (!id128) return -1;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+int bsa_comm_init(bsa_ctx *cc, int nranks, int rank, const char *id128) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!id128 || nranks < 1 || rank < 0 || rank >= nranks) return bsa::fail(c, "bad comm arguments");
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (c->comm) {
+    ncclCommDestroy((ncclComm_t)c->comm);
+    c->comm = nullptr;
+  }
+  ncclUniqueId id;
+  memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t comm;
+  BSA_NCCL(c, ncclCommInitRank(&comm, nranks, id, rank));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  return 0;
+}
+
+int bsa_comm_allreduce_max(bsa_ctx *cc, double *values, int count) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || (!values && count > 0)) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  return bsa::allreduce(c, values, count, ncclMax);
+}
+
+int bsa_comm_allreduce_sum(bsa_ctx *cc, double *values, int count) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || (!values && count > 0)) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  return bsa::allreduce(c, values, count, ncclSum);
+}
+
+int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_params *p) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!s || !p) return bsa::fail(c, "NULL sim state / params");
+  if (n <= 0 || n > 0x7fffffff) return bsa::fail(c, "bad n");
+  if (p->cd_every < 1) return bsa::fail(c, "cd_every must be >= 1");
+  BSA_HIP(c, hipSetDevice(c->device));
+  const double *src[] = {s->lat, s->lon, s->alt, s->tas, s->hdg, s->vs, s->gs, s->trk, s->gseast,
+                         s->gsnorth, s->ap_trk, s->ap_tas, s->ap_alt, s->ap_vs, s->selalt, s->bank,
+                         s->eps, s->accel, s->asas_alt};
+  for (auto q : src)
+    if (!q) return bsa::fail(c, "bsa_sim_init: NULL array");
+  if (bsa_set_state(cc, n, s->lat, s->lon, s->trk, s->gs, s->alt, s->vs)) return -1;
+  bsa::DevBuf *dst[] = {&c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
+                        &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
+                        &c->s_aalt};
+  const double *hs[] = {s->tas, s->hdg, s->gseast, s->gsnorth, s->ap_trk, s->ap_tas, s->ap_alt,
+                        s->ap_vs, s->selalt, s->bank, s->eps, s->accel, s->asas_alt};
+  const size_t N8 = (size_t)n * 8;
+  for (int k = 0; k < 13; ++k) {
+    if (!bsa::ensure(c, *dst[k], N8, "sim state")) return -1;
+    BSA_HIP(c, hipMemcpyAsync(dst[k]->p, hs[k], N8, hipMemcpyHostToDevice, c->stream));
+  }
+  // ASAS arrays: asas.trk/tas start at traf.trk/tas (asas.py:405-409), vs 0, inactive
+  if (!bsa::ensure(c, c->s_atrk, N8, "asas trk") || !bsa::ensure(c, c->s_atas, N8, "asas tas") ||
+      !bsa::ensure(c, c->s_avs, N8, "asas vs") || !bsa::ensure(c, c->s_ase, (size_t)n * 4, "asase") ||
+      !bsa::ensure(c, c->s_asn, (size_t)n * 4, "asasn") || !bsa::ensure(c, c->s_active, n, "active"))
+    return -1;
+  BSA_HIP(c, hipMemcpyAsync(c->s_atrk.p, s->trk, N8, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipMemcpyAsync(c->s_atas.p, s->tas, N8, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipMemsetAsync(c->s_avs.p, 0, N8, c->stream));
+  BSA_HIP(c, hipMemsetAsync(c->s_ase.p, 0, (size_t)n * 4, c->stream));
+  BSA_HIP(c, hipMemsetAsync(c->s_asn.p, 0, (size_t)n * 4, c->stream));
+  BSA_HIP(c, hipMemsetAsync(c->s_active.p, 0, n, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  c->simp = *p;
+  c->sim_rpr = (n + c->nranks - 1) / c->nranks;
+  c->sim_rb = std::min<int64_t>(n, (int64_t)c->rank * c->sim_rpr);
+  c->sim_re = std::min<int64_t>(n, c->sim_rb + c->sim_rpr);
+  c->sim_steps = c->sim_cd_calls = c->sim_last_conf = c->sim_last_los = 0;
+  c->sim_gathered = true;
+  c->sim_ready = true;
+  return 0;
+}
+
+int bsa_sim_step(bsa_ctx *cc, int nsteps) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_step before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  const int64_t rb = c->sim_rb, re = c->sim_re;
+  for (int s = 0; s < nsteps; ++s) {
+    if (c->sim_steps % c->simp.cd_every == 0)
+      if (bsa::sim_cd(c)) return -1;
+    if (re > rb) {
+      hipLaunchKernelGGL(bsa::k_sim_pilot_kin, dim3((unsigned)((re - rb + 255) / 256)), dim3(256), 0,
+                         c->stream, (int)rb, (int)re, c->simp.simdt, bsa::sim_dev(c));
+      BSA_HIP(c, hipGetLastError());
+    }
+    c->sim_gathered = c->nranks == 1;
+    c->sim_steps++;
+  }
+  return 0;
+}
+
+int bsa_sim_read(bsa_ctx *cc, bsa_sim_out *o) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !o) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_read before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (bsa::sim_gather(c) || bsa::sim_gather_asas(c)) return -1;
+  const size_t N8 = (size_t)c->n * 8;
+  struct {
+    void *dst;
+    const void *src;
+    size_t bytes;
+  } cp[] = {{o->lat, c->own[0].p, N8},      {o->lon, c->own[1].p, N8},      {o->alt, c->own[4].p, N8},
+            {o->tas, c->s_tas.p, N8},       {o->hdg, c->s_hdg.p, N8},       {o->vs, c->own[5].p, N8},
+            {o->gs, c->own[3].p, N8},       {o->trk, c->own[2].p, N8},      {o->gseast, c->s_gse.p, N8},
+            {o->gsnorth, c->s_gsn.p, N8},   {o->asas_trk, c->s_atrk.p, N8}, {o->asas_tas, c->s_atas.p, N8},
+            {o->asas_vs, c->s_avs.p, N8},   {o->asas_alt, c->s_aalt.p, N8},
+            {o->active, c->s_active.p, (size_t)c->n}};
+  for (auto &e : cp)
+    if (e.dst) BSA_HIP(c, hipMemcpyAsync(e.dst, e.src, e.bytes, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int bsa_sim_stats(bsa_ctx *cc, int64_t *out6) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !out6) return -1;
+  out6[0] = c->sim_steps;
+  out6[1] = c->sim_cd_calls;
+  out6[2] = c->sim_last_conf;
+  out6[3] = c->sim_last_los;
+  out6[4] = c->sim_rb;
+  out6[5] = c->sim_re;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,73 @@
+"""GPU-resident synthetic sim step over libbsaccel's bsa_sim_*.
+
+State lives in HBM across steps; the host only launches.  One step:
+CD + MVP every ``cd_every`` steps (asas.update, asas.py:473-504, with
+``asas.active = inconf`` standing in for ResumeNav), then Pilot.APorASAS
+(no wind) fused with the kinematic update (traffic.py:397-409).
+With several ranks (one process per GPU) each rank owns a contiguous row
+block and the replicated state is all-gathered over RCCL before each CD.
+"""
+import numpy as np
+
+from . import _lib, dist
+
+FT = 0.3048
+KTS = 0.514444
+NM = 1852.0
+FPM = FT / 60.
+
+
+def initial_state(traf):
+    """Sim state of a freshly created synthetic traffic set (no wind).
+
+    Mirrors Traffic.create (traffic.py:192-312) for what the step reads:
+    tas = gs, hdg = trk, gs components, AP targets = the initial values,
+    ``ap.vs = 1500 fpm`` (traffic.py:289), ``selalt = alt``, bank 25 deg,
+    eps 0.01 (traffic.py:290-308), OpenAP airborne acceleration 0.5 m/s^2
+    (perfoap.py:271-280), ``asas.alt = alt`` (asas.py:405-409).
+    """
+    n = traf.ntraf
+    tas = np.array(traf.gs, dtype=np.float64)
+    hdg = np.array(traf.trk, dtype=np.float64)
+    return dict(lat=np.array(traf.lat, dtype=np.float64), lon=np.array(traf.lon, dtype=np.float64),
+                alt=np.array(traf.alt, dtype=np.float64), tas=tas, hdg=hdg,
+                vs=np.array(traf.vs, dtype=np.float64), gs=tas.copy(), trk=hdg.copy(),
+                gseast=tas * np.sin(np.radians(hdg)), gsnorth=tas * np.cos(np.radians(hdg)),
+                ap_trk=hdg.copy(), ap_tas=tas.copy(), ap_alt=np.array(traf.alt, dtype=np.float64),
+                ap_vs=np.full(n, 1500. * FPM), selalt=np.array(traf.alt, dtype=np.float64),
+                bank=np.full(n, np.radians(25.)), eps=np.full(n, 0.01), accel=np.full(n, 0.5),
+                asas_alt=np.array(traf.alt, dtype=np.float64))
+
+
+def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, reso=True, mar=1.05,
+           swresohoriz=True, swresospd=False, swresohdg=False, swresovert=False, swprio=False,
+           priocode='FF1'):
+    """bsa_sim_params; ASAS defaults of asas.py:81-112 with asas_mar from data/default.cfg."""
+    mvp = _lib.MvpParams(Rm=rpz * mar, dhm=hpz * mar, dtlookahead=tla, vmin=200.0 * NM / 3600.,
+                         vmax=500.0 * NM / 3600., vsmin=-3000. / 60. * FT, vsmax=3000. / 60. * FT,
+                         swresohoriz=int(swresohoriz), swresospd=int(swresospd),
+                         swresohdg=int(swresohdg), swresovert=int(swresovert), swprio=int(swprio),
+                         priocode=_lib.PRIO_CODES.get(priocode, 0), swnoreso=0, swresooff=0)
+    return _lib.SimParams(simdt=simdt, rpz=rpz, hpz=hpz, tla=tla, cd_every=int(cd_every),
+                          reso=int(bool(reso)), mvp=mvp)
+
+
+class ResidentSim:
+    """Device-resident traffic; ``rank``/``world`` > 1 shards the rows over GPUs."""
+
+    def __init__(self, state, p, ctx=None, rank=0, world=1):
+        self.ctx = ctx or _lib.default_context()
+        self.rank, self.world = rank, world
+        if world > 1:
+            dist.init_comm(self.ctx, rank, world)
+        self.ctx.sim_init(state, p)
+        self.params = p
+
+    def step(self, nsteps=1):
+        self.ctx.sim_step(nsteps)
+
+    def read(self):
+        return self.ctx.sim_read()
+
+    def stats(self):
+        return self.ctx.sim_stats()

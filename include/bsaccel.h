@@ -170,6 +170,61 @@ typedef struct bsa_kin_io {
 int bsa_kinematics(bsa_ctx *ctx, int64_t n, double simdt, int winddim,
                    double windnorth, double windeast, bsa_kin_io *io);
 
+/* ---------------------------------------------------------------- multi-GPU
+ * One process per GPU, one context per process.  Rank r owns the contiguous
+ * ownship rows [r*ceil(n/R), min(n, (r+1)*ceil(n/R))) of the resident sim
+ * (SURVEY.md 8e); state is replicated and re-synchronised with one RCCL
+ * all-gather over xGMI before each CD step.  No reference equivalent (the
+ * reference's only distributed backend, bluesky/network/ ZMQ, is out of scope). */
+#define BSA_UNIQUE_ID_BYTES 128
+/* Create a communicator id on one rank (ncclGetUniqueId); ship its 128 bytes
+ * to the other ranks out of band. */
+int bsa_comm_unique_id(char *id128);
+int bsa_comm_init(bsa_ctx *ctx, int nranks, int rank, const char *id128);
+/* Collective: element-wise max of `count` host doubles over all ranks, in
+ * place (also a barrier).  Without a communicator it is a no-op. */
+int bsa_comm_allreduce_max(bsa_ctx *ctx, double *values, int count);
+/* Collective: element-wise sum of `count` host doubles over all ranks. */
+int bsa_comm_allreduce_sum(bsa_ctx *ctx, double *values, int count);
+
+/* ---------------------------------------------------------------- GPU-resident sim
+ * The synthetic sim step of SURVEY.md 8d with all state resident in HBM:
+ *   every cd_every steps: [all-gather] -> detect (own rows) -> MVP (own rows,
+ *                         only if any rank has a conflict, asas.py:486-487)
+ *                         -> asas.active = inconf
+ *   every step:           Pilot.APorASAS (no wind, pilot.py:41-63) fused with
+ *                         UpdateAirSpeed/GroundSpeed/Position (traffic.py:425-483)
+ * AP targets, selalt, bank, eps and perf.acceleration() are frozen inputs. */
+typedef struct bsa_sim_params {
+  double simdt, rpz, hpz, tla;
+  int32_t cd_every; /* >= 1: CD + MVP every k steps (1 = DTNOLOOK=simdt, 20 = asas_dt/simdt) */
+  int32_t reso;     /* 1: MVP resolution + asas.active = inconf; 0: CD only (RESO OFF) */
+  bsa_mvp_params mvp;
+} bsa_sim_params;
+
+typedef struct bsa_sim_state {
+  const double *lat, *lon, *alt, *tas, *hdg, *vs, *gs, *trk, *gseast, *gsnorth;
+  const double *ap_trk, *ap_tas, *ap_alt, *ap_vs, *selalt, *bank, *eps, *accel;
+  const double *asas_alt; /* initial asas.alt (asas.py:405-409 sets it to traf.alt) */
+} bsa_sim_state;
+
+typedef struct bsa_sim_out {
+  double *lat, *lon, *alt, *tas, *hdg, *vs, *gs, *trk, *gseast, *gsnorth;
+  double *asas_trk, *asas_tas, *asas_vs, *asas_alt;
+  uint8_t *active;
+} bsa_sim_out;
+
+/* Upload the full state (length n, all ranks pass the same) and parameters. */
+int bsa_sim_init(bsa_ctx *ctx, int64_t n, const bsa_sim_state *s, const bsa_sim_params *p);
+/* Advance nsteps; collective when a communicator is set. */
+int bsa_sim_step(bsa_ctx *ctx, int nsteps);
+/* Full-n host copies of the state (collective: gathers all ranks' rows).
+ * Any pointer may be NULL. */
+int bsa_sim_read(bsa_ctx *ctx, bsa_sim_out *o);
+/* [0] steps done, [1] CD calls, [2] conflicts and [3] LoS pairs of the last
+ * CD call (this rank's rows), [4] this rank's row_begin, [5] row_end. */
+int bsa_sim_stats(bsa_ctx *ctx, int64_t *out6);
+
 #ifdef __cplusplus
 }
 #endif
