@@ -82,7 +82,7 @@ def main():
         pf.append(tm['prefilter'])
         ex.append(tm['exact'])
         tot.append(tm['total'])
-        kept.append(ctx.last_tiles()[0])
+        kept.append(ctx.last_tiles()[2])      # (128-row x 64-col) groups swept
     ctx.sync()
     ctx.allreduce_max([0.0])     # barrier
     dt_local = time.perf_counter() - t0
@@ -94,7 +94,7 @@ def main():
     pairs = float(n) * n * cd_steps
     value = pairs / dt
     pf_s = float(np.mean(pf)) * 1e-3
-    tested = float(np.mean(kept)) * TILE * TILE
+    tested = float(np.mean(kept)) * 128 * 64   # pair tests the prefilter executed
     roof = dict(bound='valu', kernel='k_prefilter (fp32 VALU reach test, dominant)',
                 achieved=tested * PF_FLOPS_PER_PAIR / pf_s / 1e12, peak=FP32_PEAK_TFLOPS,
                 unit='TFLOP/s')
@@ -112,7 +112,8 @@ def main():
                roofline=roof,
                kernels_ms_rank0=dict(prefilter=float(np.mean(pf)), exact=float(np.mean(ex)),
                                      detect_total=float(np.mean(tot))),
-               tile_pairs_rank0=[float(np.mean(kept)), ctx.last_tiles()[1]],
+               prefilter_pair_tests_rank0=tested,
+               tile_pairs_rank0=list(ctx.last_tiles()[:2]),
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12))
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -48,7 +48,7 @@ SIGNATURES = {
     'bsa_fetch_pairs': (ctypes.c_int, [_vp, _c_i32p, _c_i32p, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
                                        _c_i32p, _c_i32p, _c_u8p, _c_dp]),
     'bsa_last_candidates': (ctypes.c_int, [_vp, _c_i64p]),
-    'bsa_last_tiles': (ctypes.c_int, [_vp, _c_i64p, _c_i64p]),
+    'bsa_last_tiles': (ctypes.c_int, [_vp, _c_i64p, _c_i64p, _c_i64p]),
     'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
 }
 
@@ -243,10 +243,10 @@ class Context:
         return v.value
 
     def last_tiles(self):
-        kept, total = ctypes.c_int64(), ctypes.c_int64()
-        self.check(self.lib.bsa_last_tiles(self.h, ctypes.byref(kept), ctypes.byref(total)),
-                   'bsa_last_tiles')
-        return kept.value, total.value
+        kept, total, groups = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self.check(self.lib.bsa_last_tiles(self.h, ctypes.byref(kept), ctypes.byref(total),
+                                           ctypes.byref(groups)), 'bsa_last_tiles')
+        return kept.value, total.value, groups.value
 
     def last_timings(self):
         t = np.zeros(5)

@@ -216,52 +216,76 @@ __device__ __forceinline__ float wmax(float v) {
   return v;
 }
 
-// one 256-thread block per tile of kTile consecutive sorted records
-__global__ __launch_bounds__(256) void k_tilebox(int cnt, const PFRec *__restrict__ P,
-                                                 TileBox *__restrict__ box) {
-  __shared__ float red[4][10];
-  const int t = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  float v[10];
-  for (int q = 0; q < 5; ++q) {
-    v[q] = INFINITY;        // minima: x y z alt (+1 spare)
-    v[5 + q] = -INFINITY;   // maxima: x y z alt s/h
-  }
+// Bounds of every group of kGroup (= one wave's 64 lanes) consecutive sorted
+// records: one wave per group, lane = record.  NaN coordinates drop out of
+// the min/max (fminf/fmaxf), which is safe: a record with a NaN coordinate
+// never passes the reach test.
+constexpr int kGroup = 64;
+static_assert(kTile % kGroup == 0, "tiles are whole groups");
+
+__global__ __launch_bounds__(256) void k_groupbox(int cnt, const PFRec *__restrict__ P,
+                                                  TileBox *__restrict__ box) {
+  const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+  const int k = g * kGroup + lane;
+  const int ngroups = (cnt + kGroup - 1) / kGroup;
+  if (g >= ngroups) return;  // whole wave exits together
+  float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   float smax = 0.f, hmax = 0.f;
-  const int b0 = t * kTile, b1 = min(cnt, b0 + kTile);
-  for (int k = b0 + tid; k < b1; k += 256) {
+  if (k < cnt) {
     const PFRec p = P[k];
-    v[0] = fminf(v[0], p.x); v[5] = fmaxf(v[5], p.x);
-    v[1] = fminf(v[1], p.y); v[6] = fmaxf(v[6], p.y);
-    v[2] = fminf(v[2], p.z); v[7] = fmaxf(v[7], p.z);
-    v[3] = fminf(v[3], p.alt); v[8] = fmaxf(v[8], p.alt);
-    smax = fmaxf(smax, p.s == p.s ? p.s : INFINITY);
-    hmax = fmaxf(hmax, p.h == p.h ? p.h : INFINITY);
+    lo[0] = hi[0] = p.x;
+    lo[1] = hi[1] = p.y;
+    lo[2] = hi[2] = p.z;
+    lo[3] = hi[3] = p.alt;
+    smax = p.s == p.s ? p.s : INFINITY;
+    hmax = p.h == p.h ? p.h : INFINITY;
   }
-  v[4] = -smax;  // store as minima of negatives
-  v[9] = hmax;
-  for (int q = 0; q < 5; ++q) v[q] = wmin(v[q]);
-  for (int q = 5; q < 10; ++q) v[q] = wmax(v[q]);
-  if (lane == 0)
-    for (int q = 0; q < 10; ++q) red[w][q] = v[q];
-  __syncthreads();
-  if (tid == 0) {
-    for (int ww = 1; ww < 4; ++ww) {
-      for (int q = 0; q < 5; ++q) v[q] = fminf(v[q], red[ww][q]);
-      for (int q = 5; q < 10; ++q) v[q] = fmaxf(v[q], red[ww][q]);
-    }
+  for (int q = 0; q < 4; ++q) {
+    lo[q] = wmin(lo[q]);
+    hi[q] = wmax(hi[q]);
+  }
+  smax = wmax(smax);
+  hmax = wmax(hmax);
+  if (lane == 0) {
     TileBox b;
     for (int q = 0; q < 3; ++q) {
-      b.lo[q] = v[q];
-      b.hi[q] = v[5 + q];
+      b.lo[q] = lo[q];
+      b.hi[q] = hi[q];
     }
-    b.altlo = v[3];
-    b.althi = v[8];
-    b.smax = -v[4];
-    b.hmax = v[9];
-    b.count = b1 - b0;
+    b.altlo = lo[3];
+    b.althi = hi[3];
+    b.smax = smax;
+    b.hmax = hmax;
+    b.count = min(kGroup, cnt - g * kGroup);
     b.pad = 0;
-    box[t] = b;
+    box[g] = b;
   }
+}
+
+__device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b) {
+  TileBox u;
+  for (int q = 0; q < 3; ++q) {
+    u.lo[q] = fminf(a.lo[q], b.lo[q]);
+    u.hi[q] = fmaxf(a.hi[q], b.hi[q]);
+  }
+  u.altlo = fminf(a.altlo, b.altlo);
+  u.althi = fmaxf(a.althi, b.althi);
+  u.smax = fmaxf(a.smax, b.smax);
+  u.hmax = fmaxf(a.hmax, b.hmax);
+  u.count = a.count + b.count;
+  u.pad = 0;
+  return u;
+}
+
+// tile box = union of its kTile / kGroup group boxes
+__global__ __launch_bounds__(256) void k_tileunion(int ntiles, int ngroups, const TileBox *__restrict__ g,
+                                                   TileBox *__restrict__ t) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ntiles) return;
+  const int g0 = k * (kTile / kGroup), g1 = min(ngroups, g0 + kTile / kGroup);
+  TileBox u = g[g0];
+  for (int q = g0 + 1; q < g1; ++q) u = box_union(u, g[q]);
+  t[k] = u;
 }
 
 // ------------------------------------------------------------------ K0d tile pairs
@@ -313,7 +337,6 @@ __global__ __launch_bounds__(256) void k_tilepairs(int nrt, int nct, const TileB
 
 // ------------------------------------------------------------------ K1a prefilter
 constexpr int PF_BLOCK = 256;
-constexpr int PF_QCAP = 512;                 // per-wave candidate queue (4 KiB)
 constexpr int PF_WAVES = PF_BLOCK / 64;
 static_assert(kTile == 2 * PF_BLOCK, "2 rows per lane");
 
@@ -336,65 +359,29 @@ __device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long 
   return ((unsigned long long)hi << 32) | lo;
 }
 
-// one ownship row held in registers for the sweep
-struct RowPF {
-  PFRec p;
-  float ex, ey, nx, ny, nz;  // local east / north basis at the row position
-  float vs;
-  bool refine;               // basis well conditioned and no quirk flag
-};
+typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ RowPF load_row(const PFRec *__restrict__ P, const PFAux *__restrict__ A,
-                                          int k, int cnt) {
-  RowPF r;
-  if (k < cnt) {
-    r.p = P[k];
-    const PFAux a = A[k];
-    r.vs = a.vs;
-    const float rho = sqrtf(r.p.x * r.p.x + r.p.y * r.p.y);
-    r.refine = (a.flags == 0) && rho > 1e-2f;
-    const float ir = r.refine ? 1.f / rho : 0.f;
-    r.ex = -r.p.y * ir;
-    r.ey = r.p.x * ir;
-    r.nx = -r.p.z * r.p.x * ir;
-    r.ny = -r.p.z * r.p.y * ir;
-    r.nz = rho;
-  } else {
-    const float qnan = __builtin_nanf("");
-    r.p.x = r.p.y = r.p.z = qnan;   // NaN never passes a test
-    r.p.s = r.p.alt = r.p.h = r.p.u = r.p.v = 0.f;
-    r.vs = 0.f;
-    r.refine = false;
-    r.ex = r.ey = r.nx = r.ny = r.nz = 0.f;
-  }
-  return r;
-}
-
-// stage 1: conservative reach test (keeps every pair that can be a conflict
-// or a loss of separation; proof in DESIGN.md)
-__device__ __forceinline__ bool pf_reach(const PFRec &a, const PFRec &c) {
-  const float dx = c.x - a.x, dy = c.y - a.y, dz = c.z - a.z;
-  const float d2 = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
-  const float st = a.s + c.s;
-  const float dh = __builtin_fabsf(c.alt - a.alt);
-  return (d2 < st * st) & (dh < a.h + c.h);
-}
-
-// stage 2: conservative closest-approach refine.  Returns false only when no
-// t in [0, max(tla,0)] can lie in both the vertical and horizontal windows of
-// the reference's geometry (DESIGN.md "CPA refine"); NaN keeps the pair.
-__device__ __forceinline__ bool pf_refine(const RowPF &r, const PFRec &c, float cvs, unsigned cflags,
-                                          const RefineParams &rp) {
-  if (!r.refine || cflags) return true;
-  const float dx = c.x - r.p.x, dy = c.y - r.p.y, dz = c.z - r.p.z;
+// stage 2: conservative closest-approach refine of one (row, column) pair.
+// Returns false only when no t in [0, max(tla,0)] can lie in both the
+// vertical and the horizontal window of the reference's geometry
+// (DESIGN.md "CPA refine"); any NaN keeps the pair.
+__device__ __forceinline__ bool pf_refine(const PFRec &r, const PFAux &ra, const PFRec &c,
+                                          const PFAux &ca, const RefineParams &rp) {
+  if (ra.flags | ca.flags) return true;
+  const float rho = sqrtf(r.x * r.x + r.y * r.y);
+  if (!(rho > 1e-2f)) return true;                         // basis ill-conditioned near a pole
+  const float ir = 1.f / rho;
+  const float ex = -r.y * ir, ey = r.x * ir;               // local east at the row position
+  const float nx = -r.z * r.x * ir, ny = -r.z * r.y * ir, nz = rho;  // local north
+  const float dx = c.x - r.x, dy = c.y - r.y, dz = c.z - r.z;
   if (dx * dx + dy * dy + dz * dz > 0.04f) return true;   // > ~1270 km: keep, no refine
-  const float pe = (dx * r.ex + dy * r.ey) * kRS;
-  const float pn = (dx * r.nx + dy * r.ny + dz * r.nz) * kRS;
-  const float ve = c.u - r.p.u, vn = c.v - r.p.v;          // own.u[j] - int.u[i]
+  const float pe = (dx * ex + dy * ey) * kRS;
+  const float pn = (dx * nx + dy * ny + dz * nz) * kRS;
+  const float ve = c.u - r.u, vn = c.v - r.v;              // own.u[j] - int.u[i]
   const float vv = ve * ve + vn * vn;
   if (!(vv >= 4e-6f)) return true;                         // reference may clamp dv2
-  const float dalt = c.alt - r.p.alt;                      // own.alt[j] - int.alt[i]
-  const float dvs = cvs - r.vs;
+  const float dalt = c.alt - r.alt;                        // own.alt[j] - int.alt[i]
+  const float dvs = ca.vs - ra.vs;
   const float adv = __builtin_fabsf(dvs);
   float t0 = 0.f, t1 = rp.T;
   if (adv < 1e-3f) {
@@ -415,6 +402,25 @@ __device__ __forceinline__ bool pf_refine(const RowPF &r, const PFRec &c, float 
   return !(qe * qe + qn * qn > rp.lim2);
 }
 
+// can any pair of the two boxes pass the reach test?  (gap bounds the chord /
+// |dalt| from below; s_i + s_j <= smax_a + smax_b, h_i + h_j <= hmax_a + hmax_b)
+__device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileBox &b) {
+  const float gx = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]);
+  const float gy = gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]);
+  const float gz = gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]);
+  const float d2 = gx * gx + gy * gy + gz * gz;
+  const float st = (a.smax + b.smax) * 1.00001f + 1e-6f;
+  const float ga = gap(a.altlo, a.althi, b.altlo, b.althi);
+  return !(d2 >= st * st) && !(ga >= (a.hmax + b.hmax) * 1.00001f + 1e-3f);
+}
+
+constexpr int PF_Q1 = 1024;  // per-wave stage-1 queue: u32 (row_local << 16 | col_local)
+constexpr int PF_Q2 = 256;   // per-wave stage-2 queue: uint2 (sorted row, sorted column)
+constexpr int PF_WROWS = 128;  // rows per wave (2 per lane)
+constexpr int kWorkShards = 8;   // one dequeue counter per XCD group
+constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
+static_assert(PF_WAVES * PF_WROWS == kTile, "4 waves x 128 rows = one row block");
+
 __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 *__restrict__ cand,
                                          unsigned long long *__restrict__ count,
                                          unsigned long long cap) {
@@ -427,62 +433,132 @@ __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 
   __builtin_amdgcn_wave_barrier();
 }
 
+// K1a: each wave sweeps its 128 rows against the 512 columns of a tile pair
+// in 64-column groups (a group is skipped when the wave's row box and the
+// group box cannot interact).  Stage 1 (packed fp32 reach test, 2 rows per
+// lane) pushes survivors into an LDS queue; the queue is drained with all 64
+// lanes busy through stage 2 (refine), whose survivors go to a second queue
+// that is flushed to HBM with one atomic per flush.
+template <bool NOPRUNE>
 __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     const PFRec *__restrict__ prow, const PFAux *__restrict__ arow, int nrows,
     const PFRec *__restrict__ pcol, const PFAux *__restrict__ acol, int ncols,
-    const uint2 *__restrict__ tiles, const unsigned long long *__restrict__ ntiles_p,
-    RefineParams rp, int noprune, uint2 *__restrict__ cand,
-    unsigned long long *__restrict__ cand_count, unsigned long long cap) {
-  __shared__ PFRec tile[kTile];
-  __shared__ PFAux aux[kTile];
-  __shared__ uint2 queue[PF_WAVES][PF_QCAP];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const unsigned long long ntiles = *ntiles_p;
-  uint2 *q = queue[w];
-  unsigned qn = 0;  // wave-uniform queue fill
-  for (unsigned long long tp = blockIdx.x; tp < ntiles; tp += gridDim.x) {
-    const uint2 rc = tiles[tp];
-    const int r0 = (int)rc.x * kTile + tid, r1 = r0 + PF_BLOCK;
-    const RowPF a = load_row(prow, arow, r0, nrows);
-    const RowPF b = load_row(prow, arow, r1, nrows);
-    const int c0 = (int)rc.y * kTile;
-    const int nt = min(kTile, ncols - c0);
-    __syncthreads();
-    for (int k = tid; k < nt; k += PF_BLOCK) {
-      tile[k] = pcol[c0 + k];
-      aux[k] = acol[c0 + k];
-    }
-    __syncthreads();
-    for (int jj = 0; jj < nt; ++jj) {
-      const PFRec c = tile[jj];
-      bool ka, kb;
-      if (noprune) {
-        ka = r0 < nrows;
-        kb = r1 < nrows;
-      } else {
-        ka = pf_reach(a.p, c);
-        kb = pf_reach(b.p, c);
-        if (__ballot(ka | kb)) {
-          const PFAux ca = aux[jj];
-          if (ka) ka = pf_refine(a, c, ca.vs, ca.flags, rp);
-          if (kb) kb = pf_refine(b, c, ca.vs, ca.flags, rp);
+    const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ gbox_c,
+    const uint2 *__restrict__ tiles, Counters *__restrict__ cnt,
+    unsigned long long *__restrict__ work, RefineParams rp,
+    uint2 *__restrict__ cand, unsigned long long cap) {
+  __shared__ unsigned q1s[PF_WAVES][PF_Q1];
+  __shared__ uint2 q2s[PF_WAVES][PF_Q2];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned long long ntiles = cnt->tiles;
+  unsigned *q1 = q1s[w];
+  uint2 *q2 = q2s[w];
+  unsigned n2 = 0;        // wave-uniform
+  unsigned groups = 0;    // 64-column groups swept by this wave (for the roofline)
+  const float qnan = __builtin_nanf("");
+  // Dynamic work distribution: an item is one (tile pair, 128-row slice);
+  // each wave dequeues items from the counter of its XCD group (blockIdx % 8)
+  // so no single word takes every dequeue (MI355X_MICROARCH 'dequeue').
+  const unsigned long long nitems = ntiles * PF_WAVES;
+  const unsigned shard = blockIdx.x & (kWorkShards - 1);
+  unsigned long long *wq = work + shard * kWorkStride;
+  for (;;) {
+    unsigned long long m = 0;
+    if (lane == 0) m = atomicAdd(wq, 1ull);
+    const unsigned long long item = wave_bcast_u64(m) * kWorkShards + shard;
+    if (item >= nitems) break;
+    const uint2 rc = tiles[item / PF_WAVES];
+    const int rbase = (int)rc.x * kTile + (int)(item % PF_WAVES) * PF_WROWS;
+    if (rbase >= nrows) continue;
+    const int cbase = (int)rc.y * kTile;
+    const int ka_row = rbase + lane, kb_row = rbase + 64 + lane;
+    const bool va = ka_row < nrows, vb = kb_row < nrows;
+    PFRec A, B;
+    if (va) A = prow[ka_row]; else { A.x = A.y = A.z = qnan; A.s = A.alt = A.h = A.u = A.v = 0.f; }
+    if (vb) B = prow[kb_row]; else { B.x = B.y = B.z = qnan; B.s = B.alt = B.h = B.u = B.v = 0.f; }
+    const f2 X = {A.x, B.x}, Y = {A.y, B.y}, Z = {A.z, B.z};
+    const f2 S = {A.s, B.s}, AL = {A.alt, B.alt}, HH = {A.h, B.h};
+    TileBox rbx = gbox_r[rbase / kGroup];
+    if (rbase + 64 < nrows) rbx = box_union(rbx, gbox_r[rbase / kGroup + 1]);
+    unsigned n1 = 0;  // wave-uniform
+    const int ng = min(kTile / kGroup, (ncols - cbase + kGroup - 1) / kGroup);
+
+    auto drain = [&]() {
+      __builtin_amdgcn_wave_barrier();
+      for (unsigned b0 = 0; b0 < n1; b0 += 64) {
+        const unsigned k = b0 + lane;
+        bool keep = false;
+        unsigned gi = 0, gj = 0;
+        if (k < n1) {
+          const unsigned e = q1[k];
+          gi = (unsigned)rbase + (e >> 16);
+          gj = (unsigned)cbase + (e & 0xffffu);
+          keep = NOPRUNE ? true : pf_refine(prow[gi], arow[gi], pcol[gj], acol[gj], rp);
         }
+        const unsigned long long m = __ballot(keep);
+        if (m) {
+          if (keep) q2[n2 + lane_prefix(m)] = make_uint2(gi, gj);
+          n2 = __builtin_amdgcn_readfirstlane(n2 + (unsigned)__popcll(m));
+          if (n2 > (unsigned)(PF_Q2 - 64)) {
+            pf_flush(q2, n2, lane, cand, &cnt->cand, cap);
+            n2 = 0;
+          }
+        }
+      }
+      n1 = 0;
+      __builtin_amdgcn_wave_barrier();
+    };
+
+    // stage 1 for one column record, packed over the lane's two rows
+    auto visit = [&](const PFRec &c, unsigned cl) {
+      bool ka, kb;
+      if (NOPRUNE) {
+        ka = va;
+        kb = vb;
+      } else {
+        const f2 dx = (f2){c.x, c.x} - X, dy = (f2){c.y, c.y} - Y, dz = (f2){c.z, c.z} - Z;
+        f2 d2 = dx * dx;
+        d2 = __builtin_elementwise_fma(dy, dy, d2);
+        d2 = __builtin_elementwise_fma(dz, dz, d2);
+        const f2 st = S + (f2){c.s, c.s};
+        const f2 st2 = st * st;
+        const f2 dh = (f2){c.alt, c.alt} - AL;
+        const f2 hh = HH + (f2){c.h, c.h};
+        ka = (d2.x < st2.x) & (__builtin_fabsf(dh.x) < hh.x);
+        kb = (d2.y < st2.y) & (__builtin_fabsf(dh.y) < hh.y);
       }
       const unsigned long long ma = __ballot(ka), mb = __ballot(kb);
       if (ma | mb) {
-        const unsigned j = (unsigned)(c0 + jj);
-        if (ka) q[qn + lane_prefix(ma)] = make_uint2((unsigned)r0, j);
-        qn += (unsigned)__popcll(ma);
-        if (kb) q[qn + lane_prefix(mb)] = make_uint2((unsigned)r1, j);
-        qn += (unsigned)__popcll(mb);
-        if (qn > (unsigned)(PF_QCAP - 2 * 64)) {
-          pf_flush(q, qn, lane, cand, cand_count, cap);
-          qn = 0;
+        if (ka) q1[n1 + lane_prefix(ma)] = ((unsigned)lane << 16) | cl;
+        n1 = __builtin_amdgcn_readfirstlane(n1 + (unsigned)__popcll(ma));
+        if (kb) q1[n1 + lane_prefix(mb)] = ((unsigned)(64 + lane) << 16) | cl;
+        n1 = __builtin_amdgcn_readfirstlane(n1 + (unsigned)__popcll(mb));
+        if (n1 > (unsigned)(PF_Q1 - 2 * 64)) drain();
+      }
+    };
+
+    for (int g = 0; g < ng; ++g) {
+      const int c0 = cbase + g * kGroup;
+      if (!NOPRUNE && !boxes_may_interact(rbx, gbox_c[c0 / kGroup])) continue;
+      ++groups;
+      const int nc = min(kGroup, ncols - c0);
+      const unsigned cl0 = (unsigned)(g * kGroup);
+      if (nc == kGroup) {
+        for (int j0 = 0; j0 < kGroup; j0 += 4) {
+          PFRec cc[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) cc[u] = pcol[c0 + j0 + u];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) visit(cc[u], cl0 + j0 + u);
         }
+      } else {
+        for (int jj = 0; jj < nc; ++jj) visit(pcol[c0 + jj], cl0 + jj);
       }
     }
+    if (n1) drain();
   }
-  if (qn) pf_flush(q, qn, lane, cand, cand_count, cap);
+  if (n2) pf_flush(q2, n2, lane, cand, &cnt->cand, cap);
+  if (lane == 0 && groups) atomicAdd(&cnt->groups, (unsigned long long)groups);
 }
 
 // ------------------------------------------------------------------ K1b exact
@@ -740,14 +816,21 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   // ---- K0c/K0d tile culling
   const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
   const long long ntp = (long long)nrt * nct;
+  const int ngr = (int)((nrows + kGroup - 1) / kGroup), ngc = (int)((n + kGroup - 1) / kGroup);
   if (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
       !ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
+      !ensure(c, c->gbox_r, ngr * sizeof(TileBox), "row group boxes") ||
+      !ensure(c, c->gbox_c, ngc * sizeof(TileBox), "column group boxes") ||
       !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
     return -1;
-  hipLaunchKernelGGL(k_tilebox, dim3(nrt), dim3(256), 0, c->stream, (int)nrows, (const PFRec *)c->pfrow.p,
-                     (TileBox *)c->tbox_r.p);
-  hipLaunchKernelGGL(k_tilebox, dim3(nct), dim3(256), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
-                     (TileBox *)c->tbox_c.p);
+  hipLaunchKernelGGL(k_groupbox, dim3(blocks_for(ngr, 4)), dim3(256), 0, c->stream, (int)nrows,
+                     (const PFRec *)c->pfrow.p, (TileBox *)c->gbox_r.p);
+  hipLaunchKernelGGL(k_groupbox, dim3(blocks_for(ngc, 4)), dim3(256), 0, c->stream, (int)n,
+                     (const PFRec *)c->pfcol.p, (TileBox *)c->gbox_c.p);
+  hipLaunchKernelGGL(k_tileunion, dim3(blocks_for(nrt, 256)), dim3(256), 0, c->stream, nrt, ngr,
+                     (const TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p);
+  hipLaunchKernelGGL(k_tileunion, dim3(blocks_for(nct, 256)), dim3(256), 0, c->stream, nct, ngc,
+                     (const TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p);
   BSA_HIP(c, hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
   Counters *dcnt = (Counters *)c->counters.p;
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + 255) / 256)), dim3(256), 0, c->stream, nrt, nct,
@@ -772,14 +855,28 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
       return -1;
     // ---- K1a prefilter over surviving tile pairs (persistent grid, count read on device)
     BSA_HIP(c, hipMemsetAsync(&dcnt->cand, 0, 24, c->stream));  // cand, conf, los
+    BSA_HIP(c, hipMemsetAsync(&dcnt->groups, 0, 8, c->stream));
+    if (!ensure(c, c->workq, kWorkShards * kWorkStride * 8, "work counters")) return -1;
+    BSA_HIP(c, hipMemsetAsync(c->workq.p, 0, kWorkShards * kWorkStride * 8, c->stream));
     BSA_HIP(c, hipMemsetAsync(c->inconf.p, 0, nrows, c->stream));
     BSA_HIP(c, hipMemsetAsync(c->tcpamax.p, 0, nrows * 8, c->stream));
-    const unsigned pf_grid = (unsigned)std::min<long long>(ntp, 256 * 6);
-    hipLaunchKernelGGL(k_prefilter, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
-                       (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
-                       (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
-                       (const uint2 *)c->tilepairs.p, &dcnt->tiles, rp, noprune, (uint2 *)c->cand.p,
-                       &dcnt->cand, c->cand_cap);
+    // persistent grid: 6 workgroups per CU (LDS/SGPR-limited residency); at
+    // least one workgroup per dequeue shard so every shard's items are taken
+    const unsigned pf_grid = (unsigned)std::max<long long>(kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * 6));
+    if (noprune)
+      hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
+                         (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
+                         (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
+                         (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
+                         (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
+                         (uint2 *)c->cand.p, c->cand_cap);
+    else
+      hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
+                         (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
+                         (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
+                         (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
+                         (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
+                         (uint2 *)c->cand.p, c->cand_cap);
     BSA_HIP(c, hipGetLastError());
     BSA_HIP(c, hipEventRecord(c->ev[2], c->stream));
     // ---- K1b exact evaluation (grid-stride, count read on device)
@@ -802,6 +899,7 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   c->last_cand = (int64_t)h.cand;
   c->last_tiles = (int64_t)h.tiles;
   c->last_tiles_total = ntp;
+  c->last_groups = (int64_t)h.groups;
 
   // ---- K2 canonical row-major order
   const int64_t P = (int64_t)h.conf, L = (int64_t)h.los;

@@ -128,6 +128,7 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage,
                         &c->pfauxrow, &c->pfauxcol, &c->key_r, &c->idx_r, &c->key_r2, &c->perm_r,
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
+                        &c->gbox_r, &c->gbox_c, &c->workq,
                         &c->tilepairs};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);
@@ -227,10 +228,11 @@ int bsa_last_candidates(bsa_ctx *c, int64_t *n_candidates) {
   return 0;
 }
 
-int bsa_last_tiles(bsa_ctx *c, int64_t *kept, int64_t *total) {
-  if (!c || !kept || !total) return -1;
+int bsa_last_tiles(bsa_ctx *c, int64_t *kept, int64_t *total, int64_t *groups) {
+  if (!c || !kept || !total || !groups) return -1;
   *kept = c->last_tiles;
   *total = c->last_tiles_total;
+  *groups = c->last_groups;
   return 0;
 }
 

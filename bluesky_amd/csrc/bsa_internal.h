@@ -85,7 +85,8 @@ struct Counters {
   unsigned long long conf;
   unsigned long long los;
   unsigned long long tiles;
-  unsigned long long pad[4];
+  unsigned long long groups;  // (128-row x 64-column) groups swept by the prefilter
+  unsigned long long pad[3];
 };
 
 // ---------------------------------------------------------------- buffers
@@ -111,7 +112,7 @@ struct Ctx {
   DevBuf rowrec, colrec, pfrow, pfcol, pfauxrow, pfauxcol;
   // spatial order: Morton keys and the sorted-position -> original-index maps
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
-  DevBuf tbox_r, tbox_c, tilepairs;
+  DevBuf tbox_r, tbox_c, gbox_r, gbox_c, tilepairs, workq;
 
   // detect buffers
   DevBuf counters;           // Counters
@@ -129,7 +130,8 @@ struct Ctx {
 
   // last detect
   int64_t last_rb = 0, last_re = 0;
-  int64_t last_conf = 0, last_los = 0, last_cand = 0, last_tiles = 0, last_tiles_total = 0;
+  int64_t last_conf = 0, last_los = 0, last_cand = 0, last_tiles = 0, last_tiles_total = 0,
+          last_groups = 0;
   int last_flags = 0;
   bool have_pairs = false;
 

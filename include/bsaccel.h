@@ -104,8 +104,9 @@ int bsa_fetch_pairs(bsa_ctx *ctx,
 int bsa_last_candidates(bsa_ctx *ctx, int64_t *n_candidates);
 
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
- * bounding-box cull, and the total number of tile pairs. */
-int bsa_last_tiles(bsa_ctx *ctx, int64_t *kept, int64_t *total);
+ * bounding-box cull, the total number of tile pairs, and the number of
+ * (128-row x 64-column) groups the prefilter actually swept. */
+int bsa_last_tiles(bsa_ctx *ctx, int64_t *kept, int64_t *total, int64_t *groups);
 
 /* Device time of the last detect's stages in milliseconds, measured with
  * HIP events on the context stream: [0] spatial order + records + tile cull,
