@@ -1,0 +1,62 @@
+"""CPU: host-side drop-in plumbing that needs no GPU."""
+import types
+
+import numpy as np
+import pytest
+
+import bluesky_amd
+from bluesky_amd import _lib, kinematics, mvp, resident, statebased, synth
+
+
+def test_register_uses_asas_plugin_api():
+    calls = {}
+
+    class FakeASAS:
+        @classmethod
+        def addCDMethod(cls, name, module):
+            calls['cd'] = (name, module)
+
+        @classmethod
+        def addCRMethod(cls, name, module):
+            calls['cr'] = (name, module)
+
+    bluesky_amd.register(FakeASAS)
+    assert calls['cd'] == ('GPU', statebased)
+    assert calls['cr'] == ('GPUMVP', mvp)
+    assert callable(statebased.detect) and callable(mvp.resolve) and callable(mvp.start)
+
+
+def test_pairs_from_indices():
+    ids = ['A', 'B', 'C']
+    assert statebased.pairs_from_indices(ids, np.array([0, 2]), np.array([1, 0])) == [('A', 'B'), ('C', 'A')]
+    assert statebased.pairs_from_indices(ids, np.array([], int), np.array([], int)) == []
+
+
+def test_mvp_params_from_asas():
+    asas = types.SimpleNamespace(Rm=1.05 * 9260, dhm=1.05 * 304.8, dtlookahead=300.0, vmin=100.0,
+                                 vmax=250.0, vsmin=-15.0, vsmax=15.0, swresohoriz=True,
+                                 swresospd=False, swresohdg=True, swresovert=False, swprio=True,
+                                 priocode='LAY2', swnoreso=False, swresooff=True)
+    p = mvp.params_from_asas(asas)
+    assert p.priocode == 5 and p.swresohdg == 1 and p.swresooff == 1 and p.Rm == asas.Rm
+
+
+def test_resident_initial_state_matches_traffic_create():
+    t = synth.box(100, 50.0, seed=3)
+    s = resident.initial_state(t)
+    assert set(_lib.SIM_STATE_FIELDS) <= set(s)
+    assert np.allclose(s['ap_vs'], 1500 * 0.3048 / 60.)
+    assert np.array_equal(s['tas'], t.gs) and np.array_equal(s['hdg'], t.trk)
+
+
+def test_kinematics_rejects_wind_fields():
+    traf = types.SimpleNamespace(wind=types.SimpleNamespace(winddim=2))
+    with pytest.raises((NotImplementedError, _lib.AccelUnavailable)):
+        kinematics.step(traf, 0.05, ctx=types.SimpleNamespace())
+
+
+def test_workloads():
+    t = synth.workload('box100k', n=2000)
+    assert t.ntraf == 2000 and len(t.id) == 2000
+    g = synth.global_traffic(5000, seed=1)
+    assert np.all(np.abs(g.lat) <= 70.5)
