@@ -645,7 +645,7 @@ __global__ __launch_bounds__(256) void k_exact(
     unsigned long long *__restrict__ ckey, unsigned *__restrict__ cval, double *__restrict__ cpay,
     unsigned long long conf_cap, unsigned long long *__restrict__ lkey, unsigned long long los_cap,
     Counters *__restrict__ cnt, unsigned char *__restrict__ inconf,
-    unsigned long long *__restrict__ tcpamax_bits) {
+    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int nrows) {
   const int lane = threadIdx.x & 63;
   const unsigned long long ncand = min(*ncand_p, cand_cap);
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
@@ -671,7 +671,6 @@ __global__ __launch_bounds__(256) void k_exact(
         const unsigned long long slot = base + lane_prefix(mc);
         if (slot < conf_cap) {
           ckey[slot] = key;
-          cval[slot] = (unsigned)slot;
           cpay[0 * conf_cap + slot] = o.qdr;
           cpay[1 * conf_cap + slot] = o.dist;
           cpay[2 * conf_cap + slot] = o.tcpa;
@@ -680,6 +679,7 @@ __global__ __launch_bounds__(256) void k_exact(
         }
         const int row = (int)oi - rb;
         inconf[row] = 1;
+        atomicAdd(&rowcnt[row], 1u);                 // K2 counting sort, conflicts
         // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
         // positive tcpa can raise it, and positive doubles order as integers.
         if (o.tcpa > 0.0)
@@ -695,43 +695,115 @@ __global__ __launch_bounds__(256) void k_exact(
       if (los) {
         const unsigned long long slot = base + lane_prefix(ml);
         if (slot < los_cap) lkey[slot] = key;
+        atomicAdd(&rowcnt[nrows + 1 + ((int)oi - rb)], 1u);  // K2 counting sort, LoS
       }
     }
   }
 }
 
-// ------------------------------------------------------------------ K2 gather
-__global__ __launch_bounds__(256) void k_gather_conf(
-    int64_t P, const unsigned long long *__restrict__ key, const unsigned *__restrict__ val,
-    const double *__restrict__ pay, unsigned long long cap, int *__restrict__ ci,
-    int *__restrict__ cj, double *__restrict__ out) {
+// ------------------------------------------------------------------ K2 canonical order
+// Per-row counting sort.  rowcnt holds [conflicts per row | 0 | LoS per row | 0]
+// (2 * (nrows + 1) words); its exclusive scan gives each row's segment in the
+// conflict list and (minus P) in the LoS list.  Pairs are scattered into their
+// row segment, then one lane per row sorts its (short) segment by column:
+// the result is exactly np.where's row-major order (StateBasedCD.py:93-95).
+__global__ __launch_bounds__(256) void k_scatter(int64_t P, int64_t L, int rb, int nrows,
+                                                 const unsigned long long *__restrict__ ckey,
+                                                 const unsigned long long *__restrict__ lkey,
+                                                 const unsigned *__restrict__ rowoff,
+                                                 unsigned *__restrict__ rowcnt,
+                                                 unsigned *__restrict__ cslot,
+                                                 unsigned *__restrict__ lslot) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= P) return;
-  const unsigned long long kk = key[k];
-  const unsigned s = val[k];
-  ci[k] = (int)(kk >> 32);
-  cj[k] = (int)(kk & 0xffffffffull);
-#pragma unroll
-  for (int f = 0; f < 5; ++f) out[f * P + k] = pay[f * cap + s];
+  if (k < P) {
+    const int row = (int)(ckey[k] >> 32) - rb;
+    const unsigned pos = rowoff[row] + atomicSub(&rowcnt[row], 1u) - 1u;
+    cslot[pos] = (unsigned)k;
+  } else if (k < P + L) {
+    const int64_t s = k - P;
+    const int r = nrows + 1 + ((int)(lkey[s] >> 32) - rb);
+    const unsigned pos = rowoff[r] - (unsigned)P + atomicSub(&rowcnt[r], 1u) - 1u;
+    lslot[pos] = (unsigned)s;
+  }
 }
 
-__global__ __launch_bounds__(256) void k_split_los(int64_t L, const unsigned long long *__restrict__ key,
-                                                   int *__restrict__ li, int *__restrict__ lj) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= L) return;
-  const unsigned long long kk = key[k];
-  li[k] = (int)(kk >> 32);
-  lj[k] = (int)(kk & 0xffffffffull);
+__global__ __launch_bounds__(256) void k_rowsort(int nrows, int64_t P, const unsigned *__restrict__ rowoff,
+                                                 const unsigned long long *__restrict__ ckey,
+                                                 unsigned *__restrict__ cslot,
+                                                 const double *__restrict__ cpay, unsigned long long cap,
+                                                 const unsigned long long *__restrict__ lkey,
+                                                 unsigned *__restrict__ lslot, int *__restrict__ ci,
+                                                 int *__restrict__ cj, double *__restrict__ out,
+                                                 int *__restrict__ li, int *__restrict__ lj) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  // conflicts of row r
+  {
+    const unsigned b = rowoff[r], e = rowoff[r + 1];
+    for (unsigned x = b + 1; x < e; ++x) {  // insertion sort by column
+      const unsigned v = cslot[x];
+      const unsigned kv = (unsigned)(ckey[v] & 0xffffffffull);
+      unsigned y = x;
+      while (y > b && (unsigned)(ckey[cslot[y - 1]] & 0xffffffffull) > kv) {
+        cslot[y] = cslot[y - 1];
+        --y;
+      }
+      cslot[y] = v;
+    }
+    for (unsigned x = b; x < e; ++x) {
+      const unsigned v = cslot[x];
+      const unsigned long long kk = ckey[v];
+      ci[x] = (int)(kk >> 32);
+      cj[x] = (int)(kk & 0xffffffffull);
+#pragma unroll
+      for (int f = 0; f < 5; ++f) out[(int64_t)f * P + x] = cpay[f * cap + v];
+    }
+  }
+  // loss-of-separation pairs of row r
+  {
+    const unsigned b = rowoff[nrows + 1 + r] - (unsigned)P, e = rowoff[nrows + 2 + r] - (unsigned)P;
+    for (unsigned x = b + 1; x < e; ++x) {
+      const unsigned v = lslot[x];
+      const unsigned kv = (unsigned)(lkey[v] & 0xffffffffull);
+      unsigned y = x;
+      while (y > b && (unsigned)(lkey[lslot[y - 1]] & 0xffffffffull) > kv) {
+        lslot[y] = lslot[y - 1];
+        --y;
+      }
+      lslot[y] = v;
+    }
+    for (unsigned x = b; x < e; ++x) {
+      const unsigned long long kk = lkey[lslot[x]];
+      li[x] = (int)(kk >> 32);
+      lj[x] = (int)(kk & 0xffffffffull);
+    }
+  }
+}
+
+// zero the per-detect state in one launch: counters (all but `tiles` unless
+// full), the dequeue shards and the per-row outputs / counts
+__global__ __launch_bounds__(256) void k_zero(int nrows, int full, Counters *__restrict__ cnt,
+                                              unsigned long long *__restrict__ work,
+                                              unsigned char *__restrict__ inconf,
+                                              unsigned long long *__restrict__ tcpamax,
+                                              unsigned *__restrict__ rowcnt) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k == 0) {
+    const unsigned long long tiles = cnt->tiles;
+    *cnt = Counters{};
+    if (!full) cnt->tiles = tiles;
+  }
+  if (k < kWorkShards * kWorkStride) work[k] = 0;
+  if (k < nrows) {
+    inconf[k] = 0;
+    tcpamax[k] = 0;
+  }
+  if (k < 2 * (nrows + 1)) rowcnt[k] = 0;
 }
 
 // ------------------------------------------------------------------ host side
 static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
-static int bitwidth(int64_t n) {
-  int b = 1;
-  while ((int64_t(1) << b) < n) ++b;
-  return b;
-}
 
 // spatial sort of cnt positions starting at original index base -> perm
 static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const double *lon,
@@ -775,11 +847,25 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   c->last_conf = c->last_los = c->last_cand = 0;
   if (!ensure(c, c->counters, sizeof(Counters), "counters") ||
       !ensure(c, c->inconf, (size_t)(nrows > 0 ? nrows : 1), "inconf") ||
-      !ensure(c, c->tcpamax, (size_t)(nrows > 0 ? nrows : 1) * 8, "tcpamax"))
+      !ensure(c, c->tcpamax, (size_t)(nrows > 0 ? nrows : 1) * 8, "tcpamax") ||
+      !ensure(c, c->workq, kWorkShards * kWorkStride * 8, "work counters") ||
+      !ensure(c, c->rowcnt, (size_t)(2 * (nrows + 1)) * 4, "row counts") ||
+      !ensure(c, c->rowoff, (size_t)(2 * (nrows + 1)) * 4, "row offsets"))
     return -1;
   BSA_HIP(c, hipEventRecord(c->ev[0], c->stream));
+  Counters *dcnt = (Counters *)c->counters.p;
+  auto zero = [&](int full) -> int {
+    const int64_t m = std::max<int64_t>(2 * (nrows + 1), kWorkShards * kWorkStride);
+    hipLaunchKernelGGL(k_zero, dim3(blocks_for(m, 256)), dim3(256), 0, c->stream, (int)nrows, full, dcnt,
+                       (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
+                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p);
+    BSA_HIP(c, hipGetLastError());
+    return 0;
+  };
+  if (zero(1)) return -1;
   if (n == 0 || nrows == 0) {
     for (int e = 1; e < 5; ++e) BSA_HIP(c, hipEventRecord(c->ev[e], c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
     c->ev_valid = true;
     c->have_pairs = true;
     *n_conf = *n_los = 0;
@@ -793,10 +879,32 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   SoA6 intr{(const double *)I[0].p, (const double *)I[1].p, (const double *)I[2].p,
             (const double *)I[3].p, (const double *)I[4].p, (const double *)I[5].p};
 
-  // ---- K0a spatial order (rows: own positions of [rb, re); columns: intruder positions)
-  if (spatial_order(c, (int)nrows, (int)rb, own.lat, own.lon, c->key_r, c->idx_r, c->key_r2, c->perm_r) ||
-      spatial_order(c, (int)n, 0, intr.lat, intr.lon, c->key_c, c->idx_c, c->key_c2, c->perm_c))
-    return -1;
+  // ---- K0a spatial order.  Any permutation gives identical results (the
+  // output is re-sorted canonically), so the order is reused for up to
+  // kResortEvery calls on the same shape: aircraft move ~km between calls,
+  // tiles span ~100 km.  Rows share the column order when own == intruder
+  // and the whole range is detected.
+  const bool shared = !distinct && rb == 0 && re == n;
+  const bool resort = !c->perm_valid || c->perm_n != n || c->perm_rb != rb || c->perm_re != re ||
+                      c->perm_shared != shared || c->perm_distinct != distinct ||
+                      (flags & BSA_FLAG_RESORT) || c->perm_age >= kResortEvery;
+  if (resort) {
+    if (spatial_order(c, (int)n, 0, intr.lat, intr.lon, c->key_c, c->idx_c, c->key_c2, c->perm_c)) return -1;
+    if (!shared &&
+        spatial_order(c, (int)nrows, (int)rb, own.lat, own.lon, c->key_r, c->idx_r, c->key_r2, c->perm_r))
+      return -1;
+    c->perm_valid = true;
+    c->perm_n = n;
+    c->perm_rb = rb;
+    c->perm_re = re;
+    c->perm_shared = shared;
+    c->perm_distinct = distinct;
+    c->perm_age = 0;
+  }
+  c->perm_age++;
+  const unsigned *perm_r = (const unsigned *)(shared ? c->perm_c.p : c->perm_r.p);
+  const unsigned *perm_c = (const unsigned *)c->perm_c.p;
+
   // ---- K0b records in sorted order
   if (!ensure(c, c->rowrec, nrows * sizeof(RowRec), "row records") ||
       !ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
@@ -805,15 +913,15 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
       !ensure(c, c->pfauxrow, nrows * sizeof(PFAux), "prefilter row aux") ||
       !ensure(c, c->pfauxcol, n * sizeof(PFAux), "prefilter column aux"))
     return -1;
-  hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows,
-                     (const unsigned *)c->perm_r.p, own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p,
-                     (PFRec *)c->pfrow.p, (PFAux *)c->pfauxrow.p);
+  hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, perm_r,
+                     own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p, (PFRec *)c->pfrow.p,
+                     (PFAux *)c->pfauxrow.p);
   BSA_HIP(c, hipGetLastError());
-  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n,
-                     (const unsigned *)c->perm_c.p, own, intr, distinct ? 1 : 0, rpz, hpz, tla,
-                     (ColRec *)c->colrec.p, (PFRec *)c->pfcol.p, (PFAux *)c->pfauxcol.p);
+  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n, perm_c, own,
+                     intr, distinct ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p, (PFRec *)c->pfcol.p,
+                     (PFAux *)c->pfauxcol.p);
   BSA_HIP(c, hipGetLastError());
-  // ---- K0c/K0d tile culling
+  // ---- K0c/K0d group / tile boxes and the tile-pair work list
   const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
   const long long ntp = (long long)nrt * nct;
   const int ngr = (int)((nrows + kGroup - 1) / kGroup), ngc = (int)((n + kGroup - 1) / kGroup);
@@ -831,8 +939,6 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
                      (const TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p);
   hipLaunchKernelGGL(k_tileunion, dim3(blocks_for(nct, 256)), dim3(256), 0, c->stream, nct, ngc,
                      (const TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p);
-  BSA_HIP(c, hipMemsetAsync(c->counters.p, 0, sizeof(Counters), c->stream));
-  Counters *dcnt = (Counters *)c->counters.p;
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + 255) / 256)), dim3(256), 0, c->stream, nrt, nct,
                      (const TileBox *)c->tbox_r.p, (const TileBox *)c->tbox_c.p, noprune,
                      (uint2 *)c->tilepairs.p, &dcnt->tiles);
@@ -849,20 +955,14 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   for (int attempt = 0;; ++attempt) {
     if (!ensure(c, c->cand, c->cand_cap * sizeof(uint2), "candidate pairs") ||
         !ensure(c, c->ckey, c->conf_cap * 8, "conflict keys") ||
-        !ensure(c, c->cval, c->conf_cap * 4, "conflict slots") ||
         !ensure(c, c->cpay, c->conf_cap * 5 * 8, "conflict payload") ||
         !ensure(c, c->lkey, c->los_cap * 8, "los keys"))
       return -1;
-    // ---- K1a prefilter over surviving tile pairs (persistent grid, count read on device)
-    BSA_HIP(c, hipMemsetAsync(&dcnt->cand, 0, 24, c->stream));  // cand, conf, los
-    BSA_HIP(c, hipMemsetAsync(&dcnt->groups, 0, 8, c->stream));
-    if (!ensure(c, c->workq, kWorkShards * kWorkStride * 8, "work counters")) return -1;
-    BSA_HIP(c, hipMemsetAsync(c->workq.p, 0, kWorkShards * kWorkStride * 8, c->stream));
-    BSA_HIP(c, hipMemsetAsync(c->inconf.p, 0, nrows, c->stream));
-    BSA_HIP(c, hipMemsetAsync(c->tcpamax.p, 0, nrows * 8, c->stream));
-    // persistent grid: 6 workgroups per CU (LDS/SGPR-limited residency); at
-    // least one workgroup per dequeue shard so every shard's items are taken
-    const unsigned pf_grid = (unsigned)std::max<long long>(kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * 6));
+    if (attempt > 0 && zero(0)) return -1;
+    // ---- K1a prefilter: persistent grid, 6 workgroups per CU (LDS/SGPR-limited
+    // residency), at least one workgroup per dequeue shard
+    const unsigned pf_grid =
+        (unsigned)std::max<long long>(kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * 6));
     if (noprune)
       hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
                          (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
@@ -879,14 +979,14 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
                          (uint2 *)c->cand.p, c->cand_cap);
     BSA_HIP(c, hipGetLastError());
     BSA_HIP(c, hipEventRecord(c->ev[2], c->stream));
-    // ---- K1b exact evaluation (grid-stride, count read on device)
-    hipLaunchKernelGGL(k_exact, dim3(256 * 16), dim3(256), 0, c->stream, (const RowRec *)c->rowrec.p,
-                       (const ColRec *)c->colrec.p, (const unsigned *)c->perm_r.p,
-                       (const unsigned *)c->perm_c.p, (const uint2 *)c->cand.p, &dcnt->cand,
+    // ---- K1b exact evaluation: grid-stride over the device-side count, one
+    // resident round (4 workgroups per CU at its register budget)
+    hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, (const RowRec *)c->rowrec.p,
+                       (const ColRec *)c->colrec.p, perm_r, perm_c, (const uint2 *)c->cand.p, &dcnt->cand,
                        c->cand_cap, rpz, hpz, tla, (int)rb, (unsigned long long *)c->ckey.p,
-                       (unsigned *)c->cval.p, (double *)c->cpay.p, c->conf_cap,
+                       (unsigned *)nullptr, (double *)c->cpay.p, c->conf_cap,
                        (unsigned long long *)c->lkey.p, c->los_cap, dcnt, (unsigned char *)c->inconf.p,
-                       (unsigned long long *)c->tcpamax.p);
+                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p, (int)nrows);
     BSA_HIP(c, hipGetLastError());
     BSA_HIP(c, hipEventRecord(c->ev[3], c->stream));
     if (read_counters(c, &h)) return -1;
@@ -901,45 +1001,36 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   c->last_tiles_total = ntp;
   c->last_groups = (int64_t)h.groups;
 
-  // ---- K2 canonical row-major order
+  // ---- K2 canonical row-major order: scan of the per-row counts, scatter,
+  // per-row insertion sort + payload gather
   const int64_t P = (int64_t)h.conf, L = (int64_t)h.los;
-  const int end_bit = 32 + bitwidth(n);
-  if (!ensure(c, c->ckey2, (size_t)std::max<int64_t>(P, 1) * 8, "sorted conflict keys") ||
-      !ensure(c, c->cval2, (size_t)std::max<int64_t>(P, 1) * 4, "sorted conflict slots") ||
-      !ensure(c, c->lkey2, (size_t)std::max<int64_t>(L, 1) * 8, "sorted los keys") ||
+  if (!ensure(c, c->cval2, (size_t)std::max<int64_t>(P, 1) * 4, "conflict slots") ||
+      !ensure(c, c->lslot, (size_t)std::max<int64_t>(L, 1) * 4, "los slots") ||
       !ensure(c, c->out_ci, (size_t)std::max<int64_t>(P, 1) * 4, "ci") ||
       !ensure(c, c->out_cj, (size_t)std::max<int64_t>(P, 1) * 4, "cj") ||
       !ensure(c, c->out_pay, (size_t)std::max<int64_t>(P, 1) * 5 * 8, "conflict outputs") ||
       !ensure(c, c->out_li, (size_t)std::max<int64_t>(L, 1) * 4, "li") ||
       !ensure(c, c->out_lj, (size_t)std::max<int64_t>(L, 1) * 4, "lj"))
     return -1;
-  size_t t1 = 0, t2 = 0;
-  BSA_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (unsigned long long *)nullptr,
-                                                (unsigned long long *)nullptr, (unsigned *)nullptr,
-                                                (unsigned *)nullptr, (int)std::max<int64_t>(P, 1), 0,
-                                                end_bit, c->stream));
-  BSA_HIP(c, hipcub::DeviceRadixSort::SortKeys(nullptr, t2, (unsigned long long *)nullptr,
-                                               (unsigned long long *)nullptr,
-                                               (int)std::max<int64_t>(L, 1), 0, end_bit, c->stream));
-  if (!ensure(c, c->sort_tmp, std::max<size_t>(std::max(t1, t2), 16), "sort scratch")) return -1;
-  if (P > 0) {
-    size_t tmp = c->sort_tmp.bytes;
-    BSA_HIP(c, hipcub::DeviceRadixSort::SortPairs(c->sort_tmp.p, tmp, (unsigned long long *)c->ckey.p,
-                                                  (unsigned long long *)c->ckey2.p, (unsigned *)c->cval.p,
-                                                  (unsigned *)c->cval2.p, (int)P, 0, end_bit, c->stream));
-    hipLaunchKernelGGL(k_gather_conf, dim3(blocks_for(P, 256)), dim3(256), 0, c->stream, P,
-                       (const unsigned long long *)c->ckey2.p, (const unsigned *)c->cval2.p,
-                       (const double *)c->cpay.p, c->conf_cap, (int *)c->out_ci.p,
-                       (int *)c->out_cj.p, (double *)c->out_pay.p);
+  if (P + L > 0) {
+    const int nscan = (int)(2 * (nrows + 1));
+    size_t tmp = 0;
+    BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (const unsigned *)c->rowcnt.p,
+                                                (unsigned *)c->rowoff.p, nscan, c->stream));
+    if (!ensure(c, c->sort_tmp, std::max<size_t>(tmp, 16), "scan scratch")) return -1;
+    tmp = c->sort_tmp.bytes;
+    BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp, (const unsigned *)c->rowcnt.p,
+                                                (unsigned *)c->rowoff.p, nscan, c->stream));
+    hipLaunchKernelGGL(k_scatter, dim3(blocks_for(P + L, 256)), dim3(256), 0, c->stream, P, L, (int)rb,
+                       (int)nrows, (const unsigned long long *)c->ckey.p, (const unsigned long long *)c->lkey.p,
+                       (const unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p, (unsigned *)c->cval2.p,
+                       (unsigned *)c->lslot.p);
     BSA_HIP(c, hipGetLastError());
-  }
-  if (L > 0) {
-    size_t tmp = c->sort_tmp.bytes;
-    BSA_HIP(c, hipcub::DeviceRadixSort::SortKeys(c->sort_tmp.p, tmp, (unsigned long long *)c->lkey.p,
-                                                 (unsigned long long *)c->lkey2.p, (int)L, 0, end_bit,
-                                                 c->stream));
-    hipLaunchKernelGGL(k_split_los, dim3(blocks_for(L, 256)), dim3(256), 0, c->stream, L,
-                       (const unsigned long long *)c->lkey2.p, (int *)c->out_li.p, (int *)c->out_lj.p);
+    hipLaunchKernelGGL(k_rowsort, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, P,
+                       (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey.p,
+                       (unsigned *)c->cval2.p, (const double *)c->cpay.p, c->conf_cap,
+                       (const unsigned long long *)c->lkey.p, (unsigned *)c->lslot.p, (int *)c->out_ci.p,
+                       (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p);
     BSA_HIP(c, hipGetLastError());
   }
   BSA_HIP(c, hipEventRecord(c->ev[4], c->stream));

@@ -78,6 +78,7 @@ struct alignas(16) TileBox {
 };
 
 constexpr int kTile = 512;  // rows per row block == columns per column tile
+constexpr int kResortEvery = 8;  // detect calls between spatial re-sorts
 
 // counters block on the device (one cache line)
 struct Counters {
@@ -113,6 +114,10 @@ struct Ctx {
   // spatial order: Morton keys and the sorted-position -> original-index maps
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
   DevBuf tbox_r, tbox_c, gbox_r, gbox_c, tilepairs, workq;
+  DevBuf rowcnt, rowoff, lslot;  // K2 counting sort
+  // reusable spatial order (any permutation gives identical results)
+  bool perm_valid = false, perm_shared = false, perm_distinct = false;
+  int64_t perm_n = 0, perm_rb = 0, perm_re = 0, perm_age = 0;
 
   // detect buffers
   DevBuf counters;           // Counters

@@ -39,6 +39,8 @@ typedef struct bsa_ctx bsa_ctx;
 /* detect flags */
 #define BSA_FLAG_WITH_DCPA 1 /* also produce dcpa = sqrt(max(dcpa2,0)) per conflict */
 #define BSA_FLAG_NOPRUNE   2 /* test aid: treat every pair as a candidate (disables the exact-safe prefilter) */
+#define BSA_FLAG_RESORT    4 /* recompute the spatial order now (it is otherwise reused for up to
+                                8 calls; results never depend on it, only the speed does) */
 
 /* ---------------------------------------------------------------- lifecycle */
 
