@@ -637,67 +637,46 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
   return o;
 }
 
+// Results are stored per candidate (flag, key, payload) rather than appended
+// to a shared list: appending needs an atomic with return on ONE counter per
+// wave, which serialises at ~88/us (MI355X_MICROARCH 'dequeue') and cost
+// ~70 us at 100k.  The per-row counts feed K2's counting sort.
 __global__ __launch_bounds__(256) void k_exact(
     const RowRec *__restrict__ R, const ColRec *__restrict__ C,
     const unsigned *__restrict__ perm_r, const unsigned *__restrict__ perm_c,
     const uint2 *__restrict__ cand, const unsigned long long *__restrict__ ncand_p,
-    unsigned long long cand_cap, double rpz, double hpz, double tla, int rb,
-    unsigned long long *__restrict__ ckey, unsigned *__restrict__ cval, double *__restrict__ cpay,
-    unsigned long long conf_cap, unsigned long long *__restrict__ lkey, unsigned long long los_cap,
-    Counters *__restrict__ cnt, unsigned char *__restrict__ inconf,
-    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int nrows) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long ncand = min(*ncand_p, cand_cap);
+    unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
+    unsigned char *__restrict__ cflag, unsigned long long *__restrict__ ckey,
+    double *__restrict__ cpay, unsigned char *__restrict__ inconf,
+    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt) {
+  const unsigned long long ncand = min(*ncand_p, cap);
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long idx = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
        idx < ncand; idx += stride) {
     const uint2 p = cand[idx];
     const unsigned oi = perm_r[p.x], oj = perm_c[p.y];
-    bool conf = false, los = false;
-    PairResult o;
+    unsigned char flag = 0;
     if (oi != oj) {
-      o = eval_pair(R[p.x], C[p.y], rpz, hpz, tla);
-      conf = o.conf;
-      los = o.los;
-    }
-    const unsigned long long key = ((unsigned long long)oi << 32) | oj;
-    const unsigned long long mc = __ballot(conf);
-    if (mc) {
-      const int leader = __builtin_ctzll(mc);
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&cnt->conf, (unsigned long long)__popcll(mc));
-      base = __shfl(base, leader);
-      if (conf) {
-        const unsigned long long slot = base + lane_prefix(mc);
-        if (slot < conf_cap) {
-          ckey[slot] = key;
-          cpay[0 * conf_cap + slot] = o.qdr;
-          cpay[1 * conf_cap + slot] = o.dist;
-          cpay[2 * conf_cap + slot] = o.tcpa;
-          cpay[3 * conf_cap + slot] = o.tin;
-          cpay[4 * conf_cap + slot] = o.dcpa;
-        }
-        const int row = (int)oi - rb;
+      const PairResult o = eval_pair(R[p.x], C[p.y], rpz, hpz, tla);
+      flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
+      const int row = (int)oi - rb;
+      if (flag) ckey[idx] = ((unsigned long long)oi << 32) | oj;
+      if (o.conf) {
+        cpay[0 * cap + idx] = o.qdr;
+        cpay[1 * cap + idx] = o.dist;
+        cpay[2 * cap + idx] = o.tcpa;
+        cpay[3 * cap + idx] = o.tin;
+        cpay[4 * cap + idx] = o.dcpa;
         inconf[row] = 1;
-        atomicAdd(&rowcnt[row], 1u);                 // K2 counting sort, conflicts
         // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
         // positive tcpa can raise it, and positive doubles order as integers.
         if (o.tcpa > 0.0)
           atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
+        atomicAdd(&rowcnt[row], 1u);
       }
+      if (o.los) atomicAdd(&rowcnt[nrows + 1 + row], 1u);
     }
-    const unsigned long long ml = __ballot(los);
-    if (ml) {
-      const int leader = __builtin_ctzll(ml);
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&cnt->los, (unsigned long long)__popcll(ml));
-      base = __shfl(base, leader);
-      if (los) {
-        const unsigned long long slot = base + lane_prefix(ml);
-        if (slot < los_cap) lkey[slot] = key;
-        atomicAdd(&rowcnt[nrows + 1 + ((int)oi - rb)], 1u);  // K2 counting sort, LoS
-      }
-    }
+    cflag[idx] = flag;
   }
 }
 
@@ -707,23 +686,31 @@ __global__ __launch_bounds__(256) void k_exact(
 // conflict list and (minus P) in the LoS list.  Pairs are scattered into their
 // row segment, then one lane per row sorts its (short) segment by column:
 // the result is exactly np.where's row-major order (StateBasedCD.py:93-95).
-__global__ __launch_bounds__(256) void k_scatter(int64_t P, int64_t L, int rb, int nrows,
+__global__ __launch_bounds__(256) void k_scatter(const unsigned long long *__restrict__ ncand_p,
+                                                 unsigned long long cap, int rb, int nrows,
+                                                 const unsigned char *__restrict__ cflag,
                                                  const unsigned long long *__restrict__ ckey,
-                                                 const unsigned long long *__restrict__ lkey,
                                                  const unsigned *__restrict__ rowoff,
                                                  unsigned *__restrict__ rowcnt,
                                                  unsigned *__restrict__ cslot,
                                                  unsigned *__restrict__ lslot) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < P) {
+  const unsigned long long ncand = min(*ncand_p, cap);
+  const unsigned P = rowoff[nrows];
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < ncand;
+       k += stride) {
+    const unsigned char f = cflag[k];
+    if (!f) continue;
     const int row = (int)(ckey[k] >> 32) - rb;
-    const unsigned pos = rowoff[row] + atomicSub(&rowcnt[row], 1u) - 1u;
-    cslot[pos] = (unsigned)k;
-  } else if (k < P + L) {
-    const int64_t s = k - P;
-    const int r = nrows + 1 + ((int)(lkey[s] >> 32) - rb);
-    const unsigned pos = rowoff[r] - (unsigned)P + atomicSub(&rowcnt[r], 1u) - 1u;
-    lslot[pos] = (unsigned)s;
+    if (f & 1) {
+      const unsigned pos = rowoff[row] + atomicSub(&rowcnt[row], 1u) - 1u;
+      cslot[pos] = (unsigned)k;
+    }
+    if (f & 2) {
+      const int r = nrows + 1 + row;
+      const unsigned pos = rowoff[r] - P + atomicSub(&rowcnt[r], 1u) - 1u;
+      lslot[pos] = (unsigned)k;
+    }
   }
 }
 
@@ -731,7 +718,6 @@ __global__ __launch_bounds__(256) void k_rowsort(int nrows, int64_t P, const uns
                                                  const unsigned long long *__restrict__ ckey,
                                                  unsigned *__restrict__ cslot,
                                                  const double *__restrict__ cpay, unsigned long long cap,
-                                                 const unsigned long long *__restrict__ lkey,
                                                  unsigned *__restrict__ lslot, int *__restrict__ ci,
                                                  int *__restrict__ cj, double *__restrict__ out,
                                                  int *__restrict__ li, int *__restrict__ lj) {
@@ -764,16 +750,16 @@ __global__ __launch_bounds__(256) void k_rowsort(int nrows, int64_t P, const uns
     const unsigned b = rowoff[nrows + 1 + r] - (unsigned)P, e = rowoff[nrows + 2 + r] - (unsigned)P;
     for (unsigned x = b + 1; x < e; ++x) {
       const unsigned v = lslot[x];
-      const unsigned kv = (unsigned)(lkey[v] & 0xffffffffull);
+      const unsigned kv = (unsigned)(ckey[v] & 0xffffffffull);
       unsigned y = x;
-      while (y > b && (unsigned)(lkey[lslot[y - 1]] & 0xffffffffull) > kv) {
+      while (y > b && (unsigned)(ckey[lslot[y - 1]] & 0xffffffffull) > kv) {
         lslot[y] = lslot[y - 1];
         --y;
       }
       lslot[y] = v;
     }
     for (unsigned x = b; x < e; ++x) {
-      const unsigned long long kk = lkey[lslot[x]];
+      const unsigned long long kk = ckey[lslot[x]];
       li[x] = (int)(kk >> 32);
       lj[x] = (int)(kk & 0xffffffffull);
     }
@@ -826,11 +812,6 @@ static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const dou
   return 0;
 }
 
-static int read_counters(Ctx *c, Counters *h) {
-  BSA_HIP(c, hipMemcpyAsync(h, c->counters.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-  BSA_HIP(c, hipStreamSynchronize(c->stream));
-  return 0;
-}
 
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
            int64_t *n_conf, int64_t *n_los) {
@@ -946,17 +927,22 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   BSA_HIP(c, hipEventRecord(c->ev[1], c->stream));
 
   if (c->cand_cap == 0) c->cand_cap = (unsigned long long)std::max<int64_t>(1 << 20, 16 * nrows);
-  if (c->conf_cap == 0) c->conf_cap = (unsigned long long)std::max<int64_t>(1 << 16, 8 * nrows);
-  if (c->los_cap == 0) c->los_cap = (unsigned long long)std::max<int64_t>(1 << 16, 4 * nrows);
   const float T = (float)(tla > 0.0 ? tla : 0.0);
   const float lim = (float)((rpz + kEABS) / (1.0 - kE1));
   const RefineParams rp{(float)rpz, (float)hpz, T, lim * lim};
+  const int nscan = (int)(2 * (nrows + 1));
+  size_t scan_tmp = 0;
+  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const unsigned *)c->rowcnt.p,
+                                              (unsigned *)c->rowoff.p, nscan, c->stream));
+  if (!ensure(c, c->sort_tmp, std::max<size_t>(scan_tmp, 16), "scan scratch")) return -1;
   Counters h;
+  unsigned tot[2] = {0, 0};  // P and P + L from the scan
   for (int attempt = 0;; ++attempt) {
-    if (!ensure(c, c->cand, c->cand_cap * sizeof(uint2), "candidate pairs") ||
-        !ensure(c, c->ckey, c->conf_cap * 8, "conflict keys") ||
-        !ensure(c, c->cpay, c->conf_cap * 5 * 8, "conflict payload") ||
-        !ensure(c, c->lkey, c->los_cap * 8, "los keys"))
+    const unsigned long long cap = c->cand_cap;
+    if (!ensure(c, c->cand, cap * sizeof(uint2), "candidate pairs") ||
+        !ensure(c, c->cflag, cap, "candidate flags") ||
+        !ensure(c, c->ckey, cap * 8, "candidate keys") ||
+        !ensure(c, c->cpay, cap * 5 * 8, "candidate payload"))
       return -1;
     if (attempt > 0 && zero(0)) return -1;
     // ---- K1a prefilter: persistent grid, 6 workgroups per CU (LDS/SGPR-limited
@@ -969,41 +955,47 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
                          (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
                          (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
                          (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
-                         (uint2 *)c->cand.p, c->cand_cap);
+                         (uint2 *)c->cand.p, cap);
     else
       hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
                          (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
                          (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
                          (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
                          (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
-                         (uint2 *)c->cand.p, c->cand_cap);
+                         (uint2 *)c->cand.p, cap);
     BSA_HIP(c, hipGetLastError());
     BSA_HIP(c, hipEventRecord(c->ev[2], c->stream));
     // ---- K1b exact evaluation: grid-stride over the device-side count, one
     // resident round (4 workgroups per CU at its register budget)
     hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, (const RowRec *)c->rowrec.p,
                        (const ColRec *)c->colrec.p, perm_r, perm_c, (const uint2 *)c->cand.p, &dcnt->cand,
-                       c->cand_cap, rpz, hpz, tla, (int)rb, (unsigned long long *)c->ckey.p,
-                       (unsigned *)nullptr, (double *)c->cpay.p, c->conf_cap,
-                       (unsigned long long *)c->lkey.p, c->los_cap, dcnt, (unsigned char *)c->inconf.p,
-                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p, (int)nrows);
+                       cap, rpz, hpz, tla, (int)rb, (int)nrows, (unsigned char *)c->cflag.p,
+                       (unsigned long long *)c->ckey.p, (double *)c->cpay.p, (unsigned char *)c->inconf.p,
+                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p);
     BSA_HIP(c, hipGetLastError());
+    // ---- K2 part 1: row offsets (exclusive scan of [conf per row | 0 | LoS per row | 0])
+    size_t tmp = c->sort_tmp.bytes;
+    BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp, (const unsigned *)c->rowcnt.p,
+                                                (unsigned *)c->rowoff.p, nscan, c->stream));
     BSA_HIP(c, hipEventRecord(c->ev[3], c->stream));
-    if (read_counters(c, &h)) return -1;
-    if (h.cand <= c->cand_cap && h.conf <= c->conf_cap && h.los <= c->los_cap) break;
-    if (attempt > 3) return fail(c, "pair buffer overflow (cand %llu conf %llu los %llu)", h.cand, h.conf, h.los);
-    if (h.cand > c->cand_cap) c->cand_cap = h.cand + h.cand / 4 + 1024;
-    if (h.conf > c->conf_cap) c->conf_cap = h.conf + h.conf / 4 + 1024;
-    if (h.los > c->los_cap) c->los_cap = h.los + h.los / 4 + 1024;
+    // the detect's only host sync: candidate count + totals P and P + L
+    BSA_HIP(c, hipMemcpyAsync(&h, c->counters.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipMemcpyAsync(&tot[0], (const unsigned *)c->rowoff.p + nrows, 4, hipMemcpyDeviceToHost,
+                              c->stream));
+    BSA_HIP(c, hipMemcpyAsync(&tot[1], (const unsigned *)c->rowoff.p + nscan - 1, 4,
+                              hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    if (h.cand <= cap) break;
+    if (attempt > 3) return fail(c, "candidate buffer overflow (%llu)", h.cand);
+    c->cand_cap = h.cand + h.cand / 4 + 1024;
   }
   c->last_cand = (int64_t)h.cand;
   c->last_tiles = (int64_t)h.tiles;
   c->last_tiles_total = ntp;
   c->last_groups = (int64_t)h.groups;
 
-  // ---- K2 canonical row-major order: scan of the per-row counts, scatter,
-  // per-row insertion sort + payload gather
-  const int64_t P = (int64_t)h.conf, L = (int64_t)h.los;
+  // ---- K2 part 2: scatter into row segments, per-row insertion sort + gather
+  const int64_t P = (int64_t)tot[0], L = (int64_t)tot[1] - (int64_t)tot[0];
   if (!ensure(c, c->cval2, (size_t)std::max<int64_t>(P, 1) * 4, "conflict slots") ||
       !ensure(c, c->lslot, (size_t)std::max<int64_t>(L, 1) * 4, "los slots") ||
       !ensure(c, c->out_ci, (size_t)std::max<int64_t>(P, 1) * 4, "ci") ||
@@ -1013,24 +1005,16 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
       !ensure(c, c->out_lj, (size_t)std::max<int64_t>(L, 1) * 4, "lj"))
     return -1;
   if (P + L > 0) {
-    const int nscan = (int)(2 * (nrows + 1));
-    size_t tmp = 0;
-    BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (const unsigned *)c->rowcnt.p,
-                                                (unsigned *)c->rowoff.p, nscan, c->stream));
-    if (!ensure(c, c->sort_tmp, std::max<size_t>(tmp, 16), "scan scratch")) return -1;
-    tmp = c->sort_tmp.bytes;
-    BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp, (const unsigned *)c->rowcnt.p,
-                                                (unsigned *)c->rowoff.p, nscan, c->stream));
-    hipLaunchKernelGGL(k_scatter, dim3(blocks_for(P + L, 256)), dim3(256), 0, c->stream, P, L, (int)rb,
-                       (int)nrows, (const unsigned long long *)c->ckey.p, (const unsigned long long *)c->lkey.p,
-                       (const unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p, (unsigned *)c->cval2.p,
-                       (unsigned *)c->lslot.p);
+    hipLaunchKernelGGL(k_scatter, dim3(256 * 4), dim3(256), 0, c->stream, &dcnt->cand, c->cand_cap,
+                       (int)rb, (int)nrows, (const unsigned char *)c->cflag.p,
+                       (const unsigned long long *)c->ckey.p, (const unsigned *)c->rowoff.p,
+                       (unsigned *)c->rowcnt.p, (unsigned *)c->cval2.p, (unsigned *)c->lslot.p);
     BSA_HIP(c, hipGetLastError());
     hipLaunchKernelGGL(k_rowsort, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, P,
                        (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey.p,
-                       (unsigned *)c->cval2.p, (const double *)c->cpay.p, c->conf_cap,
-                       (const unsigned long long *)c->lkey.p, (unsigned *)c->lslot.p, (int *)c->out_ci.p,
-                       (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p);
+                       (unsigned *)c->cval2.p, (const double *)c->cpay.p, c->cand_cap,
+                       (unsigned *)c->lslot.p, (int *)c->out_ci.p, (int *)c->out_cj.p,
+                       (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p);
     BSA_HIP(c, hipGetLastError());
   }
   BSA_HIP(c, hipEventRecord(c->ev[4], c->stream));

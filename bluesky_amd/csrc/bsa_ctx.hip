@@ -129,6 +129,7 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->pfauxrow, &c->pfauxcol, &c->key_r, &c->idx_r, &c->key_r2, &c->perm_r,
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
                         &c->gbox_r, &c->gbox_c, &c->workq, &c->rowcnt, &c->rowoff, &c->lslot,
+                        &c->cflag,
                         &c->tilepairs};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);

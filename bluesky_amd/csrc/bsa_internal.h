@@ -122,6 +122,7 @@ struct Ctx {
   // detect buffers
   DevBuf counters;           // Counters
   DevBuf cand;               // uint2 (i, j)
+  DevBuf cflag;              // per candidate: bit0 conflict, bit1 LoS
   unsigned long long cand_cap = 0;
   DevBuf ckey, cval, ckey2, cval2;  // conflict keys / slot ids (+ sorted)
   DevBuf cpay;               // 5 x cap doubles: qdr dist tcpa tin dcpa (slot order)
