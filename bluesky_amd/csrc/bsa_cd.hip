@@ -147,6 +147,16 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   PFAux a;
   a.vs = (float)r.vs;
   a.flags = 0;
+  // local east / north basis of the CPA refine (fp64, then rounded)
+  // e = (-sin lon, cos lon, 0), n = (-sin lat cos lon, -sin lat sin lon, cos lat)
+  const double slo = sin(lor), clo = cos(lor);
+  a.ex = (float)(-slo);
+  a.ey = (float)clo;
+  a.nx = (float)(-sinl * clo);
+  a.ny = (float)(-sinl * slo);
+  a.nz = (float)cosl;
+  a.pad = 0.f;
+  if (!(cosl > 1e-2)) a.flags = 1;  // within ~0.6 deg of a pole (or |lat| > 90): never refine
   if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
     p.s = INFINITY;
     a.flags = 1;
@@ -196,6 +206,7 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
   PFAux a;
   a.vs = (float)c.vs;
   a.flags = 0;
+  a.ex = a.ey = a.nx = a.ny = a.nz = a.pad = 0.f;  // the refine uses the row's basis only
   // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
   // when own != intruder (geo.py:128): never prune or refine such a column.
   if ((distinct && olat == 0.0) || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
@@ -367,16 +378,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // (DESIGN.md "CPA refine"); any NaN keeps the pair.
 __device__ __forceinline__ bool pf_refine(const PFRec &r, const PFAux &ra, const PFRec &c,
                                           const PFAux &ca, const RefineParams &rp) {
+  // flags: row basis unusable (pole), quirk columns, non-finite positions
   if (ra.flags | ca.flags) return true;
-  const float rho = sqrtf(r.x * r.x + r.y * r.y);
-  if (!(rho > 1e-2f)) return true;                         // basis ill-conditioned near a pole
-  const float ir = 1.f / rho;
-  const float ex = -r.y * ir, ey = r.x * ir;               // local east at the row position
-  const float nx = -r.z * r.x * ir, ny = -r.z * r.y * ir, nz = rho;  // local north
   const float dx = c.x - r.x, dy = c.y - r.y, dz = c.z - r.z;
   if (dx * dx + dy * dy + dz * dz > 0.04f) return true;   // > ~1270 km: keep, no refine
-  const float pe = (dx * ex + dy * ey) * kRS;
-  const float pn = (dx * nx + dy * ny + dz * nz) * kRS;
+  // chord projected on the row's local east / north basis (precomputed in prep)
+  const float pe = (dx * ra.ex + dy * ra.ey) * kRS;
+  const float pn = (dx * ra.nx + dy * ra.ny + dz * ra.nz) * kRS;
   const float ve = c.u - r.u, vn = c.v - r.v;              // own.u[j] - int.u[i]
   const float vv = ve * ve + vn * vn;
   if (!(vv >= 4e-6f)) return true;                         // reference may clamp dv2
@@ -384,19 +392,23 @@ __device__ __forceinline__ bool pf_refine(const PFRec &r, const PFAux &ra, const
   const float dvs = ca.vs - ra.vs;
   const float adv = __builtin_fabsf(dvs);
   float t0 = 0.f, t1 = rp.T;
+  // reciprocals by v_rcp_f32 (1 ulp): every division here only places a
+  // window edge or the closest-approach time, and the margins below are
+  // many orders of magnitude wider than 1 ulp
   if (adv < 1e-3f) {
     if (__builtin_fabsf(dalt) >= rp.H + 1e-3f * rp.T + 2.f + 1e-5f * __builtin_fabsf(dalt)) return false;
   } else {
-    const float ta = (-rp.H - dalt) / dvs, tb = (rp.H - dalt) / dvs;
+    const float inv = __builtin_amdgcn_rcpf(dvs);
+    const float ta = (-rp.H - dalt) * inv, tb = (rp.H - dalt) * inv;
     const float lo = fminf(ta, tb), hi = fmaxf(ta, tb);
-    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + rp.H)) / adv +
+    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + rp.H)) * __builtin_fabsf(inv) +
                     1e-4f * fmaxf(__builtin_fabsf(lo), __builtin_fabsf(hi));
     t0 = fmaxf(lo - d, 0.f);
     t1 = fminf(hi + d, rp.T);
     if (t0 > t1) return false;
   }
   const float tl = t0 * (1.f - kE1), th = t1 * (1.f + 2.f * kE1);
-  float ts = -(pe * ve + pn * vn) / vv;
+  float ts = -(pe * ve + pn * vn) * __builtin_amdgcn_rcpf(vv);
   ts = fminf(fmaxf(ts, tl), th);
   const float qe = pe + ve * ts, qn = pn + vn * ts;
   return !(qe * qe + qn * qn > rp.lim2);
@@ -509,9 +521,10 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
       __builtin_amdgcn_wave_barrier();
     };
 
-    // stage 1 for one column record, packed over the lane's two rows
-    auto visit = [&](const PFRec &c, unsigned cl) {
-      bool ka, kb;
+    // stage 1 for one column record, packed over the lane's two rows; the
+    // survivors of an 8-column chunk accumulate as per-lane bit masks and are
+    // queued once per chunk (one wave prefix sum instead of per-column ballots)
+    auto reach = [&](const PFRec &c, bool &ka, bool &kb) {
       if (NOPRUNE) {
         ka = va;
         kb = vb;
@@ -527,14 +540,28 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
         ka = (d2.x < st2.x) & (__builtin_fabsf(dh.x) < hh.x);
         kb = (d2.y < st2.y) & (__builtin_fabsf(dh.y) < hh.y);
       }
-      const unsigned long long ma = __ballot(ka), mb = __ballot(kb);
-      if (ma | mb) {
-        if (ka) q1[n1 + lane_prefix(ma)] = ((unsigned)lane << 16) | cl;
-        n1 = __builtin_amdgcn_readfirstlane(n1 + (unsigned)__popcll(ma));
-        if (kb) q1[n1 + lane_prefix(mb)] = ((unsigned)(64 + lane) << 16) | cl;
-        n1 = __builtin_amdgcn_readfirstlane(n1 + (unsigned)__popcll(mb));
-        if (n1 > (unsigned)(PF_Q1 - 2 * 64)) drain();
+    };
+    auto enqueue = [&](unsigned ba, unsigned bb, unsigned col0) {
+      const unsigned cnt = (unsigned)__popc(ba) + (unsigned)__popc(bb);
+      if (!__ballot(cnt != 0)) return;
+      unsigned x = cnt;  // inclusive wave prefix sum of cnt
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, o);
+        if (lane >= o) x += y;
       }
+      const unsigned total = __builtin_amdgcn_readlane(x, 63);
+      if (n1 + total > (unsigned)PF_Q1) drain();  // total <= 2 * 64 * 8 = PF_Q1
+      unsigned pos = n1 + x - cnt;
+      while (ba) {
+        q1[pos++] = ((unsigned)lane << 16) | (col0 + (unsigned)__builtin_ctz(ba));
+        ba &= ba - 1;
+      }
+      while (bb) {
+        q1[pos++] = ((unsigned)(64 + lane) << 16) | (col0 + (unsigned)__builtin_ctz(bb));
+        bb &= bb - 1;
+      }
+      n1 = __builtin_amdgcn_readfirstlane(n1 + total);
     };
 
     for (int g = 0; g < ng; ++g) {
@@ -544,15 +571,34 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
       const int nc = min(kGroup, ncols - c0);
       const unsigned cl0 = (unsigned)(g * kGroup);
       if (nc == kGroup) {
-        for (int j0 = 0; j0 < kGroup; j0 += 4) {
-          PFRec cc[4];
+        for (int j0 = 0; j0 < kGroup; j0 += 8) {
+          unsigned ba = 0, bb = 0;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) cc[u] = pcol[c0 + j0 + u];
+          for (int h4 = 0; h4 < 8; h4 += 4) {
+            PFRec cc[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) visit(cc[u], cl0 + j0 + u);
+            for (int u = 0; u < 4; ++u) cc[u] = pcol[c0 + j0 + h4 + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              bool ka, kb;
+              reach(cc[u], ka, kb);
+              ba |= (unsigned)ka << (h4 + u);
+              bb |= (unsigned)kb << (h4 + u);
+            }
+          }
+          enqueue(ba, bb, cl0 + (unsigned)j0);
         }
       } else {
-        for (int jj = 0; jj < nc; ++jj) visit(pcol[c0 + jj], cl0 + jj);
+        for (int j0 = 0; j0 < nc; j0 += 8) {
+          unsigned ba = 0, bb = 0;
+          for (int u = 0; u < 8 && j0 + u < nc; ++u) {
+            bool ka, kb;
+            reach(pcol[c0 + j0 + u], ka, kb);
+            ba |= (unsigned)ka << u;
+            bb |= (unsigned)kb << u;
+          }
+          enqueue(ba, bb, cl0 + (unsigned)j0);
+        }
       }
     }
     if (n1) drain();

@@ -64,10 +64,15 @@ struct alignas(16) PFRec {
 static_assert(sizeof(PFRec) == 32, "PFRec must be 32 B");
 
 // cold part of the prefilter record, read only by the CPA refine
-struct alignas(8) PFAux {
+struct alignas(16) PFAux {
   float vs;        // vertical speed [m/s]
-  unsigned flags;  // bit 0: never refine this index (unbounded radius quirk / non-finite)
+  unsigned flags;  // bit 0: never refine this index (unbounded radius quirk / non-finite
+                   //        / tangent basis ill-conditioned near a pole)
+  float ex, ey;    // rows: local east unit vector at the position (ez = 0)
+  float nx, ny, nz;  //       local north unit vector
+  float pad;
 };
+static_assert(sizeof(PFAux) == 32, "PFAux must be 32 B");
 
 // axis-aligned bounds of one tile of sorted PFRecs (tile culling)
 struct alignas(16) TileBox {
