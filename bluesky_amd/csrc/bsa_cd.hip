@@ -92,15 +92,39 @@ __global__ __launch_bounds__(256) void k_keys(int cnt, int base, const double *_
 }
 
 // ------------------------------------------------------------------ K0b prep
+// Horizontal half-bound in unit-sphere chord units: a pair is
+// kept iff chord < s_i + s_j,  s = ((R/2 + (|gs| + 0.5e-3) tla)(1 + 1e-5)) / 6.3e6 + 1e-6.
+// s >= 0.5 (a reach beyond ~3000 km) or non-finite -> INF (never pruned
+// horizontally); the bound also caps the magnitudes in the fp32 test (kPlaneMargin).
 __device__ __forceinline__ float reach_h(double rpz, double gs, double tlap) {
-  // horizontal half-bound in unit-sphere chord units: a pair is kept iff
-  // chord < s_i + s_j,  s = ((R/2 + (|gs| + 0.5e-3) tla)(1 + 1e-5)) / 6.3e6 + 1e-6
   const double s = ((0.5 * rpz + (fabs(gs) + 0.5e-3) * tlap) * (1.0 + 1e-5)) / 6.3e6 + 1e-6;
-  return isfinite(s) ? (float)s : INFINITY;
+  return (s < 0.5) ? (float)s : INFINITY;
 }
-__device__ __forceinline__ float reach_v(double hpz, double vs, double alt, double tlap) {
-  const double h = (0.5 * hpz + (fabs(vs) + 0.5e-6) * tlap) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(alt);
-  return isfinite(h) ? (float)h : INFINITY;
+// vertical half-bound [m]: kept iff |dalt| < h_i + h_j
+__device__ __forceinline__ double reach_v(double hpz, double vs, double alt, double tlap) {
+  return (0.5 * hpz + (fabs(vs) + 0.5e-6) * tlap) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(alt);
+}
+
+// Prefilter record from the fp64 unit vector, reach and altitude.
+// lo / hi = alt -/+ h rounded to fp32 (error
+// <= 1e-3 m at flight levels, inside h's 0.5 m + 1e-6 |alt| margin); a
+// non-finite h keeps the pair vertically (lo = -INF, hi = +INF).
+__device__ __forceinline__ PFRec make_pf(double px, double py, double pz, float s, double alt, double h) {
+  PFRec p;
+  p.x = (float)px;
+  p.y = (float)py;
+  p.z = (float)pz;
+  p.s = s;
+  if (isfinite(h)) {
+    p.lo = (float)(alt - h);
+    p.hi = (float)(alt + h);
+  } else {
+    p.lo = -INFINITY;
+    p.hi = INFINITY;
+  }
+  p.alt = (float)alt;
+  p.pad = 0.f;
+  return p;
 }
 
 struct SoA6 {
@@ -112,7 +136,7 @@ struct SoA6 {
 __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__restrict__ perm,
                                                    SoA6 own, SoA6 intr, double rpz, double hpz,
                                                    double tla, RowRec *__restrict__ R,
-                                                   PFRec *__restrict__ PR, PFAux *__restrict__ PA) {
+                                                   PFRec *__restrict__ PR, PFVel *__restrict__ PV) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const int o = (int)perm[k];
@@ -135,41 +159,24 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   for (int q = 0; q < 7; ++q) r.pad[q] = 0.0;
   R[k] = r;
   const double lor = lo * kD2R;
-  PFRec p;
-  p.x = (float)(cosl * cos(lor));
-  p.y = (float)(cosl * sin(lor));
-  p.z = (float)sinl;
-  p.s = reach_h(rpz, gs, tlap);
-  p.alt = (float)r.alt;
-  p.h = reach_v(hpz, r.vs, r.alt, tlap);
-  p.u = (float)r.u;
-  p.v = (float)r.v;
-  PFAux a;
-  a.vs = (float)r.vs;
-  a.flags = 0;
-  // local east / north basis of the CPA refine (fp64, then rounded)
-  // e = (-sin lon, cos lon, 0), n = (-sin lat cos lon, -sin lat sin lon, cos lat)
-  const double slo = sin(lor), clo = cos(lor);
-  a.ex = (float)(-slo);
-  a.ey = (float)clo;
-  a.nx = (float)(-sinl * clo);
-  a.ny = (float)(-sinl * slo);
-  a.nz = (float)cosl;
-  a.pad = 0.f;
-  if (!(cosl > 1e-2)) a.flags = 1;  // within ~0.6 deg of a pole (or |lat| > 90): never refine
-  if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
-    p.s = INFINITY;
-    a.flags = 1;
-  }
+  const PFRec p = make_pf(cosl * cos(lor), cosl * sin(lor), sinl, reach_h(rpz, gs, tlap), r.alt,
+                          reach_v(hpz, r.vs, r.alt, tlap));
+  PFVel v;
+  v.u = (float)r.u;
+  v.v = (float)r.v;
+  v.vs = (float)r.vs;
+  // within ~0.6 deg of a pole (or |lat| > 90: the refine's local east / north
+  // basis is ill-conditioned), or a non-finite position: never refine
+  v.flags = (!(cosl > 1e-2) || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) ? 1u : 0u;
   PR[k] = p;
-  PA[k] = a;
+  PV[k] = v;
 }
 
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
 __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__restrict__ perm,
                                                    SoA6 own, SoA6 intr, int distinct, double rpz,
                                                    double hpz, double tla, ColRec *__restrict__ C,
-                                                   PFRec *__restrict__ PC, PFAux *__restrict__ PA) {
+                                                   PFRec *__restrict__ PC, PFVel *__restrict__ PV) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const int o = (int)perm[k];
@@ -194,27 +201,20 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
   for (int q = 0; q < 6; ++q) c.pad[q] = 0.0;
   C[k] = c;
   const double lor = lo * kD2R;
-  PFRec p;
-  p.x = (float)(cosl * cos(lor));
-  p.y = (float)(cosl * sin(lor));
-  p.z = (float)sinl;
-  p.s = reach_h(rpz, gs, tlap);
-  p.alt = (float)c.alt;
-  p.h = reach_v(hpz, c.vs, c.alt, tlap);
-  p.u = (float)c.u;
-  p.v = (float)c.v;
-  PFAux a;
-  a.vs = (float)c.vs;
-  a.flags = 0;
-  a.ex = a.ey = a.nx = a.ny = a.nz = a.pad = 0.f;  // the refine uses the row's basis only
   // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
-  // when own != intruder (geo.py:128): never prune or refine such a column.
-  if ((distinct && olat == 0.0) || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) {
-    p.s = INFINITY;
-    a.flags = 1;
-  }
+  // when own != intruder (geo.py:128): never prune such a column horizontally
+  // nor refine it.
+  const bool quirk = distinct && olat == 0.0;
+  const PFRec p = make_pf(cosl * cos(lor), cosl * sin(lor), sinl,
+                          quirk ? INFINITY : reach_h(rpz, gs, tlap), c.alt,
+                          reach_v(hpz, c.vs, c.alt, tlap));
+  PFVel v;
+  v.u = (float)c.u;
+  v.v = (float)c.v;
+  v.vs = (float)c.vs;
+  v.flags = (quirk || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) ? 1u : 0u;
   PC[k] = p;
-  PA[k] = a;
+  PV[k] = v;
 }
 
 // ------------------------------------------------------------------ K0c tile boxes
@@ -241,34 +241,33 @@ __global__ __launch_bounds__(256) void k_groupbox(int cnt, const PFRec *__restri
   const int ngroups = (cnt + kGroup - 1) / kGroup;
   if (g >= ngroups) return;  // whole wave exits together
   float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  float smax = 0.f, hmax = 0.f;
+  float smax = 0.f;
   if (k < cnt) {
     const PFRec p = P[k];
     lo[0] = hi[0] = p.x;
     lo[1] = hi[1] = p.y;
     lo[2] = hi[2] = p.z;
-    lo[3] = hi[3] = p.alt;
+    lo[3] = p.lo;
+    hi[3] = p.hi;
     smax = p.s == p.s ? p.s : INFINITY;
-    hmax = p.h == p.h ? p.h : INFINITY;
   }
   for (int q = 0; q < 4; ++q) {
     lo[q] = wmin(lo[q]);
     hi[q] = wmax(hi[q]);
   }
   smax = wmax(smax);
-  hmax = wmax(hmax);
   if (lane == 0) {
     TileBox b;
     for (int q = 0; q < 3; ++q) {
       b.lo[q] = lo[q];
       b.hi[q] = hi[q];
     }
-    b.altlo = lo[3];
-    b.althi = hi[3];
+    b.vlo = lo[3];
+    b.vhi = hi[3];
     b.smax = smax;
-    b.hmax = hmax;
+    b.pad0 = 0.f;
     b.count = min(kGroup, cnt - g * kGroup);
-    b.pad = 0;
+    b.pad1 = 0;
     box[g] = b;
   }
 }
@@ -279,12 +278,12 @@ __device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b)
     u.lo[q] = fminf(a.lo[q], b.lo[q]);
     u.hi[q] = fmaxf(a.hi[q], b.hi[q]);
   }
-  u.altlo = fminf(a.altlo, b.altlo);
-  u.althi = fmaxf(a.althi, b.althi);
+  u.vlo = fminf(a.vlo, b.vlo);
+  u.vhi = fmaxf(a.vhi, b.vhi);
   u.smax = fmaxf(a.smax, b.smax);
-  u.hmax = fmaxf(a.hmax, b.hmax);
+  u.pad0 = 0.f;
   u.count = a.count + b.count;
-  u.pad = 0;
+  u.pad1 = 0;
   return u;
 }
 
@@ -304,6 +303,18 @@ __device__ __forceinline__ float gap(float alo, float ahi, float blo, float bhi)
   return fmaxf(0.f, fmaxf(alo - bhi, blo - ahi));
 }
 
+// Can any pair of the two boxes pass stage 1?  Horizontally the gaps bound the
+// chord from below and s_i + s_j <= smax_a + smax_b; vertically stage 1 needs
+// lo_j < hi_i and hi_j > lo_i, so the [vlo, vhi] intervals must overlap.
+__device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileBox &b) {
+  const float gx = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]);
+  const float gy = gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]);
+  const float gz = gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]);
+  const float d2 = gx * gx + gy * gy + gz * gz;
+  const float st = (a.smax + b.smax) * 1.00001f + 1e-5f;
+  return !(d2 >= st * st) && (b.vlo < a.vhi) && (b.vhi > a.vlo);
+}
+
 __global__ __launch_bounds__(256) void k_tilepairs(int nrt, int nct, const TileBox *__restrict__ rb,
                                                    const TileBox *__restrict__ cb, int noprune,
                                                    uint2 *__restrict__ out,
@@ -315,20 +326,7 @@ __global__ __launch_bounds__(256) void k_tilepairs(int nrt, int nct, const TileB
   if (valid) {
     rt = (int)(id / nct);
     ct = (int)(id % nct);
-    if (noprune) {
-      keep = true;
-    } else {
-      const TileBox a = rb[rt], b = cb[ct];
-      const float gx = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]);
-      const float gy = gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]);
-      const float gz = gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]);
-      const float d2 = gx * gx + gy * gy + gz * gz;
-      const float st = (a.smax + b.smax) * 1.00001f + 1e-6f;
-      const float ga = gap(a.altlo, a.althi, b.altlo, b.althi);
-      // a pair inside can pass only if its chord < s_i + s_j <= smax_a + smax_b
-      // and |dalt| < h_i + h_j <= hmax_a + hmax_b; the gaps bound chord/dalt below
-      keep = !(d2 >= st * st) && !(ga >= (a.hmax + b.hmax) * 1.00001f + 1e-3f);
-    }
+    keep = noprune ? true : boxes_may_interact(rb[rt], cb[ct]);
   }
   const unsigned long long m = __ballot(keep);
   if (m) {
@@ -360,78 +358,91 @@ struct RefineParams {
 constexpr float kRS = 6371000.f;   // scale of the unit-sphere chord to metres
 constexpr float kE1 = 0.012f;      // bound on |log(reference dist / estimated dist)|
 constexpr float kEABS = 50.f;      // absolute position error budget [m]
+// Stage 1 rounding budget (planar test).  Rows lie within
+// ~0.02 of the plane origin and a kept pair has s < 0.5, so every term of
+// acc is < 0.6 in magnitude and its fp32 roundings (k, K, 1 add, 2 fma; the
+// projection errors are inside s's 1e-6 chord margin) total < 2e-7.
+constexpr float kPlaneMargin = 4e-7f;
 
-__device__ __forceinline__ unsigned lane_prefix(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
 __device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long v) {
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
   return ((unsigned long long)hi << 32) | lo;
 }
+__device__ __forceinline__ unsigned lane_prefix(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+// inclusive wave64 prefix sum on the DPP crossbar (no LDS round trips):
+// row_shr 1/2/4/8 within each 16-lane row, then row_bcast 15 / 31 across rows
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned x) {
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 // stage 2: conservative closest-approach refine of one (row, column) pair.
-// Returns false only when no t in [0, max(tla,0)] can lie in both the
-// vertical and the horizontal window of the reference's geometry
-// (DESIGN.md "CPA refine"); any NaN keeps the pair.
-__device__ __forceinline__ bool pf_refine(const PFRec &r, const PFAux &ra, const PFRec &c,
-                                          const PFAux &ca, const RefineParams &rp) {
-  // flags: row basis unusable (pole), quirk columns, non-finite positions
-  if (ra.flags | ca.flags) return true;
-  const float dx = c.x - r.x, dy = c.y - r.y, dz = c.z - r.z;
+// rp = (x, y, z, -) and rv = (u, v, vs, alt) of the row; cp = (x, y, z, -) and
+// cv = (u, v, vs, alt) of the column; u is NaN for an index that must never
+// be refined (quirk column, non-finite position, row within ~0.6 deg of a
+// pole), which keeps the pair through the `vv` test.  Returns false only
+// when no t in [0, max(tla,0)] can lie in both the vertical and the
+// horizontal window of the reference's geometry (DESIGN.md "CPA refine");
+// any NaN keeps the pair.
+__device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, const float4 &cp,
+                                          const float4 &cv, const RefineParams &prm) {
+  const float dx = cp.x - rp.x, dy = cp.y - rp.y, dz = cp.z - rp.z;
   if (dx * dx + dy * dy + dz * dz > 0.04f) return true;   // > ~1270 km: keep, no refine
-  // chord projected on the row's local east / north basis (precomputed in prep)
-  const float pe = (dx * ra.ex + dy * ra.ey) * kRS;
-  const float pn = (dx * ra.nx + dy * ra.ny + dz * ra.nz) * kRS;
-  const float ve = c.u - r.u, vn = c.v - r.v;              // own.u[j] - int.u[i]
+  // chord projected on the row's local east / north basis
+  //   e = (-y, x, 0) / rho,  n = (-z x / rho, -z y / rho, rho),  rho = cos(lat)
+  // (from the fp32 unit vector; |lat| > ~89.4 deg rows are flagged)
+  const float rho2 = rp.x * rp.x + rp.y * rp.y;
+  const float irho = __builtin_amdgcn_rsqf(rho2);
+  const float rho = rho2 * irho;
+  const float pe = (dy * rp.x - dx * rp.y) * irho * kRS;
+  const float pn = (dz * rho - rp.z * (dx * rp.x + dy * rp.y) * irho) * kRS;
+  const float ve = cv.x - rv.x, vn = cv.y - rv.y;          // own.u[j] - int.u[i]
   const float vv = ve * ve + vn * vn;
-  if (!(vv >= 4e-6f)) return true;                         // reference may clamp dv2
-  const float dalt = c.alt - r.alt;                        // own.alt[j] - int.alt[i]
-  const float dvs = ca.vs - ra.vs;
+  if (!(vv >= 4e-6f)) return true;                         // reference may clamp dv2; NaN
+  const float dalt = cv.w - rv.w;                          // own.alt[j] - int.alt[i]
+  const float dvs = cv.z - rv.z;
   const float adv = __builtin_fabsf(dvs);
-  float t0 = 0.f, t1 = rp.T;
+  float t0 = 0.f, t1 = prm.T;
   // reciprocals by v_rcp_f32 (1 ulp): every division here only places a
   // window edge or the closest-approach time, and the margins below are
   // many orders of magnitude wider than 1 ulp
   if (adv < 1e-3f) {
-    if (__builtin_fabsf(dalt) >= rp.H + 1e-3f * rp.T + 2.f + 1e-5f * __builtin_fabsf(dalt)) return false;
+    if (__builtin_fabsf(dalt) >= prm.H + 1e-3f * prm.T + 2.f + 1e-5f * __builtin_fabsf(dalt)) return false;
   } else {
     const float inv = __builtin_amdgcn_rcpf(dvs);
-    const float ta = (-rp.H - dalt) * inv, tb = (rp.H - dalt) * inv;
+    const float ta = (-prm.H - dalt) * inv, tb = (prm.H - dalt) * inv;
     const float lo = fminf(ta, tb), hi = fmaxf(ta, tb);
-    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + rp.H)) * __builtin_fabsf(inv) +
+    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + prm.H)) * __builtin_fabsf(inv) +
                     1e-4f * fmaxf(__builtin_fabsf(lo), __builtin_fabsf(hi));
     t0 = fmaxf(lo - d, 0.f);
-    t1 = fminf(hi + d, rp.T);
+    t1 = fminf(hi + d, prm.T);
     if (t0 > t1) return false;
   }
   const float tl = t0 * (1.f - kE1), th = t1 * (1.f + 2.f * kE1);
   float ts = -(pe * ve + pn * vn) * __builtin_amdgcn_rcpf(vv);
   ts = fminf(fmaxf(ts, tl), th);
   const float qe = pe + ve * ts, qn = pn + vn * ts;
-  return !(qe * qe + qn * qn > rp.lim2);
+  return !(qe * qe + qn * qn > prm.lim2);
 }
 
-// can any pair of the two boxes pass the reach test?  (gap bounds the chord /
-// |dalt| from below; s_i + s_j <= smax_a + smax_b, h_i + h_j <= hmax_a + hmax_b)
-__device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileBox &b) {
-  const float gx = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]);
-  const float gy = gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]);
-  const float gz = gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]);
-  const float d2 = gx * gx + gy * gy + gz * gz;
-  const float st = (a.smax + b.smax) * 1.00001f + 1e-6f;
-  const float ga = gap(a.altlo, a.althi, b.altlo, b.althi);
-  return !(d2 >= st * st) && !(ga >= (a.hmax + b.hmax) * 1.00001f + 1e-3f);
-}
-
-constexpr int PF_Q1 = 1024;  // per-wave stage-1 queue: u32 (row_local << 16 | col_local)
-constexpr int PF_Q2 = 256;   // per-wave stage-2 queue: uint2 (sorted row, sorted column)
+constexpr int PF_Q1 = 1024;  // per-wave stage-1 queue: u16 (row_local << 6 | col_in_group)
+constexpr int PF_Q2 = 128;   // per-wave stage-2 queue: uint2 (sorted row, sorted column)
 constexpr int PF_WROWS = 128;  // rows per wave (2 per lane)
+constexpr int PF_BLOCKS_PER_CU = 4;  // LDS-limited: 10 KB per wave
 constexpr int kWorkShards = 8;   // one dequeue counter per XCD group
 constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
 static_assert(PF_WAVES * PF_WROWS == kTile, "4 waves x 128 rows = one row block");
+static_assert(PF_Q1 >= 2 * 64 * 8, "one 8-column chunk of survivors fits the stage-1 queue");
 
 __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 *__restrict__ cand,
                                          unsigned long long *__restrict__ count,
@@ -445,26 +456,71 @@ __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 
   __builtin_amdgcn_wave_barrier();
 }
 
-// K1a: each wave sweeps its 128 rows against the 512 columns of a tile pair
-// in 64-column groups (a group is skipped when the wave's row box and the
-// group box cannot interact).  Stage 1 (packed fp32 reach test, 2 rows per
-// lane) pushes survivors into an LDS queue; the queue is drained with all 64
-// lanes busy through stage 2 (refine), whose survivors go to a second queue
-// that is flushed to HBM with one atomic per flush.
+// Diagnostic phase timers (build with -DBSA_PF_STAMPS; `make stamps`):
+// cycles per wave spent in 0 dequeue/setup, 1 stage 1, 2 refine drains,
+// 3 flushes, summed over waves into Counters::stamp.
+#ifdef BSA_PF_STAMPS
+#define PF_STAMP(k)                                               \
+  do {                                                            \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += now_ - st_last;                                  \
+    st_last = now_;                                               \
+  } while (0)
+#else
+#define PF_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
+// K1a: each wave sweeps its 128 rows (2 per lane, in registers) against the
+// 512 columns of a tile pair, one 64-column group at a time; groups whose box
+// cannot interact with the wave's row box are skipped.
+//
+// Stage 1 works in a plane: rows and columns are projected orthogonally onto
+// the plane spanned by an (fp32-)orthonormal pair E, N (the tangent plane at
+// the item's first row).  A projection never lengthens a vector, so the planar
+// distance is <= the chord and "planar < s_i + s_j" keeps every pair with
+// chord < s_i + s_j, wherever E, N point.  With P = ((p - o).E, (p - o).N) and
+// k = s^2/2 - |P|^2/2 the test is linear in the column's values:
+//   acc = (K_i + k_j) + s_i s_j + E_i e_j + N_i n_j = ((s_i + s_j)^2 - |P_i - P_j|^2) / 2
+// (K_i = k_i + kPlaneMargin), plus the vertical interval test
+// lo_j < hi_i and hi_j > lo_i.  The three signs are combined with integer ops
+// (keep iff sign(acc) = 0, sign(lo_j - hi_i) = 1, sign(hi_j - lo_i) = 0;
+// the +-0 and NaN cases can only keep a pair, never drop one) and shifted
+// into a per-lane column bit mask with v_alignbit.
+//
+// The column records of a group are loaded with one coalesced vector load
+// per lane (issued one group ahead), projected and staged in the wave's LDS
+// slot, from which every lane reads them as broadcasts.  Survivors of each
+// 8-column chunk go to an LDS queue (DPP prefix sum of the per-lane counts).
+// The queue is drained at the end of every group (or when full) with all 64
+// lanes busy through stage 2 (refine) on LDS-resident inputs (the group's
+// staged columns, the item's staged rows, row unit vectors by ds_bpermute).
+// Stage-2 survivors go to a second queue flushed to HBM with one atomic.
 template <bool NOPRUNE>
 __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
-    const PFRec *__restrict__ prow, const PFAux *__restrict__ arow, int nrows,
-    const PFRec *__restrict__ pcol, const PFAux *__restrict__ acol, int ncols,
+    const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, int nrows,
+    const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, int ncols,
     const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ gbox_c,
     const uint2 *__restrict__ tiles, Counters *__restrict__ cnt,
-    unsigned long long *__restrict__ work, RefineParams rp,
+    unsigned long long *__restrict__ work, RefineParams prm,
     uint2 *__restrict__ cand, unsigned long long cap) {
-  __shared__ unsigned q1s[PF_WAVES][PF_Q1];
+  __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ uint2 q2s[PF_WAVES][PF_Q2];
+  __shared__ float4 csa[PF_WAVES][kGroup];    // staged column group: e n s k   (stage 1)
+  __shared__ float2 csb[PF_WAVES][kGroup];    //                      lo hi     (stage 1)
+  __shared__ float4 csx[PF_WAVES][kGroup];    //                      x y z -   (refine)
+  __shared__ float4 csc[PF_WAVES][kGroup];    //                      u v vs alt (refine)
+  __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:         u v vs alt (refine)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned long long ntiles = cnt->tiles;
-  unsigned *q1 = q1s[w];
+  unsigned short *q1 = q1s[w];
   uint2 *q2 = q2s[w];
+  float4 *sa = csa[w];
+  float2 *sb = csb[w];
+  float4 *sx = csx[w];
+  float4 *sc = csc[w];
+  float4 *rv = rsv[w];
   unsigned n2 = 0;        // wave-uniform
   unsigned groups = 0;    // 64-column groups swept by this wave (for the roofline)
   const float qnan = __builtin_nanf("");
@@ -474,6 +530,10 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
   const unsigned long long nitems = ntiles * PF_WAVES;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
+#ifdef BSA_PF_STAMPS
+  unsigned long long st_acc[4] = {0, 0, 0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     unsigned long long m = 0;
     if (lane == 0) m = atomicAdd(wq, 1ull);
@@ -483,128 +543,217 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     const int rbase = (int)rc.x * kTile + (int)(item % PF_WAVES) * PF_WROWS;
     if (rbase >= nrows) continue;
     const int cbase = (int)rc.y * kTile;
+    // column groups of this tile that may interact with the wave's row box
+    const int ng = min(kTile / kGroup, (ncols - cbase + kGroup - 1) / kGroup);
+    TileBox rbx = gbox_r[rbase / kGroup];
+    if (rbase + 64 < nrows) rbx = box_union(rbx, gbox_r[rbase / kGroup + 1]);
+    const bool gk = lane < ng && (NOPRUNE || boxes_may_interact(rbx, gbox_c[cbase / kGroup + lane]));
+    unsigned gm = (unsigned)__ballot(gk);
+    if (!gm) continue;
+    groups += (unsigned)__popc(gm);
+
+    // the next group's column record of this lane (loaded one group ahead)
+    auto load_col = [&](int g, PFRec &r, PFVel &v) {
+      const int j = cbase + g * kGroup + lane;
+      if (j < ncols) {
+        r = pcol[j];
+        v = vcol[j];
+      } else {
+        r.x = r.y = r.z = r.s = qnan;
+        r.lo = INFINITY;
+        r.hi = -INFINITY;
+        r.alt = r.pad = 0.f;
+        v.u = v.v = v.vs = qnan;
+        v.flags = 1;
+      }
+    };
+    int g = __builtin_ctz(gm);
+    PFRec nx;
+    PFVel nv;
+    load_col(g, nx, nv);
+
     const int ka_row = rbase + lane, kb_row = rbase + 64 + lane;
     const bool va = ka_row < nrows, vb = kb_row < nrows;
     PFRec A, B;
-    if (va) A = prow[ka_row]; else { A.x = A.y = A.z = qnan; A.s = A.alt = A.h = A.u = A.v = 0.f; }
-    if (vb) B = prow[kb_row]; else { B.x = B.y = B.z = qnan; B.s = B.alt = B.h = B.u = B.v = 0.f; }
-    const f2 X = {A.x, B.x}, Y = {A.y, B.y}, Z = {A.z, B.z};
-    const f2 S = {A.s, B.s}, AL = {A.alt, B.alt}, HH = {A.h, B.h};
-    TileBox rbx = gbox_r[rbase / kGroup];
-    if (rbase + 64 < nrows) rbx = box_union(rbx, gbox_r[rbase / kGroup + 1]);
+    PFVel AV, BV;
+    if (va) { A = prow[ka_row]; AV = vrow[ka_row]; }
+    else { A.x = A.y = A.z = A.s = A.alt = A.pad = 0.f; A.lo = A.hi = 0.f; AV.u = AV.v = AV.vs = 0.f; AV.flags = 1; }
+    if (vb) { B = prow[kb_row]; BV = vrow[kb_row]; }
+    else { B.x = B.y = B.z = B.s = B.alt = B.pad = 0.f; B.lo = B.hi = 0.f; BV.u = BV.v = BV.vs = 0.f; BV.flags = 1; }
+    // the item's plane: o = first row of the slice, E / N an orthonormal
+    // tangent pair at o (any orthonormal pair is exact-safe; near a pole, or
+    // for a non-finite o, the x / y axes)
+    const PFRec O = prow[rbase];
+    float ex = 1.f, ey = 0.f, nxx = 0.f, nyy = 1.f, nzz = 0.f;
+    {
+      const float rho2 = O.x * O.x + O.y * O.y;
+      if (rho2 > 1e-6f && rho2 <= 1.f) {
+        const float ir = __builtin_amdgcn_rsqf(rho2);
+        const float rho = rho2 * ir;
+        ex = -O.y * ir;
+        ey = O.x * ir;
+        nxx = -O.z * O.x * ir;
+        nyy = -O.z * O.y * ir;
+        nzz = rho;
+      }
+    }
+    const float ox = isfinite(O.x) ? O.x : 0.f, oy = isfinite(O.y) ? O.y : 0.f,
+                oz = isfinite(O.z) ? O.z : 0.f;
+    auto project = [&](float x, float y, float z, float &e, float &n) {
+      const float dx = x - ox, dy = y - oy, dz = z - oz;
+      e = dx * ex + dy * ey;
+      n = dx * nxx + dy * nyy + dz * nzz;
+    };
+    float ea, na, eb, nb;
+    project(A.x, A.y, A.z, ea, na);
+    project(B.x, B.y, B.z, eb, nb);
+    const f2 E = {ea, eb}, N = {na, nb}, S = {A.s, B.s};
+    const f2 K = {0.5f * A.s * A.s - 0.5f * (ea * ea + na * na) + kPlaneMargin,
+                  0.5f * B.s * B.s - 0.5f * (eb * eb + nb * nb) + kPlaneMargin};
+    const f2 HI = {A.hi, B.hi}, LO = {A.lo, B.lo};
+    const float rxa = A.x, rya = A.y, rza = A.z, rxb = B.x, ryb = B.y, rzb = B.z;
+    // rows of this item for the refine (u = NaN: never refine)
+    rv[lane] = make_float4(AV.flags ? qnan : AV.u, AV.v, AV.vs, A.alt);
+    rv[64 + lane] = make_float4(BV.flags ? qnan : BV.u, BV.v, BV.vs, B.alt);
+    const unsigned rowmask_a = va ? 0xffu : 0u, rowmask_b = vb ? 0xffu : 0u;
     unsigned n1 = 0;  // wave-uniform
-    const int ng = min(kTile / kGroup, (ncols - cbase + kGroup - 1) / kGroup);
+    int gs = g;       // the group being swept (its columns are staged)
+    unsigned long long colmask = 0;  // valid columns of the swept group
 
     auto drain = [&]() {
       __builtin_amdgcn_wave_barrier();
+      PF_STAMP(1);
       for (unsigned b0 = 0; b0 < n1; b0 += 64) {
         const unsigned k = b0 + lane;
+        const unsigned e = q1[k < n1 ? k : b0];
+        const unsigned rl = e >> 6, cl = e & 63u;
+        // the row's unit vector from its owner lane's registers
+        const int src = (int)((rl & 63u) << 2);
+        const float pxa = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rxa)));
+        const float pxb = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rxb)));
+        const float pya = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rya)));
+        const float pyb = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(ryb)));
+        const float pza = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rza)));
+        const float pzb = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rzb)));
         bool keep = false;
         unsigned gi = 0, gj = 0;
         if (k < n1) {
-          const unsigned e = q1[k];
-          gi = (unsigned)rbase + (e >> 16);
-          gj = (unsigned)cbase + (e & 0xffffu);
-          keep = NOPRUNE ? true : pf_refine(prow[gi], arow[gi], pcol[gj], acol[gj], rp);
+          const bool hb = rl >= 64u;
+          const float4 rpos = make_float4(hb ? pxb : pxa, hb ? pyb : pya, hb ? pzb : pza, 0.f);
+          gi = (unsigned)rbase + rl;
+          gj = (unsigned)(cbase + gs * kGroup) + cl;
+          keep = NOPRUNE ? true : pf_refine(rpos, rv[rl], sx[cl], sc[cl], prm);
         }
-        const unsigned long long m = __ballot(keep);
-        if (m) {
-          if (keep) q2[n2 + lane_prefix(m)] = make_uint2(gi, gj);
-          n2 = __builtin_amdgcn_readfirstlane(n2 + (unsigned)__popcll(m));
+        const unsigned long long mk = __ballot(keep);
+        if (mk) {
+          if (keep) q2[n2 + lane_prefix(mk)] = make_uint2(gi, gj);
+          n2 = __builtin_amdgcn_readfirstlane(n2 + (unsigned)__popcll(mk));
           if (n2 > (unsigned)(PF_Q2 - 64)) {
+            PF_STAMP(2);
             pf_flush(q2, n2, lane, cand, &cnt->cand, cap);
             n2 = 0;
+            PF_STAMP(3);
           }
         }
       }
       n1 = 0;
       __builtin_amdgcn_wave_barrier();
+      PF_STAMP(2);
     };
 
-    // stage 1 for one column record, packed over the lane's two rows; the
-    // survivors of an 8-column chunk accumulate as per-lane bit masks and are
-    // queued once per chunk (one wave prefix sum instead of per-column ballots)
-    auto reach = [&](const PFRec &c, bool &ka, bool &kb) {
-      if (NOPRUNE) {
-        ka = va;
-        kb = vb;
-      } else {
-        const f2 dx = (f2){c.x, c.x} - X, dy = (f2){c.y, c.y} - Y, dz = (f2){c.z, c.z} - Z;
-        f2 d2 = dx * dx;
-        d2 = __builtin_elementwise_fma(dy, dy, d2);
-        d2 = __builtin_elementwise_fma(dz, dz, d2);
-        const f2 st = S + (f2){c.s, c.s};
-        const f2 st2 = st * st;
-        const f2 dh = (f2){c.alt, c.alt} - AL;
-        const f2 hh = HH + (f2){c.h, c.h};
-        ka = (d2.x < st2.x) & (__builtin_fabsf(dh.x) < hh.x);
-        kb = (d2.y < st2.y) & (__builtin_fabsf(dh.y) < hh.y);
-      }
-    };
+    // survivors of an 8-column chunk arrive as per-lane bit masks (ba: row a,
+    // bb: row b; bit 7 - u = column col0 + u) and are queued once per chunk
     auto enqueue = [&](unsigned ba, unsigned bb, unsigned col0) {
-      const unsigned cnt = (unsigned)__popc(ba) + (unsigned)__popc(bb);
-      if (!__ballot(cnt != 0)) return;
-      unsigned x = cnt;  // inclusive wave prefix sum of cnt
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-      }
+      const unsigned c = (unsigned)__popc(ba) + (unsigned)__popc(bb);
+      const unsigned x = wave_incl_scan(c);
       const unsigned total = __builtin_amdgcn_readlane(x, 63);
-      if (n1 + total > (unsigned)PF_Q1) drain();  // total <= 2 * 64 * 8 = PF_Q1
-      unsigned pos = n1 + x - cnt;
+      if (total == 0) return;
+      if (n1 + total > (unsigned)PF_Q1) drain();
+      unsigned pos = n1 + x - c;
       while (ba) {
-        q1[pos++] = ((unsigned)lane << 16) | (col0 + (unsigned)__builtin_ctz(ba));
-        ba &= ba - 1;
+        const unsigned b = 31u - (unsigned)__builtin_clz(ba);
+        q1[pos++] = (unsigned short)(((unsigned)lane << 6) | (col0 + 7u - b));
+        ba ^= 1u << b;
       }
       while (bb) {
-        q1[pos++] = ((unsigned)(64 + lane) << 16) | (col0 + (unsigned)__builtin_ctz(bb));
-        bb &= bb - 1;
+        const unsigned b = 31u - (unsigned)__builtin_clz(bb);
+        q1[pos++] = (unsigned short)(((unsigned)(64 + lane) << 6) | (col0 + 7u - b));
+        bb ^= 1u << b;
       }
       n1 = __builtin_amdgcn_readfirstlane(n1 + total);
     };
 
-    for (int g = 0; g < ng; ++g) {
-      const int c0 = cbase + g * kGroup;
-      if (!NOPRUNE && !boxes_may_interact(rbx, gbox_c[c0 / kGroup])) continue;
-      ++groups;
-      const int nc = min(kGroup, ncols - c0);
-      const unsigned cl0 = (unsigned)(g * kGroup);
-      if (nc == kGroup) {
-        for (int j0 = 0; j0 < kGroup; j0 += 8) {
-          unsigned ba = 0, bb = 0;
+    PF_STAMP(0);
+    for (;;) {
+      // project and stage the current group (in-order LDS within the wave:
+      // these writes land after the previous group's reads, incl. its drain)
+      {
+        float ce, cn;
+        project(nx.x, nx.y, nx.z, ce, cn);
+        const float ck = 0.5f * nx.s * nx.s - 0.5f * (ce * ce + cn * cn);
+        sa[lane] = make_float4(ce, cn, nx.s, ck);
+        sb[lane] = make_float2(nx.lo, nx.hi);
+        sx[lane] = make_float4(nx.x, nx.y, nx.z, 0.f);
+        sc[lane] = make_float4(nv.flags ? qnan : nv.u, nv.v, nv.vs, nx.alt);
+        colmask = __ballot(cbase + g * kGroup + lane < ncols);
+      }
+      gs = g;
+      gm &= gm - 1;
+      if (gm) {  // prefetch the next group while this one is swept
+        g = __builtin_ctz(gm);
+        load_col(g, nx, nv);
+      }
+      for (int j0 = 0; j0 < kGroup; j0 += 8) {
+        unsigned ba = 0, bb = 0;
 #pragma unroll
-          for (int h4 = 0; h4 < 8; h4 += 4) {
-            PFRec cc[4];
+        for (int h4 = 0; h4 < 8; h4 += 4) {
+          float4 ca[4];
+          float2 cb[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) cc[u] = pcol[c0 + j0 + h4 + u];
+          for (int u = 0; u < 4; ++u) {
+            ca[u] = sa[j0 + h4 + u];
+            cb[u] = sb[j0 + h4 + u];
+          }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              bool ka, kb;
-              reach(cc[u], ka, kb);
-              ba |= (unsigned)ka << (h4 + u);
-              bb |= (unsigned)kb << (h4 + u);
+          for (int u = 0; u < 4; ++u) {
+            if (NOPRUNE) {
+              ba = (ba << 1) | 1u;
+              bb = (bb << 1) | 1u;
+            } else {
+              f2 acc = K + (f2){ca[u].w, ca[u].w};
+              acc = __builtin_elementwise_fma(S, (f2){ca[u].z, ca[u].z}, acc);
+              acc = __builtin_elementwise_fma(E, (f2){ca[u].x, ca[u].x}, acc);
+              acc = __builtin_elementwise_fma(N, (f2){ca[u].y, ca[u].y}, acc);
+              const f2 dlo = (f2){cb[u].x, cb[u].x} - HI;   // < 0 to keep
+              const f2 dhi = (f2){cb[u].y, cb[u].y} - LO;   // > 0 to keep
+              const unsigned ta = (unsigned)__float_as_int(dlo.x) &
+                                  ~((unsigned)__float_as_int(acc.x) | (unsigned)__float_as_int(dhi.x));
+              const unsigned tb = (unsigned)__float_as_int(dlo.y) &
+                                  ~((unsigned)__float_as_int(acc.y) | (unsigned)__float_as_int(dhi.y));
+              ba = __builtin_amdgcn_alignbit(ba, ta, 31);   // (ba << 1) | (ta >> 31)
+              bb = __builtin_amdgcn_alignbit(bb, tb, 31);
             }
           }
-          enqueue(ba, bb, cl0 + (unsigned)j0);
         }
-      } else {
-        for (int j0 = 0; j0 < nc; j0 += 8) {
-          unsigned ba = 0, bb = 0;
-          for (int u = 0; u < 8 && j0 + u < nc; ++u) {
-            bool ka, kb;
-            reach(pcol[c0 + j0 + u], ka, kb);
-            ba |= (unsigned)ka << u;
-            bb |= (unsigned)kb << u;
-          }
-          enqueue(ba, bb, cl0 + (unsigned)j0);
-        }
+        const unsigned cm = (unsigned)(colmask >> j0) & 0xffu;
+        // bit 7 - u <-> column j0 + u: reverse the 8 column-valid bits
+        const unsigned cmr = __builtin_bitreverse32(cm) >> 24;
+        enqueue(ba & cmr & rowmask_a, bb & cmr & rowmask_b, (unsigned)j0);
       }
+      // refine this group's survivors while its columns are staged
+      if (n1) drain();
+      PF_STAMP(1);
+      if (!gm) break;
     }
-    if (n1) drain();
   }
+  PF_STAMP(0);
   if (n2) pf_flush(q2, n2, lane, cand, &cnt->cand, cap);
   if (lane == 0 && groups) atomicAdd(&cnt->groups, (unsigned long long)groups);
+#ifdef BSA_PF_STAMPS
+  PF_STAMP(3);
+  if (lane == 0)
+    for (int k = 0; k < 4; ++k) atomicAdd(&cnt->stamp[k], st_acc[k]);
+#endif
 }
 
 // ------------------------------------------------------------------ K1b exact
@@ -937,16 +1086,16 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
       !ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
       !ensure(c, c->pfrow, nrows * sizeof(PFRec), "prefilter rows") ||
       !ensure(c, c->pfcol, n * sizeof(PFRec), "prefilter columns") ||
-      !ensure(c, c->pfauxrow, nrows * sizeof(PFAux), "prefilter row aux") ||
-      !ensure(c, c->pfauxcol, n * sizeof(PFAux), "prefilter column aux"))
+      !ensure(c, c->pfvrow, nrows * sizeof(PFVel), "prefilter row velocities") ||
+      !ensure(c, c->pfvcol, n * sizeof(PFVel), "prefilter column velocities"))
     return -1;
   hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, perm_r,
                      own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p, (PFRec *)c->pfrow.p,
-                     (PFAux *)c->pfauxrow.p);
+                     (PFVel *)c->pfvrow.p);
   BSA_HIP(c, hipGetLastError());
   hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n, perm_c, own,
                      intr, distinct ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p, (PFRec *)c->pfcol.p,
-                     (PFAux *)c->pfauxcol.p);
+                     (PFVel *)c->pfvcol.p);
   BSA_HIP(c, hipGetLastError());
   // ---- K0c/K0d group / tile boxes and the tile-pair work list
   const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
@@ -991,21 +1140,21 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
         !ensure(c, c->cpay, cap * 5 * 8, "candidate payload"))
       return -1;
     if (attempt > 0 && zero(0)) return -1;
-    // ---- K1a prefilter: persistent grid, 6 workgroups per CU (LDS/SGPR-limited
-    // residency), at least one workgroup per dequeue shard
-    const unsigned pf_grid =
-        (unsigned)std::max<long long>(kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * 6));
+    // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
+    // (LDS-limited residency), at least one workgroup per dequeue shard
+    const unsigned pf_grid = (unsigned)std::max<long long>(
+        kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * PF_BLOCKS_PER_CU));
     if (noprune)
       hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
-                         (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
-                         (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
+                         (const PFRec *)c->pfrow.p, (const PFVel *)c->pfvrow.p, (int)nrows,
+                         (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n,
                          (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
                          (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
                          (uint2 *)c->cand.p, cap);
     else
       hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
-                         (const PFRec *)c->pfrow.p, (const PFAux *)c->pfauxrow.p, (int)nrows,
-                         (const PFRec *)c->pfcol.p, (const PFAux *)c->pfauxcol.p, (int)n,
+                         (const PFRec *)c->pfrow.p, (const PFVel *)c->pfvrow.p, (int)nrows,
+                         (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n,
                          (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
                          (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
                          (uint2 *)c->cand.p, cap);
@@ -1035,6 +1184,10 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
     if (attempt > 3) return fail(c, "candidate buffer overflow (%llu)", h.cand);
     c->cand_cap = h.cand + h.cand / 4 + 1024;
   }
+#ifdef BSA_PF_STAMPS
+  fprintf(stderr, "[bsa stamps] prefilter wave-cycles: setup %.4g stage1 %.4g drain %.4g flush %.4g\n",
+          (double)h.stamp[0], (double)h.stamp[1], (double)h.stamp[2], (double)h.stamp[3]);
+#endif
   c->last_cand = (int64_t)h.cand;
   c->last_tiles = (int64_t)h.tiles;
   c->last_tiles_total = ntp;

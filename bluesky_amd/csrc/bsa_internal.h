@@ -52,35 +52,35 @@ struct alignas(16) ColRec {
 static_assert(sizeof(RowRec) == 128, "RowRec must be one cache line");
 static_assert(sizeof(ColRec) == 128, "ColRec must be one cache line");
 
-// fp32 prefilter record (32 B): unit-sphere position + conservative
-// horizontal / vertical reach terms (see DESIGN.md "exact-safe prefilter").
+// fp32 prefilter record (32 B), one per sorted row / column.
+// Stage 1 keeps a pair iff chord < s_i + s_j (tested in a plane, see
+// k_prefilter) and lo_j < hi_i and hi_j > lo_i (<=> |alt_j - alt_i| < h_i + h_j).
 struct alignas(16) PFRec {
   float x, y, z;   // unit vector of the position
-  float s;         // horizontal reach, chord units (half of the pair bound)
+  float s;         // horizontal reach, chord units (half of the pair bound); INF = always
+  float lo, hi;    // alt -/+ h, h = vertical reach [m] (half of the pair bound)
   float alt;       // altitude [m]
-  float h;         // vertical reach [m] (half of the pair bound)
-  float u, v;      // east / north velocity [m/s] (same orientation as RowRec/ColRec)
+  float pad;
 };
 static_assert(sizeof(PFRec) == 32, "PFRec must be 32 B");
 
-// cold part of the prefilter record, read only by the CPA refine
-struct alignas(16) PFAux {
+// velocity part, read only by the CPA refine (rows and columns)
+struct alignas(16) PFVel {
+  float u, v;      // east / north velocity [m/s] (orientation as RowRec / ColRec)
   float vs;        // vertical speed [m/s]
   unsigned flags;  // bit 0: never refine this index (unbounded radius quirk / non-finite
                    //        / tangent basis ill-conditioned near a pole)
-  float ex, ey;    // rows: local east unit vector at the position (ez = 0)
-  float nx, ny, nz;  //       local north unit vector
-  float pad;
 };
-static_assert(sizeof(PFAux) == 32, "PFAux must be 32 B");
+static_assert(sizeof(PFVel) == 16, "PFVel must be 16 B");
 
-// axis-aligned bounds of one tile of sorted PFRecs (tile culling)
+// axis-aligned bounds of a group / tile of sorted PFRecs (culling)
 struct alignas(16) TileBox {
-  float lo[3], hi[3];
-  float altlo, althi;
-  float smax, hmax;
-  int count, pad;
+  float lo[3], hi[3];   // unit-vector bounds
+  float vlo, vhi;       // min lo, max hi (vertical reach intervals)
+  float smax, pad0;
+  int count, pad1;
 };
+static_assert(sizeof(TileBox) == 48, "TileBox must be 48 B");
 
 constexpr int kTile = 512;  // rows per row block == columns per column tile
 constexpr int kResortEvery = 8;  // detect calls between spatial re-sorts
@@ -93,6 +93,8 @@ struct Counters {
   unsigned long long tiles;
   unsigned long long groups;  // (128-row x 64-column) groups swept by the prefilter
   unsigned long long pad[3];
+  // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
+  unsigned long long stamp[8];
 };
 
 // ---------------------------------------------------------------- buffers
@@ -115,7 +117,7 @@ struct Ctx {
   bool has_intruder = false;
   DevBuf own[6];   // lat lon trk gs alt vs
   DevBuf intr[6];
-  DevBuf rowrec, colrec, pfrow, pfcol, pfauxrow, pfauxcol;
+  DevBuf rowrec, colrec, pfrow, pfcol, pfvrow, pfvcol;
   // spatial order: Morton keys and the sorted-position -> original-index maps
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
   DevBuf tbox_r, tbox_c, gbox_r, gbox_c, tilepairs, workq;
