@@ -74,27 +74,22 @@ def main():
     sim.step(args.warmup)
     ctx.allreduce_max([0.0])     # barrier
     ctx.sync()
-    pf, ex, tot, kept = [], [], [], []
+    ctx.timing_reset()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sim.step(1)
-        tm = ctx.last_timings()
-        pf.append(tm['prefilter'])
-        ex.append(tm['exact'])
-        tot.append(tm['total'])
-        kept.append(ctx.last_tiles()[2])      # (128-row x 64-col) groups swept
+    sim.step(args.steps)         # one batch: no host synchronisation between steps
     ctx.sync()
     ctx.allreduce_max([0.0])     # barrier
     dt_local = time.perf_counter() - t0
     dt = float(ctx.allreduce_max([dt_local])[0])   # max over ranks
+    tm, ts = ctx.timing_summary()
     st = sim.stats()
-    counts = ctx.allreduce_sum([st['n_conf'], st['n_los'], ctx.last_candidates()])
+    counts = ctx.allreduce_sum([st['n_conf'], st['n_los'], ts['candidates'] / max(ts['detects'], 1)])
 
     cd_steps = sum(1 for k in range(args.warmup, args.warmup + args.steps) if k % args.cd_every == 0)
     pairs = float(n) * n * cd_steps
     value = pairs / dt
-    pf_s = float(np.mean(pf)) * 1e-3
-    tested = float(np.mean(kept)) * 128 * 64   # pair tests the prefilter executed
+    pf_s = tm['prefilter'] * 1e-3
+    tested = ts['groups'] / max(ts['detects'], 1) * 128 * 64   # pair tests the prefilter executed
     roof = dict(bound='valu', kernel='k_prefilter (fp32 VALU reach test, dominant)',
                 achieved=tested * PF_FLOPS_PER_PAIR / pf_s / 1e12, peak=FP32_PEAK_TFLOPS,
                 unit='TFLOP/s')
@@ -110,10 +105,10 @@ def main():
                            simdt_s=0.05, parallelism='rows%d' % world),
                sim_steps_per_s=args.steps / dt,
                roofline=roof,
-               kernels_ms_rank0=dict(prefilter=float(np.mean(pf)), exact=float(np.mean(ex)),
-                                     detect_total=float(np.mean(tot))),
+               kernels_ms_rank0=dict(k0_prep=tm['prep'], prefilter=tm['prefilter'], exact=tm['exact'],
+                                     k2_sort=tm['sort'], detect_total=tm['total']),
                prefilter_pair_tests_rank0=tested,
-               tile_pairs_rank0=list(ctx.last_tiles()[:2]),
+               tile_pairs_rank0=ts['tiles'] / max(ts['detects'], 1),
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12))
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -50,6 +50,8 @@ SIGNATURES = {
     'bsa_last_candidates': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_last_tiles': (ctypes.c_int, [_vp, _c_i64p, _c_i64p, _c_i64p]),
     'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
+    'bsa_timing_reset': (ctypes.c_int, [_vp]),
+    'bsa_timing_summary': (ctypes.c_int, [_vp, _c_dp, _c_i64p]),
 }
 
 PRIO_CODES = {'FF1': 1, 'FF2': 2, 'FF3': 3, 'LAY1': 4, 'LAY2': 5}
@@ -252,6 +254,19 @@ class Context:
         t = np.zeros(5)
         self.check(self.lib.bsa_last_timings(self.h, ptr(t)), 'bsa_last_timings')
         return dict(prep=t[0], prefilter=t[1], exact=t[2], sort=t[3], total=t[4])
+
+    def timing_reset(self):
+        """Forget recorded detect timings / statistics (bsa_timing_reset)."""
+        self.check(self.lib.bsa_timing_reset(self.h), 'bsa_timing_reset')
+
+    def timing_summary(self):
+        """Mean stage times [ms] over the detects since the last reset and the
+        summed statistics (bsa_timing_summary)."""
+        t = np.zeros(5)
+        st = np.zeros(4, np.int64)
+        self.check(self.lib.bsa_timing_summary(self.h, ptr(t), ptr(st, _c_i64p)), 'bsa_timing_summary')
+        return (dict(prep=t[0], prefilter=t[1], exact=t[2], sort=t[3], total=t[4]),
+                dict(groups=int(st[0]), candidates=int(st[1]), tiles=int(st[2]), detects=int(st[3])))
 
     def sync(self):
         self.check(self.lib.bsa_sync(self.h), 'bsa_sync')

@@ -174,9 +174,10 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
 
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
 __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__restrict__ perm,
-                                                   SoA6 own, SoA6 intr, int distinct, double rpz,
-                                                   double hpz, double tla, ColRec *__restrict__ C,
-                                                   PFRec *__restrict__ PC, PFVel *__restrict__ PV) {
+                                                   SoA6 own, SoA6 intr, int distinct, int shared,
+                                                   double rpz, double hpz, double tla,
+                                                   ColRec *__restrict__ C, PFRec *__restrict__ PC,
+                                                   PFVel *__restrict__ PV) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const int o = (int)perm[k];
@@ -213,6 +214,8 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
   v.v = (float)c.v;
   v.vs = (float)c.vs;
   v.flags = (quirk || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) ? 1u : 0u;
+  // shared records also serve as rows: add the rows' pole flag (k_prep_rows)
+  if (shared && !(cosl > 1e-2)) v.flags = 1u;
   PC[k] = p;
   PV[k] = v;
 }
@@ -228,18 +231,37 @@ __device__ __forceinline__ float wmax(float v) {
 }
 
 // Bounds of every group of kGroup (= one wave's 64 lanes) consecutive sorted
-// records: one wave per group, lane = record.  NaN coordinates drop out of
-// the min/max (fminf/fmaxf), which is safe: a record with a NaN coordinate
+// records and of every tile (kTile / kGroup groups).  NaN coordinates drop out
+// of the min/max (fminf/fmaxf), which is safe: a record with a NaN coordinate
 // never passes the reach test.
 constexpr int kGroup = 64;
 static_assert(kTile % kGroup == 0, "tiles are whole groups");
+constexpr int kGroupsPerTile = kTile / kGroup;
 
-__global__ __launch_bounds__(256) void k_groupbox(int cnt, const PFRec *__restrict__ P,
-                                                  TileBox *__restrict__ box) {
-  const int g = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+__device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b) {
+  TileBox u;
+  for (int q = 0; q < 3; ++q) {
+    u.lo[q] = fminf(a.lo[q], b.lo[q]);
+    u.hi[q] = fmaxf(a.hi[q], b.hi[q]);
+  }
+  u.vlo = fminf(a.vlo, b.vlo);
+  u.vhi = fmaxf(a.vhi, b.vhi);
+  u.smax = fmaxf(a.smax, b.smax);
+  u.pad0 = 0.f;
+  u.count = a.count + b.count;
+  u.pad1 = 0;
+  return u;
+}
+
+// one workgroup per tile, one wave per group (lane = record): group boxes to
+// gbox, their union to tbox
+__global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restrict__ P,
+                                                 TileBox *__restrict__ gbox, TileBox *__restrict__ tbox) {
+  __shared__ TileBox gb[kGroupsPerTile];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int g = blockIdx.x * kGroupsPerTile + w;
   const int k = g * kGroup + lane;
   const int ngroups = (cnt + kGroup - 1) / kGroup;
-  if (g >= ngroups) return;  // whole wave exits together
   float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   float smax = 0.f;
   if (k < cnt) {
@@ -266,36 +288,17 @@ __global__ __launch_bounds__(256) void k_groupbox(int cnt, const PFRec *__restri
     b.vhi = hi[3];
     b.smax = smax;
     b.pad0 = 0.f;
-    b.count = min(kGroup, cnt - g * kGroup);
+    b.count = g < ngroups ? min(kGroup, cnt - g * kGroup) : 0;
     b.pad1 = 0;
-    box[g] = b;
+    gb[w] = b;
+    if (g < ngroups) gbox[g] = b;
   }
-}
-
-__device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b) {
-  TileBox u;
-  for (int q = 0; q < 3; ++q) {
-    u.lo[q] = fminf(a.lo[q], b.lo[q]);
-    u.hi[q] = fmaxf(a.hi[q], b.hi[q]);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    TileBox u = gb[0];
+    for (int q = 1; q < kGroupsPerTile; ++q) u = box_union(u, gb[q]);
+    tbox[blockIdx.x] = u;
   }
-  u.vlo = fminf(a.vlo, b.vlo);
-  u.vhi = fmaxf(a.vhi, b.vhi);
-  u.smax = fmaxf(a.smax, b.smax);
-  u.pad0 = 0.f;
-  u.count = a.count + b.count;
-  u.pad1 = 0;
-  return u;
-}
-
-// tile box = union of its kTile / kGroup group boxes
-__global__ __launch_bounds__(256) void k_tileunion(int ntiles, int ngroups, const TileBox *__restrict__ g,
-                                                   TileBox *__restrict__ t) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= ntiles) return;
-  const int g0 = k * (kTile / kGroup), g1 = min(ngroups, g0 + kTile / kGroup);
-  TileBox u = g[g0];
-  for (int q = g0 + 1; q < g1; ++q) u = box_union(u, g[q]);
-  t[k] = u;
 }
 
 // ------------------------------------------------------------------ K0d tile pairs
@@ -507,7 +510,7 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     uint2 *__restrict__ cand, unsigned long long cap) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ uint2 q2s[PF_WAVES][PF_Q2];
-  __shared__ float4 csa[PF_WAVES][kGroup];    // staged column group: e n s k   (stage 1)
+  __shared__ float4 csa[PF_WAVES][kGroup];    // staged column group: k s e n   (stage 1)
   __shared__ float2 csb[PF_WAVES][kGroup];    //                      lo hi     (stage 1)
   __shared__ float4 csx[PF_WAVES][kGroup];    //                      x y z -   (refine)
   __shared__ float4 csc[PF_WAVES][kGroup];    //                      u v vs alt (refine)
@@ -530,18 +533,27 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
   const unsigned long long nitems = ntiles * PF_WAVES;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
+  // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
+  // its own counter (spreads the flush atomics over kCandShards addresses)
+  const unsigned long long ccap = cap / kCandShards;
+  uint2 *ccand = cand + (unsigned long long)(shard % kCandShards) * ccap;
+  unsigned long long *cshard = &cnt->cshard[shard % kCandShards][0];
 #ifdef BSA_PF_STAMPS
   unsigned long long st_acc[4] = {0, 0, 0, 0};
   unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
-    unsigned long long m = 0;
-    if (lane == 0) m = atomicAdd(wq, 1ull);
-    const unsigned long long item = wave_bcast_u64(m) * kWorkShards + shard;
+    unsigned long long item;
+    {
+      unsigned long long m0 = 0;
+      if (lane == 0) m0 = atomicAdd(wq, 1ull);
+      item = wave_bcast_u64(m0) * kWorkShards + shard;
+    }
     if (item >= nitems) break;
+    do {  // one item; `break` ends it
     const uint2 rc = tiles[item / PF_WAVES];
     const int rbase = (int)rc.x * kTile + (int)(item % PF_WAVES) * PF_WROWS;
-    if (rbase >= nrows) continue;
+    if (rbase >= nrows) break;
     const int cbase = (int)rc.y * kTile;
     // column groups of this tile that may interact with the wave's row box
     const int ng = min(kTile / kGroup, (ncols - cbase + kGroup - 1) / kGroup);
@@ -549,7 +561,7 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     if (rbase + 64 < nrows) rbx = box_union(rbx, gbox_r[rbase / kGroup + 1]);
     const bool gk = lane < ng && (NOPRUNE || boxes_may_interact(rbx, gbox_c[cbase / kGroup + lane]));
     unsigned gm = (unsigned)__ballot(gk);
-    if (!gm) continue;
+    if (!gm) break;
     groups += (unsigned)__popc(gm);
 
     // the next group's column record of this lane (loaded one group ahead)
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
           n2 = __builtin_amdgcn_readfirstlane(n2 + (unsigned)__popcll(mk));
           if (n2 > (unsigned)(PF_Q2 - 64)) {
             PF_STAMP(2);
-            pf_flush(q2, n2, lane, cand, &cnt->cand, cap);
+            pf_flush(q2, n2, lane, ccand, cshard, ccap);
             n2 = 0;
             PF_STAMP(3);
           }
@@ -691,7 +703,7 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
         float ce, cn;
         project(nx.x, nx.y, nx.z, ce, cn);
         const float ck = 0.5f * nx.s * nx.s - 0.5f * (ce * ce + cn * cn);
-        sa[lane] = make_float4(ce, cn, nx.s, ck);
+        sa[lane] = make_float4(ck, nx.s, ce, cn);
         sb[lane] = make_float2(nx.lo, nx.hi);
         sx[lane] = make_float4(nx.x, nx.y, nx.z, 0.f);
         sc[lane] = make_float4(nv.flags ? qnan : nv.u, nv.v, nv.vs, nx.alt);
@@ -720,10 +732,10 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
               ba = (ba << 1) | 1u;
               bb = (bb << 1) | 1u;
             } else {
-              f2 acc = K + (f2){ca[u].w, ca[u].w};
-              acc = __builtin_elementwise_fma(S, (f2){ca[u].z, ca[u].z}, acc);
-              acc = __builtin_elementwise_fma(E, (f2){ca[u].x, ca[u].x}, acc);
-              acc = __builtin_elementwise_fma(N, (f2){ca[u].y, ca[u].y}, acc);
+              f2 acc = K + (f2){ca[u].x, ca[u].x};
+              acc = __builtin_elementwise_fma(S, (f2){ca[u].y, ca[u].y}, acc);
+              acc = __builtin_elementwise_fma(E, (f2){ca[u].z, ca[u].z}, acc);
+              acc = __builtin_elementwise_fma(N, (f2){ca[u].w, ca[u].w}, acc);
               const f2 dlo = (f2){cb[u].x, cb[u].x} - HI;   // < 0 to keep
               const f2 dhi = (f2){cb[u].y, cb[u].y} - LO;   // > 0 to keep
               const unsigned ta = (unsigned)__float_as_int(dlo.x) &
@@ -745,9 +757,10 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
       PF_STAMP(1);
       if (!gm) break;
     }
+    } while (0);
   }
   PF_STAMP(0);
-  if (n2) pf_flush(q2, n2, lane, cand, &cnt->cand, cap);
+  if (n2) pf_flush(q2, n2, lane, ccand, cshard, ccap);
   if (lane == 0 && groups) atomicAdd(&cnt->groups, (unsigned long long)groups);
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
@@ -757,6 +770,25 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
 }
 
 // ------------------------------------------------------------------ K1b exact
+// flat candidate index space: shard s holds min(count_s, cap / kCandShards)
+// candidates; pre[s] = candidates of the shards before s, returns the total
+__device__ __forceinline__ unsigned long long cand_prefix(const Counters *cnt, unsigned long long cap,
+                                                          unsigned long long *pre) {
+  const unsigned long long ccap = cap / kCandShards;
+  pre[0] = 0;
+#pragma unroll
+  for (int q = 0; q < kCandShards; ++q) pre[q + 1] = pre[q] + min(cnt->cshard[q][0], ccap);
+  return pre[kCandShards];
+}
+__device__ __forceinline__ bool cand_overflow(const Counters *cnt, unsigned long long cap) {
+  const unsigned long long ccap = cap / kCandShards;
+  bool o = false;
+#pragma unroll
+  for (int q = 0; q < kCandShards; ++q) o |= cnt->cshard[q][0] > ccap;
+  return o;
+}
+
+
 struct PairResult {
   bool conf, los;
   double qdr, dist, tcpa, tin, dcpa;
@@ -839,16 +871,22 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
 __global__ __launch_bounds__(256) void k_exact(
     const RowRec *__restrict__ R, const ColRec *__restrict__ C,
     const unsigned *__restrict__ perm_r, const unsigned *__restrict__ perm_c,
-    const uint2 *__restrict__ cand, const unsigned long long *__restrict__ ncand_p,
+    const uint2 *__restrict__ cand, const Counters *__restrict__ cnt,
     unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
     unsigned char *__restrict__ cflag, unsigned long long *__restrict__ ckey,
     double *__restrict__ cpay, unsigned char *__restrict__ inconf,
     unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt) {
-  const unsigned long long ncand = min(*ncand_p, cap);
+  if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
+  unsigned long long pre[kCandShards + 1];
+  const unsigned long long ncand = cand_prefix(cnt, cap, pre);
+  const unsigned long long ccap = cap / kCandShards;
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long idx = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
        idx < ncand; idx += stride) {
-    const uint2 p = cand[idx];
+    int sh = 0;
+#pragma unroll
+    for (int q = 1; q < kCandShards; ++q) sh += (idx >= pre[q]) ? 1 : 0;
+    const uint2 p = cand[(unsigned long long)sh * ccap + (idx - pre[sh])];
     const unsigned oi = perm_r[p.x], oj = perm_c[p.y];
     unsigned char flag = 0;
     if (oi != oj) {
@@ -877,114 +915,155 @@ __global__ __launch_bounds__(256) void k_exact(
 
 // ------------------------------------------------------------------ K2 canonical order
 // Per-row counting sort.  rowcnt holds [conflicts per row | 0 | LoS per row | 0]
-// (2 * (nrows + 1) words); its exclusive scan gives each row's segment in the
-// conflict list and (minus P) in the LoS list.  Pairs are scattered into their
-// row segment, then one lane per row sorts its (short) segment by column:
-// the result is exactly np.where's row-major order (StateBasedCD.py:93-95).
-__global__ __launch_bounds__(256) void k_scatter(const unsigned long long *__restrict__ ncand_p,
-                                                 unsigned long long cap, int rb, int nrows,
-                                                 const unsigned char *__restrict__ cflag,
+// (2 (nrows + 1) words); its exclusive scan rowoff gives each row's segment
+// in the conflict list and (minus P) in the LoS list.  k_scatter drops every
+// pair's key into its row segment (in any order); k_rowsort ranks each row's
+// short segment by column in registers, so the lists come out exactly in
+// np.where's row-major order (StateBasedCD.py:93-95).  All counts are read on
+// the device (no host round trip inside a detect), and nothing is written
+// when the candidate list overflowed: the caller retries with more room.
+__global__ __launch_bounds__(256) void k_scatter(const Counters *__restrict__ cnt, unsigned long long cap,
+                                                 int rb, int nrows, const unsigned char *__restrict__ cflag,
                                                  const unsigned long long *__restrict__ ckey,
                                                  const unsigned *__restrict__ rowoff,
                                                  unsigned *__restrict__ rowcnt,
-                                                 unsigned *__restrict__ cslot,
-                                                 unsigned *__restrict__ lslot) {
-  const unsigned long long ncand = min(*ncand_p, cap);
+                                                 unsigned long long *__restrict__ skey,
+                                                 unsigned *__restrict__ sslot,
+                                                 unsigned long long *__restrict__ lkey) {
+  if (cand_overflow(cnt, cap)) return;
+  unsigned long long pre[kCandShards + 1];
+  const unsigned long long ncand = cand_prefix(cnt, cap, pre);
   const unsigned P = rowoff[nrows];
   const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
   for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < ncand;
        k += stride) {
     const unsigned char f = cflag[k];
     if (!f) continue;
-    const int row = (int)(ckey[k] >> 32) - rb;
+    const unsigned long long key = ckey[k];
+    const int row = (int)(key >> 32) - rb;
     if (f & 1) {
       const unsigned pos = rowoff[row] + atomicSub(&rowcnt[row], 1u) - 1u;
-      cslot[pos] = (unsigned)k;
+      skey[pos] = key;
+      sslot[pos] = (unsigned)k;
     }
     if (f & 2) {
       const int r = nrows + 1 + row;
-      const unsigned pos = rowoff[r] - P + atomicSub(&rowcnt[r], 1u) - 1u;
-      lslot[pos] = (unsigned)k;
+      lkey[rowoff[r] - P + atomicSub(&rowcnt[r], 1u) - 1u] = key;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_rowsort(int nrows, int64_t P, const unsigned *__restrict__ rowoff,
-                                                 const unsigned long long *__restrict__ ckey,
-                                                 unsigned *__restrict__ cslot,
-                                                 const double *__restrict__ cpay, unsigned long long cap,
-                                                 unsigned *__restrict__ lslot, int *__restrict__ ci,
-                                                 int *__restrict__ cj, double *__restrict__ out,
-                                                 int *__restrict__ li, int *__restrict__ lj) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrows) return;
-  // conflicts of row r
-  {
-    const unsigned b = rowoff[r], e = rowoff[r + 1];
-    for (unsigned x = b + 1; x < e; ++x) {  // insertion sort by column
-      const unsigned v = cslot[x];
-      const unsigned kv = (unsigned)(ckey[v] & 0xffffffffull);
-      unsigned y = x;
-      while (y > b && (unsigned)(ckey[cslot[y - 1]] & 0xffffffffull) > kv) {
-        cslot[y] = cslot[y - 1];
-        --y;
-      }
-      cslot[y] = v;
-    }
-    for (unsigned x = b; x < e; ++x) {
-      const unsigned v = cslot[x];
-      const unsigned long long kk = ckey[v];
-      ci[x] = (int)(kk >> 32);
-      cj[x] = (int)(kk & 0xffffffffull);
+constexpr int kRankMax = 16;  // segments up to this length are ranked in registers
+
+// rank the keys of segment [b, e) (one row: the column is the low word) and
+// hand each entry's final index to emit(entry, index)
+template <typename Emit>
+__device__ __forceinline__ void rank_segment(unsigned b, unsigned e, unsigned long long *__restrict__ key,
+                                             unsigned *__restrict__ slot, Emit emit) {
+  const unsigned n = e - b;
+  if (n == 0) return;
+  if (n <= (unsigned)kRankMax) {
+    unsigned col[kRankMax];
 #pragma unroll
-      for (int f = 0; f < 5; ++f) out[(int64_t)f * P + x] = cpay[f * cap + v];
-    }
-  }
-  // loss-of-separation pairs of row r
-  {
-    const unsigned b = rowoff[nrows + 1 + r] - (unsigned)P, e = rowoff[nrows + 2 + r] - (unsigned)P;
-    for (unsigned x = b + 1; x < e; ++x) {
-      const unsigned v = lslot[x];
-      const unsigned kv = (unsigned)(ckey[v] & 0xffffffffull);
-      unsigned y = x;
-      while (y > b && (unsigned)(ckey[lslot[y - 1]] & 0xffffffffull) > kv) {
-        lslot[y] = lslot[y - 1];
-        --y;
+    for (int i = 0; i < kRankMax; ++i) col[i] = (unsigned)i < n ? (unsigned)key[b + i] : 0xffffffffu;
+#pragma unroll
+    for (int i = 0; i < kRankMax; ++i) {
+      if ((unsigned)i < n) {
+        unsigned rank = 0;
+#pragma unroll
+        for (int j = 0; j < kRankMax; ++j) rank += (col[j] < col[i]) ? 1u : 0u;
+        emit(b + (unsigned)i, b + rank);
       }
-      lslot[y] = v;
     }
-    for (unsigned x = b; x < e; ++x) {
-      const unsigned long long kk = ckey[lslot[x]];
-      li[x] = (int)(kk >> 32);
-      lj[x] = (int)(kk & 0xffffffffull);
-    }
+    return;
   }
+  // long segment (rare): insertion sort in place, then emit in order
+  for (unsigned x = b + 1; x < e; ++x) {
+    const unsigned long long kv = key[x];
+    const unsigned sv = slot ? slot[x] : 0u;
+    unsigned y = x;
+    while (y > b && (unsigned)key[y - 1] > (unsigned)kv) {
+      key[y] = key[y - 1];
+      if (slot) slot[y] = slot[y - 1];
+      --y;
+    }
+    key[y] = kv;
+    if (slot) slot[y] = sv;
+  }
+  for (unsigned x = b; x < e; ++x) emit(x, x);
 }
 
-// zero the per-detect state in one launch: counters (all but `tiles` unless
-// full), the dequeue shards and the per-row outputs / counts
+// One lane per row.  Block 0 / lane 0 also publishes the detect's totals:
+// cnt->conf / los, the accumulated statistics and the gate words
+// (gate[0] = overflow, gate[1] = P) the resident sim step reads.
+__global__ __launch_bounds__(256) void k_rowsort(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
+                                                 const unsigned *__restrict__ rowoff,
+                                                 unsigned long long *__restrict__ skey,
+                                                 unsigned *__restrict__ sslot,
+                                                 const double *__restrict__ cpay,
+                                                 unsigned long long *__restrict__ lkey, int *__restrict__ ci,
+                                                 int *__restrict__ cj, double *__restrict__ out,
+                                                 int *__restrict__ li, int *__restrict__ lj,
+                                                 unsigned long long *__restrict__ stats,
+                                                 unsigned long long *__restrict__ gate) {
+  const bool ovf = cand_overflow(cnt, cap);
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned P = rowoff[nrows], L = rowoff[2 * nrows + 1] - P;
+  if (r == 0) {
+    unsigned long long pre[kCandShards + 1];
+    const unsigned long long ncand = cand_prefix(cnt, cap, pre);
+    cnt->conf = ovf ? 0 : P;
+    cnt->los = ovf ? 0 : L;
+    cnt->cand = ncand;
+    stats[0] += cnt->groups;
+    stats[1] += ncand;
+    stats[2] += cnt->tiles;
+    stats[3] += 1;
+    if (gate) {
+      gate[0] = ovf ? 1 : 0;
+      gate[1] = ovf ? 0 : P;
+    }
+  }
+  if (ovf || r >= nrows) return;
+  rank_segment(rowoff[r], rowoff[r + 1], skey, sslot, [&](unsigned x, unsigned pos) {
+    const unsigned long long kk = skey[x];
+    const unsigned v = sslot[x];
+    ci[pos] = (int)(kk >> 32);
+    cj[pos] = (int)(kk & 0xffffffffull);
+#pragma unroll
+    for (int f = 0; f < 5; ++f) out[(size_t)f * P + pos] = cpay[f * cap + v];
+  });
+  rank_segment(rowoff[nrows + 1 + r] - P, rowoff[nrows + 2 + r] - P, lkey, nullptr,
+               [&](unsigned x, unsigned pos) {
+                 const unsigned long long kk = lkey[x];
+                 li[pos] = (int)(kk >> 32);
+                 lj[pos] = (int)(kk & 0xffffffffull);
+               });
+}
+
+// Zero the per-detect state: counters (but `tiles` unless full), the dequeue
+// shards and the per-row outputs / counts.  Grid-stride, one word per lane.
 __global__ __launch_bounds__(256) void k_zero(int nrows, int full, Counters *__restrict__ cnt,
                                               unsigned long long *__restrict__ work,
                                               unsigned char *__restrict__ inconf,
                                               unsigned long long *__restrict__ tcpamax,
                                               unsigned *__restrict__ rowcnt) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k == 0) {
-    const unsigned long long tiles = cnt->tiles;
-    *cnt = Counters{};
-    if (!full) cnt->tiles = tiles;
+  constexpr int kWords = (int)(sizeof(Counters) / 8);
+  constexpr int kTilesWord = (int)(offsetof(Counters, tiles) / 8);
+  const int m = max(max(2 * (nrows + 1), kWorkShards * kWorkStride), kWords);
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
+    if (k < kWords && (full || k != kTilesWord)) reinterpret_cast<unsigned long long *>(cnt)[k] = 0;
+    if (k < kWorkShards * kWorkStride) work[k] = 0;
+    if (k < nrows) {
+      inconf[k] = 0;
+      tcpamax[k] = 0;
+    }
+    if (k < 2 * (nrows + 1)) rowcnt[k] = 0;
   }
-  if (k < kWorkShards * kWorkStride) work[k] = 0;
-  if (k < nrows) {
-    inconf[k] = 0;
-    tcpamax[k] = 0;
-  }
-  if (k < 2 * (nrows + 1)) rowcnt[k] = 0;
 }
 
 // ------------------------------------------------------------------ host side
 static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
-
 
 // spatial sort of cnt positions starting at original index base -> perm
 static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const double *lon,
@@ -1007,9 +1086,25 @@ static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const dou
   return 0;
 }
 
+// event set of this detect (the pool keeps one set per detect since the last
+// bsa_timing_reset, up to kEvSets; later detects reuse the last set)
+static int next_events(Ctx *c, hipEvent_t **ev) {
+  const int k = std::min(c->ev_sets, kEvSets - 1);
+  if ((int)c->evpool.size() < 5 * (k + 1)) {
+    const size_t old = c->evpool.size();
+    c->evpool.resize(5 * (size_t)(k + 1), nullptr);
+    for (size_t q = old; q < c->evpool.size(); ++q) BSA_HIP(c, hipEventCreate(&c->evpool[q]));
+  }
+  *ev = &c->evpool[5 * (size_t)k];
+  c->ev_last = k;
+  if (c->ev_sets < kEvSets) c->ev_sets++;
+  return 0;
+}
 
-int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
-           int64_t *n_conf, int64_t *n_los) {
+// Enqueue one complete detect on the stream (K0-K2), no host synchronisation.
+// gate (device, nullable): receives {overflow, P} for the resident sim step.
+int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
+                   unsigned long long *gate) {
   const int64_t n = c->n;
   if (re <= 0) re = n;
   if (rb < 0 || rb > re || re > n)
@@ -1022,31 +1117,33 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   c->last_flags = flags;
   c->last_conf = c->last_los = c->last_cand = 0;
   if (!ensure(c, c->counters, sizeof(Counters), "counters") ||
+      !ensure(c, c->stats, 8 * 8, "detect statistics") ||
       !ensure(c, c->inconf, (size_t)(nrows > 0 ? nrows : 1), "inconf") ||
       !ensure(c, c->tcpamax, (size_t)(nrows > 0 ? nrows : 1) * 8, "tcpamax") ||
       !ensure(c, c->workq, kWorkShards * kWorkStride * 8, "work counters") ||
       !ensure(c, c->rowcnt, (size_t)(2 * (nrows + 1)) * 4, "row counts") ||
       !ensure(c, c->rowoff, (size_t)(2 * (nrows + 1)) * 4, "row offsets"))
     return -1;
-  BSA_HIP(c, hipEventRecord(c->ev[0], c->stream));
+  hipEvent_t *ev = nullptr;
+  if (next_events(c, &ev)) return -1;
+  BSA_HIP(c, hipEventRecord(ev[0], c->stream));
   Counters *dcnt = (Counters *)c->counters.p;
-  auto zero = [&](int full) -> int {
-    const int64_t m = std::max<int64_t>(2 * (nrows + 1), kWorkShards * kWorkStride);
-    hipLaunchKernelGGL(k_zero, dim3(blocks_for(m, 256)), dim3(256), 0, c->stream, (int)nrows, full, dcnt,
-                       (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
-                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p);
+  {
+    const int64_t m = std::max<int64_t>(2 * (nrows + 1), 256);
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>(blocks_for(m, 256), 1024)), dim3(256), 0,
+                       c->stream, (int)nrows, 1, dcnt, (unsigned long long *)c->workq.p,
+                       (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
+                       (unsigned *)c->rowcnt.p);
     BSA_HIP(c, hipGetLastError());
-    return 0;
-  };
-  if (zero(1)) return -1;
+  }
   if (n == 0 || nrows == 0) {
-    for (int e = 1; e < 5; ++e) BSA_HIP(c, hipEventRecord(c->ev[e], c->stream));
-    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
+    for (int e = 1; e < 5; ++e) BSA_HIP(c, hipEventRecord(ev[e], c->stream));
     c->ev_valid = true;
-    c->have_pairs = true;
-    *n_conf = *n_los = 0;
+    c->empty_detect = true;
     return 0;
   }
+  c->empty_detect = false;
   const int noprune = (flags & BSA_FLAG_NOPRUNE) ? 1 : 0;
   const bool distinct = c->has_intruder;
   DevBuf *I = distinct ? c->intr : c->own;
@@ -1058,8 +1155,8 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   // ---- K0a spatial order.  Any permutation gives identical results (the
   // output is re-sorted canonically), so the order is reused for up to
   // kResortEvery calls on the same shape: aircraft move ~km between calls,
-  // tiles span ~100 km.  Rows share the column order when own == intruder
-  // and the whole range is detected.
+  // tiles span ~100 km.  Rows share the column order (and the records) when
+  // own == intruder and the whole range is detected.
   const bool shared = !distinct && rb == 0 && re == n;
   const bool resort = !c->perm_valid || c->perm_n != n || c->perm_rb != rb || c->perm_re != re ||
                       c->perm_shared != shared || c->perm_distinct != distinct ||
@@ -1081,148 +1178,166 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
   const unsigned *perm_r = (const unsigned *)(shared ? c->perm_c.p : c->perm_r.p);
   const unsigned *perm_c = (const unsigned *)c->perm_c.p;
 
-  // ---- K0b records in sorted order
-  if (!ensure(c, c->rowrec, nrows * sizeof(RowRec), "row records") ||
-      !ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
-      !ensure(c, c->pfrow, nrows * sizeof(PFRec), "prefilter rows") ||
+  // ---- K0b records in sorted order (shared: the column records serve as
+  // row records too; RowRec and ColRec agree field for field up to `vs`)
+  if (!ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
       !ensure(c, c->pfcol, n * sizeof(PFRec), "prefilter columns") ||
-      !ensure(c, c->pfvrow, nrows * sizeof(PFVel), "prefilter row velocities") ||
       !ensure(c, c->pfvcol, n * sizeof(PFVel), "prefilter column velocities"))
     return -1;
-  hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, perm_r,
-                     own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p, (PFRec *)c->pfrow.p,
-                     (PFVel *)c->pfvrow.p);
-  BSA_HIP(c, hipGetLastError());
+  if (!shared && (!ensure(c, c->rowrec, nrows * sizeof(RowRec), "row records") ||
+                  !ensure(c, c->pfrow, nrows * sizeof(PFRec), "prefilter rows") ||
+                  !ensure(c, c->pfvrow, nrows * sizeof(PFVel), "prefilter row velocities")))
+    return -1;
+  const RowRec *rowrec = shared ? (const RowRec *)c->colrec.p : (const RowRec *)c->rowrec.p;
+  const PFRec *pfrow = shared ? (const PFRec *)c->pfcol.p : (const PFRec *)c->pfrow.p;
+  const PFVel *pfvrow = shared ? (const PFVel *)c->pfvcol.p : (const PFVel *)c->pfvrow.p;
+  if (!shared) {
+    hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows,
+                       perm_r, own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p, (PFRec *)c->pfrow.p,
+                       (PFVel *)c->pfvrow.p);
+    BSA_HIP(c, hipGetLastError());
+  }
   hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n, perm_c, own,
-                     intr, distinct ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p, (PFRec *)c->pfcol.p,
-                     (PFVel *)c->pfvcol.p);
+                     intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
+                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p);
   BSA_HIP(c, hipGetLastError());
   // ---- K0c/K0d group / tile boxes and the tile-pair work list
   const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
   const long long ntp = (long long)nrt * nct;
   const int ngr = (int)((nrows + kGroup - 1) / kGroup), ngc = (int)((n + kGroup - 1) / kGroup);
-  if (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
-      !ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
-      !ensure(c, c->gbox_r, ngr * sizeof(TileBox), "row group boxes") ||
+  if (!ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
       !ensure(c, c->gbox_c, ngc * sizeof(TileBox), "column group boxes") ||
       !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
     return -1;
-  hipLaunchKernelGGL(k_groupbox, dim3(blocks_for(ngr, 4)), dim3(256), 0, c->stream, (int)nrows,
-                     (const PFRec *)c->pfrow.p, (TileBox *)c->gbox_r.p);
-  hipLaunchKernelGGL(k_groupbox, dim3(blocks_for(ngc, 4)), dim3(256), 0, c->stream, (int)n,
-                     (const PFRec *)c->pfcol.p, (TileBox *)c->gbox_c.p);
-  hipLaunchKernelGGL(k_tileunion, dim3(blocks_for(nrt, 256)), dim3(256), 0, c->stream, nrt, ngr,
-                     (const TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p);
-  hipLaunchKernelGGL(k_tileunion, dim3(blocks_for(nct, 256)), dim3(256), 0, c->stream, nct, ngc,
-                     (const TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p);
+  if (!shared && (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
+                  !ensure(c, c->gbox_r, ngr * sizeof(TileBox), "row group boxes")))
+    return -1;
+  const TileBox *gbox_r = shared ? (const TileBox *)c->gbox_c.p : (const TileBox *)c->gbox_r.p;
+  const TileBox *tbox_r = shared ? (const TileBox *)c->tbox_c.p : (const TileBox *)c->tbox_r.p;
+  if (!shared)
+    hipLaunchKernelGGL(k_boxes, dim3(nrt), dim3(kTile), 0, c->stream, (int)nrows, pfrow,
+                       (TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p);
+  hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
+                     (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p);
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + 255) / 256)), dim3(256), 0, c->stream, nrt, nct,
-                     (const TileBox *)c->tbox_r.p, (const TileBox *)c->tbox_c.p, noprune,
-                     (uint2 *)c->tilepairs.p, &dcnt->tiles);
+                     tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p, &dcnt->tiles);
   BSA_HIP(c, hipGetLastError());
-  BSA_HIP(c, hipEventRecord(c->ev[1], c->stream));
+  BSA_HIP(c, hipEventRecord(ev[1], c->stream));
 
-  if (c->cand_cap == 0) c->cand_cap = (unsigned long long)std::max<int64_t>(1 << 20, 16 * nrows);
+  // ---- buffers sized by the candidate capacity (every pair list <= candidates)
+  if (c->cand_cap == 0)
+    c->cand_cap = (unsigned long long)kCandShards * (unsigned long long)std::max<int64_t>(1 << 17, 4 * nrows);
+  const unsigned long long cap = c->cand_cap;
+  if (!ensure(c, c->cand, cap * sizeof(uint2), "candidate pairs") ||
+      !ensure(c, c->cflag, cap, "candidate flags") || !ensure(c, c->ckey, cap * 8, "candidate keys") ||
+      !ensure(c, c->cpay, cap * 5 * 8, "candidate payload") ||
+      !ensure(c, c->ckey2, cap * 8, "conflict keys") || !ensure(c, c->cval2, cap * 4, "conflict slots") ||
+      !ensure(c, c->lkey2, cap * 8, "los keys") || !ensure(c, c->out_ci, cap * 4, "ci") ||
+      !ensure(c, c->out_cj, cap * 4, "cj") || !ensure(c, c->out_pay, cap * 5 * 8, "conflict outputs") ||
+      !ensure(c, c->out_li, cap * 4, "li") || !ensure(c, c->out_lj, cap * 4, "lj"))
+    return -1;
   const float T = (float)(tla > 0.0 ? tla : 0.0);
   const float lim = (float)((rpz + kEABS) / (1.0 - kE1));
   const RefineParams rp{(float)rpz, (float)hpz, T, lim * lim};
+  // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
+  // (LDS-limited residency), at least one workgroup per dequeue shard
+  const unsigned pf_grid = (unsigned)std::max<long long>(
+      kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * PF_BLOCKS_PER_CU));
+  if (noprune)
+    hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
+                       (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
+                       (const TileBox *)c->gbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap);
+  else
+    hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
+                       (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
+                       (const TileBox *)c->gbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap);
+  BSA_HIP(c, hipGetLastError());
+  BSA_HIP(c, hipEventRecord(ev[2], c->stream));
+  // ---- K1b exact evaluation: grid-stride over the device-side count, one
+  // resident round (4 workgroups per CU at its register budget)
+  hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
+                     perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, cap, rpz, hpz, tla, (int)rb, (int)nrows,
+                     (unsigned char *)c->cflag.p, (unsigned long long *)c->ckey.p, (double *)c->cpay.p,
+                     (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
+                     (unsigned *)c->rowcnt.p);
+  BSA_HIP(c, hipGetLastError());
+  BSA_HIP(c, hipEventRecord(ev[3], c->stream));
+  // ---- K2: row offsets, scatter into row segments, per-row rank + gather
   const int nscan = (int)(2 * (nrows + 1));
   size_t scan_tmp = 0;
   BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const unsigned *)c->rowcnt.p,
                                               (unsigned *)c->rowoff.p, nscan, c->stream));
   if (!ensure(c, c->sort_tmp, std::max<size_t>(scan_tmp, 16), "scan scratch")) return -1;
+  scan_tmp = c->sort_tmp.bytes;
+  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, scan_tmp, (const unsigned *)c->rowcnt.p,
+                                              (unsigned *)c->rowoff.p, nscan, c->stream));
+  hipLaunchKernelGGL(k_scatter, dim3(256 * 4), dim3(256), 0, c->stream, (const Counters *)dcnt, cap, (int)rb,
+                     (int)nrows, (const unsigned char *)c->cflag.p, (const unsigned long long *)c->ckey.p,
+                     (const unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
+                     (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
+                     (unsigned long long *)c->lkey2.p);
+  BSA_HIP(c, hipGetLastError());
+  hipLaunchKernelGGL(k_rowsort, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
+                     (const unsigned *)c->rowoff.p, (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
+                     (const double *)c->cpay.p, (unsigned long long *)c->lkey2.p, (int *)c->out_ci.p,
+                     (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
+                     (unsigned long long *)c->stats.p, gate);
+  BSA_HIP(c, hipGetLastError());
+  BSA_HIP(c, hipEventRecord(ev[4], c->stream));
+  c->ev_valid = true;
+  return 0;
+}
+
+// Wait for the enqueued detect and read its totals.  *retry is set (and the
+// candidate capacity grown) when the candidate list overflowed.
+int detect_finish(Ctx *c, bool *retry) {
+  *retry = false;
   Counters h;
-  unsigned tot[2] = {0, 0};  // P and P + L from the scan
-  for (int attempt = 0;; ++attempt) {
-    const unsigned long long cap = c->cand_cap;
-    if (!ensure(c, c->cand, cap * sizeof(uint2), "candidate pairs") ||
-        !ensure(c, c->cflag, cap, "candidate flags") ||
-        !ensure(c, c->ckey, cap * 8, "candidate keys") ||
-        !ensure(c, c->cpay, cap * 5 * 8, "candidate payload"))
-      return -1;
-    if (attempt > 0 && zero(0)) return -1;
-    // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
-    // (LDS-limited residency), at least one workgroup per dequeue shard
-    const unsigned pf_grid = (unsigned)std::max<long long>(
-        kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * PF_BLOCKS_PER_CU));
-    if (noprune)
-      hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
-                         (const PFRec *)c->pfrow.p, (const PFVel *)c->pfvrow.p, (int)nrows,
-                         (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n,
-                         (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
-                         (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
-                         (uint2 *)c->cand.p, cap);
-    else
-      hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream,
-                         (const PFRec *)c->pfrow.p, (const PFVel *)c->pfvrow.p, (int)nrows,
-                         (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n,
-                         (const TileBox *)c->gbox_r.p, (const TileBox *)c->gbox_c.p,
-                         (const uint2 *)c->tilepairs.p, dcnt, (unsigned long long *)c->workq.p, rp,
-                         (uint2 *)c->cand.p, cap);
-    BSA_HIP(c, hipGetLastError());
-    BSA_HIP(c, hipEventRecord(c->ev[2], c->stream));
-    // ---- K1b exact evaluation: grid-stride over the device-side count, one
-    // resident round (4 workgroups per CU at its register budget)
-    hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, (const RowRec *)c->rowrec.p,
-                       (const ColRec *)c->colrec.p, perm_r, perm_c, (const uint2 *)c->cand.p, &dcnt->cand,
-                       cap, rpz, hpz, tla, (int)rb, (int)nrows, (unsigned char *)c->cflag.p,
-                       (unsigned long long *)c->ckey.p, (double *)c->cpay.p, (unsigned char *)c->inconf.p,
-                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p);
-    BSA_HIP(c, hipGetLastError());
-    // ---- K2 part 1: row offsets (exclusive scan of [conf per row | 0 | LoS per row | 0])
-    size_t tmp = c->sort_tmp.bytes;
-    BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, tmp, (const unsigned *)c->rowcnt.p,
-                                                (unsigned *)c->rowoff.p, nscan, c->stream));
-    BSA_HIP(c, hipEventRecord(c->ev[3], c->stream));
-    // the detect's only host sync: candidate count + totals P and P + L
-    BSA_HIP(c, hipMemcpyAsync(&h, c->counters.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    BSA_HIP(c, hipMemcpyAsync(&tot[0], (const unsigned *)c->rowoff.p + nrows, 4, hipMemcpyDeviceToHost,
-                              c->stream));
-    BSA_HIP(c, hipMemcpyAsync(&tot[1], (const unsigned *)c->rowoff.p + nscan - 1, 4,
-                              hipMemcpyDeviceToHost, c->stream));
-    BSA_HIP(c, hipStreamSynchronize(c->stream));
-    if (h.cand <= cap) break;
-    if (attempt > 3) return fail(c, "candidate buffer overflow (%llu)", h.cand);
-    c->cand_cap = h.cand + h.cand / 4 + 1024;
+  BSA_HIP(c, hipMemcpyAsync(&h, c->counters.p, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  if (c->empty_detect) {
+    c->last_conf = c->last_los = c->last_cand = c->last_tiles = c->last_groups = 0;
+    c->have_pairs = true;
+    return 0;
   }
+  unsigned long long worst = 0, total = 0;
+  for (int q = 0; q < kCandShards; ++q) {
+    worst = std::max(worst, h.cshard[q][0]);
+    total += h.cshard[q][0];
+  }
+  if (worst > c->cand_cap / kCandShards) {
+    c->cand_cap = (unsigned long long)kCandShards * (worst + worst / 4 + 1024);
+    *retry = true;
+    return 0;
+  }
+  const int64_t nrows = c->last_re - c->last_rb;
+  c->last_cand = (int64_t)total;
+  c->last_tiles = (int64_t)h.tiles;
+  c->last_tiles_total = (int64_t)(((nrows + kTile - 1) / kTile) * ((c->n + kTile - 1) / kTile));
+  c->last_groups = (int64_t)h.groups;
+  c->last_conf = (int64_t)h.conf;
+  c->last_los = (int64_t)h.los;
+  c->have_pairs = true;
 #ifdef BSA_PF_STAMPS
   fprintf(stderr, "[bsa stamps] prefilter wave-cycles: setup %.4g stage1 %.4g drain %.4g flush %.4g\n",
           (double)h.stamp[0], (double)h.stamp[1], (double)h.stamp[2], (double)h.stamp[3]);
 #endif
-  c->last_cand = (int64_t)h.cand;
-  c->last_tiles = (int64_t)h.tiles;
-  c->last_tiles_total = ntp;
-  c->last_groups = (int64_t)h.groups;
+  return 0;
+}
 
-  // ---- K2 part 2: scatter into row segments, per-row insertion sort + gather
-  const int64_t P = (int64_t)tot[0], L = (int64_t)tot[1] - (int64_t)tot[0];
-  if (!ensure(c, c->cval2, (size_t)std::max<int64_t>(P, 1) * 4, "conflict slots") ||
-      !ensure(c, c->lslot, (size_t)std::max<int64_t>(L, 1) * 4, "los slots") ||
-      !ensure(c, c->out_ci, (size_t)std::max<int64_t>(P, 1) * 4, "ci") ||
-      !ensure(c, c->out_cj, (size_t)std::max<int64_t>(P, 1) * 4, "cj") ||
-      !ensure(c, c->out_pay, (size_t)std::max<int64_t>(P, 1) * 5 * 8, "conflict outputs") ||
-      !ensure(c, c->out_li, (size_t)std::max<int64_t>(L, 1) * 4, "li") ||
-      !ensure(c, c->out_lj, (size_t)std::max<int64_t>(L, 1) * 4, "lj"))
-    return -1;
-  if (P + L > 0) {
-    hipLaunchKernelGGL(k_scatter, dim3(256 * 4), dim3(256), 0, c->stream, &dcnt->cand, c->cand_cap,
-                       (int)rb, (int)nrows, (const unsigned char *)c->cflag.p,
-                       (const unsigned long long *)c->ckey.p, (const unsigned *)c->rowoff.p,
-                       (unsigned *)c->rowcnt.p, (unsigned *)c->cval2.p, (unsigned *)c->lslot.p);
-    BSA_HIP(c, hipGetLastError());
-    hipLaunchKernelGGL(k_rowsort, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, P,
-                       (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey.p,
-                       (unsigned *)c->cval2.p, (const double *)c->cpay.p, c->cand_cap,
-                       (unsigned *)c->lslot.p, (int *)c->out_ci.p, (int *)c->out_cj.p,
-                       (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p);
-    BSA_HIP(c, hipGetLastError());
+int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
+           int64_t *n_conf, int64_t *n_los) {
+  for (int attempt = 0;; ++attempt) {
+    if (detect_enqueue(c, rpz, hpz, tla, flags, rb, re, nullptr)) return -1;
+    bool retry = false;
+    if (detect_finish(c, &retry)) return -1;
+    if (!retry) break;
+    if (attempt >= 4) return fail(c, "candidate buffer overflow after %d retries", attempt + 1);
   }
-  BSA_HIP(c, hipEventRecord(c->ev[4], c->stream));
-  c->ev_valid = true;
-  c->last_conf = P;
-  c->last_los = L;
-  c->have_pairs = true;
-  *n_conf = P;
-  *n_los = L;
+  *n_conf = c->last_conf;
+  *n_los = c->last_los;
   return 0;
 }
 

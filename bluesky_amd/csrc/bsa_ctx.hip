@@ -107,14 +107,6 @@ bsa_ctx *bsa_create(int device) {
     delete c;
     return nullptr;
   }
-  for (int k = 0; k < 5; ++k) {
-    e = hipEventCreate(&c->ev[k]);
-    if (e != hipSuccess) {
-      bsa::fail(nullptr, "hipEventCreate: %s", hipGetErrorString(e));
-      delete c;
-      return nullptr;
-    }
-  }
   return c;
 }
 
@@ -125,11 +117,11 @@ void bsa_destroy(bsa_ctx *c) {
   bsa::DevBuf *all[] = {&c->rowrec, &c->colrec, &c->pfrow, &c->pfcol, &c->counters, &c->cand,
                         &c->ckey, &c->cval, &c->ckey2, &c->cval2, &c->cpay, &c->lkey, &c->lkey2,
                         &c->out_ci, &c->out_cj, &c->out_li, &c->out_lj, &c->out_pay, &c->inconf,
-                        &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage,
+                        &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage, &c->mvp_pdv, &c->mvp_pfl,
                         &c->pfvrow, &c->pfvcol, &c->key_r, &c->idx_r, &c->key_r2, &c->perm_r,
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
                         &c->gbox_r, &c->gbox_c, &c->workq, &c->rowcnt, &c->rowoff, &c->lslot,
-                        &c->cflag,
+                        &c->cflag, &c->stats,
                         &c->tilepairs};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);
@@ -137,8 +129,8 @@ void bsa_destroy(bsa_ctx *c) {
     bsa::release(c->own[k]);
     bsa::release(c->intr[k]);
   }
-  for (int k = 0; k < 5; ++k)
-    if (c->ev[k]) (void)hipEventDestroy(c->ev[k]);
+  for (hipEvent_t e : c->evpool)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -237,17 +229,54 @@ int bsa_last_tiles(bsa_ctx *c, int64_t *kept, int64_t *total, int64_t *groups) {
   return 0;
 }
 
+// stage durations [ms] of one recorded detect: K0 (zero, order, records,
+// boxes, tile pairs), K1a prefilter, K1b exact, K2 (scan, scatter, rank), total
+static int event_set_ms(bsa::Ctx *c, int set, double *ms5) {
+  hipEvent_t *ev = &c->evpool[5 * (size_t)set];
+  BSA_HIP(c, hipEventSynchronize(ev[4]));
+  float t;
+  for (int k = 0; k < 4; ++k) {
+    BSA_HIP(c, hipEventElapsedTime(&t, ev[k], ev[k + 1]));
+    ms5[k] = t;
+  }
+  BSA_HIP(c, hipEventElapsedTime(&t, ev[0], ev[4]));
+  ms5[4] = t;
+  return 0;
+}
+
 int bsa_last_timings(bsa_ctx *c, double *ms5) {
   if (!c || !ms5) return -1;
   if (!c->ev_valid) return bsa::fail(c, "no timed detect yet");
-  BSA_HIP(c, hipEventSynchronize(c->ev[4]));
-  float t;
-  for (int k = 0; k < 4; ++k) {
-    BSA_HIP(c, hipEventElapsedTime(&t, c->ev[k], c->ev[k + 1]));
-    ms5[k] = t;
+  BSA_HIP(c, hipSetDevice(c->device));
+  return event_set_ms(c, c->ev_last, ms5);
+}
+
+int bsa_timing_reset(bsa_ctx *c) {
+  if (!c) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  c->ev_sets = 0;
+  c->ev_valid = false;
+  if (!bsa::ensure(c, c->stats, 8 * 8, "detect statistics")) return -1;
+  BSA_HIP(c, hipMemsetAsync(c->stats.p, 0, 8 * 8, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int bsa_timing_summary(bsa_ctx *c, double *ms5, int64_t *stats4) {
+  if (!c || !ms5 || !stats4) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < 5; ++k) ms5[k] = 0.0;
+  const int sets = std::min(c->ev_sets, bsa::kEvSets);
+  for (int q = 0; q < sets; ++q) {
+    double m[5];
+    if (event_set_ms(c, q, m)) return -1;
+    for (int k = 0; k < 5; ++k) ms5[k] += m[k] / sets;
   }
-  BSA_HIP(c, hipEventElapsedTime(&t, c->ev[0], c->ev[4]));
-  ms5[4] = t;
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c->stats.p) BSA_HIP(c, hipMemcpy(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 4; ++k) stats4[k] = (int64_t)st[k];
   return 0;
 }
 

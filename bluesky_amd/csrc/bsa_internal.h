@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/bsaccel.h"
 
@@ -84,10 +85,13 @@ static_assert(sizeof(TileBox) == 48, "TileBox must be 48 B");
 
 constexpr int kTile = 512;  // rows per row block == columns per column tile
 constexpr int kResortEvery = 8;  // detect calls between spatial re-sorts
+constexpr int kEvSets = 4096;    // detect timing event sets kept between resets
 
-// counters block on the device (one cache line)
+constexpr int kCandShards = 8;  // candidate list shards (one counter each, 128 B apart)
+
+// counters block on the device
 struct Counters {
-  unsigned long long cand;
+  unsigned long long cand;    // host-side total (sum of the shard counts)
   unsigned long long conf;
   unsigned long long los;
   unsigned long long tiles;
@@ -95,6 +99,7 @@ struct Counters {
   unsigned long long pad[3];
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];
+  unsigned long long cshard[kCandShards][16];  // candidates per shard (word 0 of each line)
 };
 
 // ---------------------------------------------------------------- buffers
@@ -148,11 +153,15 @@ struct Ctx {
   int last_flags = 0;
   bool have_pairs = false;
 
-  hipEvent_t ev[5] = {};
+  // detect timing: one set of 5 events per detect since the last reset
+  std::vector<hipEvent_t> evpool;
+  int ev_sets = 0, ev_last = 0;
   bool ev_valid = false;
+  bool empty_detect = false;
+  DevBuf stats;  // accumulated per-detect statistics {groups, candidates, tiles, detects}
 
   // MVP / kinematics staging (host-buffer entry points)
-  DevBuf seg, mvp_stage, kin_stage;
+  DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl;
 
   // multi-GPU (RCCL); comm is an ncclComm_t
   void *comm = nullptr;
@@ -169,6 +178,7 @@ struct Ctx {
   DevBuf s_aptrk, s_aptas, s_apalt, s_apvs, s_selalt, s_bank, s_eps, s_accel;  // frozen
   DevBuf s_atrk, s_atas, s_avs, s_aalt, s_ase, s_asn, s_active;  // ASAS (full n)
   DevBuf g_send, g_recv;                                    // all-gather staging
+  DevBuf sim_ctl;  // [0,16) gate {overflow, P}; [16,20) sticky abort; [24,32) steps done
 };
 
 // device pointers for the MVP kernel (full-N traffic arrays, per-row outputs)
@@ -179,7 +189,9 @@ struct MvpDev {
   float *o_asase, *o_asasn;
   double *o_tsolv;
 };
-int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d);
+int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned *seg,
+               const unsigned long long *gate, unsigned *sticky, const uint8_t *inconf, uint8_t *active,
+               bool resolve);
 
 // device pointers for the fused kinematics kernel
 struct KinDev {
@@ -203,8 +215,11 @@ int fail(Ctx *c, const char *fmt, ...);
 // sim / comm teardown (bsa_sim.hip)
 void sim_release(Ctx *c);
 
-// detect entry (bsa_cd.hip)
+// detect entry points (bsa_cd.hip): detect = enqueue + finish (+ retries)
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
            int64_t *n_conf, int64_t *n_los);
+int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
+                   unsigned long long *gate);
+int detect_finish(Ctx *c, bool *retry);
 
 }  // namespace bsa

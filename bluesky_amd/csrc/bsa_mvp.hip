@@ -4,10 +4,11 @@
 // bluesky/traffic/asas/MVP.py:14-143 loops over confpairs and only ever
 // writes dv[id1] (MVP.py:46-61; prioRules' dv2 is discarded), and confpairs
 // are in row-major order, so each ownship's dv is a sequential fold over its
-// own contiguous segment of pairs in j order.  One lane per ownship walks its
-// segment in that order, which reproduces the reference's summation order
-// exactly (no tree reduction); then the same lane runs the per-aircraft
-// finalize (MVP.py:67-143).
+// own contiguous segment of pairs in j order.  Each pair's MVP vector does
+// not depend on the fold, so k_mvp_pair computes them all in parallel (one
+// lane per pair); k_mvp_row then folds each ownship's segment in order, which
+// reproduces the reference's summation order exactly (no tree reduction),
+// and runs the per-aircraft finalize (MVP.py:67-143).
 #include "bsa_internal.h"
 
 #pragma clang fp contract(off)
@@ -31,10 +32,12 @@ __device__ __forceinline__ double np_rem(double a, double b) {
   return mod;
 }
 
-// segment start of each row: first k with ci[k] >= rb + r  (ci sorted)
+// segment start of each row: first k with ci[k] >= rb + r  (ci sorted);
+// seg[nrows] = P.  Used when the pairs came from the host (bsa_set_pairs);
+// a device detect hands its K2 row offsets over directly.
 __global__ __launch_bounds__(256) void k_segments(int nrows, int rb, int64_t P,
                                                   const int *__restrict__ ci,
-                                                  int64_t *__restrict__ seg) {
+                                                  unsigned *__restrict__ seg) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r > nrows) return;
   const int key = rb + r;
@@ -43,13 +46,13 @@ __global__ __launch_bounds__(256) void k_segments(int nrows, int rb, int64_t P,
     const int64_t mid = (lo + hi) >> 1;
     if (ci[mid] < key) lo = mid + 1; else hi = mid;
   }
-  seg[r] = lo;
+  seg[r] = (unsigned)lo;
 }
 
 struct MvpIn {
-  const int *cj;
-  const double *qdr, *dist, *tcpa, *tlos;  // sorted pair payload
-  const int64_t *seg;
+  const int *ci, *cj;
+  const double *pay;                 // sorted pair payload, 5 x P (qdr dist tcpa tlos dcpa)
+  const unsigned *seg;               // row segments, nrows + 1 entries; seg[nrows] = P
   const double *gseast, *gsnorth, *vs, *alt, *trk, *gs;  // full-N traffic arrays
   const double *selalt, *apvs;                           // full-N
   const uint8_t *noreso, *resooff;                       // full-N flags or NULL
@@ -57,21 +60,37 @@ struct MvpIn {
   double *o_trk, *o_tas, *o_vs;                          // rows [rb, re)
   float *o_asase, *o_asasn;
   double *o_tsolv;                                       // optional (may be NULL)
+  double4 *pdv;                                          // per pair: dv1 dv2 dv3 tsolV
+  uint8_t *pfl;                                          // per pair: bit0 subtract, bit1 add back
+  // resident sim step only (else NULL): gate = {overflow, P (max over ranks)},
+  // sticky = abort flag of the whole step batch, inconf -> active copy
+  const unsigned long long *gate;
+  unsigned *sticky;
+  const uint8_t *inconf;
+  uint8_t *active;
+  int nrows;
+  int resolve;                                           // 0: only the active copy
 };
 
-__global__ __launch_bounds__(256) void k_mvp(int nrows, int rb, bsa_mvp_params p, MvpIn in) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrows) return;
-  const int id1 = rb + r;
-  const double gse1 = in.gseast[id1], gsn1 = in.gsnorth[id1], vs1 = in.vs[id1], alt1 = in.alt[id1];
-  double dvx = 0.0, dvy = 0.0, dvz = 0.0;
-  double tsv = 1e9;  // np.ones(n) * 1e9
-  const bool resooff1 = p.swresooff && in.resooff && in.resooff[id1];
-  for (int64_t k = in.seg[r]; k < in.seg[r + 1]; ++k) {
-    const int id2 = in.cj[k];
-    const double dist = in.dist[k], tcpa = in.tcpa[k], tLOS = in.tlos[k];
+__device__ __forceinline__ bool mvp_aborted(const MvpIn &in) {
+  return in.gate && (in.sticky[0] != 0 || in.gate[0] != 0);
+}
+
+// Per pair (MVP.py:33-56): MVP.MVP (MVP.py:149-231) and the priority rules
+// (MVP.py:235-300; only the first return value is kept, MVP.py:46) for one
+// confpair.  Nothing here depends on the running dv sum, so the pairs are
+// independent; k_mvp_row applies the results in the reference's order.
+__global__ __launch_bounds__(256) void k_mvp_pair(int rb, bsa_mvp_params p, MvpIn in) {
+  if (mvp_aborted(in) || !in.resolve) return;
+  const unsigned P = in.seg[in.nrows];
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < P; k += stride) {
+    const int id1 = in.ci[k], id2 = in.cj[k];
+    const double gse1 = in.gseast[id1], gsn1 = in.gsnorth[id1], vs1 = in.vs[id1], alt1 = in.alt[id1];
+    const double dist = in.pay[(size_t)1 * P + k], tcpa = in.pay[(size_t)2 * P + k];
+    const double tLOS = in.pay[(size_t)3 * P + k];
     // ---- MVP.MVP (MVP.py:149-231)
-    const double qdr = in.qdr[k] * kD2R;
+    const double qdr = in.pay[k] * kD2R;
     const double drel0 = sin(qdr) * dist;
     const double drel1 = cos(qdr) * dist;
     const double drel2 = in.alt[id2] - alt1;
@@ -102,47 +121,68 @@ __global__ __launch_bounds__(256) void k_mvp(int nrows, int rb, bsa_mvp_params p
       iV = p.dhm;
     }
     double dv3 = vz ? (iV / tsolV) * (-vrel2 / fabs(vrel2)) : (iV / tsolV);
-    if (tsolV < tsv) tsv = tsolV;
-    // ---- accumulation (MVP.py:44-61)
+    // ---- accumulation rule (MVP.py:44-56): subtract? (then) add back?
+    bool sub = true;
     if (p.swprio) {
       const double vs2 = in.vs[id2];
       const bool c1 = fabs(vs1) < 0.1 && fabs(vs2) > 0.1;  // ac1 cruising, ac2 climbing
       const bool c2 = fabs(vs2) < 0.1 && fabs(vs1) > 0.1;  // ac2 cruising, ac1 climbing
       switch (p.priocode) {
-        case BSA_PRIO_FF1:
-          dv3 = dv3 / 2.0;
-          dvx = dvx - dv1; dvy = dvy - dv2; dvz = dvz - dv3;
-          break;
-        case BSA_PRIO_FF2:
-          dv3 = dv3 / 2.0;
-          if (!c1) { dvx = dvx - dv1; dvy = dvy - dv2; dvz = dvz - dv3; }
-          break;
+        case BSA_PRIO_FF1: dv3 = dv3 / 2.0; break;
+        case BSA_PRIO_FF2: dv3 = dv3 / 2.0; sub = !c1; break;
         case BSA_PRIO_FF3:
-          if (c1) { dv3 = 0.0; dvx = dvx - dv1; dvy = dvy - dv2; dvz = dvz - dv3; }
-          else if (c2) { dv3 = 0.0; }
-          else { dv3 = dv3 / 2.0; dvx = dvx - dv1; dvy = dvy - dv2; dvz = dvz - dv3; }
+          if (c1) dv3 = 0.0;
+          else if (c2) { dv3 = 0.0; sub = false; }
+          else dv3 = dv3 / 2.0;
           break;
-        case BSA_PRIO_LAY1:
-          dv3 = 0.0;
-          if (!c1) { dvx = dvx - dv1; dvy = dvy - dv2; dvz = dvz - dv3; }
-          break;
-        case BSA_PRIO_LAY2:
-          dv3 = 0.0;
-          if (!c2) { dvx = dvx - dv1; dvy = dvy - dv2; dvz = dvz - dv3; }
-          break;
-        default:
-          break;  // unknown code: prioRules changes nothing
+        case BSA_PRIO_LAY1: dv3 = 0.0; sub = !c1; break;
+        case BSA_PRIO_LAY2: dv3 = 0.0; sub = !c2; break;
+        default: sub = false; break;  // unknown code: prioRules changes nothing
       }
     } else {
       dv3 = 0.5 * dv3;
-      dvx = dvx - dv1;
-      dvy = dvy - dv2;
-      dvz = dvz - dv3;
     }
-    if (p.swnoreso && in.noreso && in.noreso[id2]) {
-      dvx = dvx + dv1;
-      dvy = dvy + dv2;
-      dvz = dvz + dv3;
+    const bool add = p.swnoreso && in.noreso && in.noreso[id2];
+    in.pdv[k] = make_double4(dv1, dv2, dv3, tsolV);
+    in.pfl[k] = (uint8_t)((sub ? 1 : 0) | (add ? 2 : 0));
+  }
+}
+
+// Per row: the dv fold over the row's pairs in confpair order (MVP.py:44-61),
+// then the per-aircraft finalize (MVP.py:67-143).  In the resident sim step
+// this kernel also gates the step (overflow -> sticky abort) and copies
+// asas.active = inconf.
+__global__ __launch_bounds__(256) void k_mvp_row(int rb, bsa_mvp_params p, MvpIn in) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (in.gate) {
+    const bool abort = in.sticky[0] != 0 || in.gate[0] != 0;
+    if (r == 0 && in.gate[0] != 0) in.sticky[0] = 1u;
+    if (abort || r >= in.nrows || !in.resolve) return;  // RESO off: asas stays inactive
+    in.active[rb + r] = in.inconf[r];  // build-defined stand-in for ResumeNav
+    // asas.py:486-487: resolve only if confpairs is non-empty (over all ranks)
+    if (in.gate[1] == 0) return;
+  } else if (r >= in.nrows) {
+    return;
+  }
+  const int id1 = rb + r;
+  const double gse1 = in.gseast[id1], gsn1 = in.gsnorth[id1], vs1 = in.vs[id1], alt1 = in.alt[id1];
+  double dvx = 0.0, dvy = 0.0, dvz = 0.0;
+  double tsv = 1e9;  // np.ones(n) * 1e9
+  const bool resooff1 = p.swresooff && in.resooff && in.resooff[id1];
+  const unsigned e = in.seg[r + 1];
+  for (unsigned k = in.seg[r]; k < e; ++k) {
+    const double4 d = in.pdv[k];
+    const uint8_t f = in.pfl[k];
+    if (d.w < tsv) tsv = d.w;
+    if (f & 1) {
+      dvx = dvx - d.x;
+      dvy = dvy - d.y;
+      dvz = dvz - d.z;
+    }
+    if (f & 2) {
+      dvx = dvx + d.x;
+      dvy = dvy + d.y;
+      dvz = dvz + d.z;
     }
     if (resooff1) dvx = dvy = dvz = 0.0;
   }
@@ -195,23 +235,30 @@ __global__ __launch_bounds__(256) void k_mvp(int nrows, int rb, bsa_mvp_params p
 }
 
 // Device-side MVP over the last detect's pairs; all pointers are device
-// pointers (full-N traffic arrays, per-row outputs).
-int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d) {
-  if (!c->have_pairs) return fail(c, "bsa_mvp: no detect results (call bsa_detect first)");
-  const int64_t rb = c->last_rb, re = c->last_re, nrows = re - rb, P = c->last_conf;
+// pointers (full-N traffic arrays, per-row outputs).  seg: the detect's K2
+// row offsets (device path) or NULL (pairs from the host: binary search).
+// gate / sticky / inconf / active: resident sim step only.
+int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned *seg,
+               const unsigned long long *gate, unsigned *sticky, const uint8_t *inconf, uint8_t *active,
+               bool resolve) {
+  const int64_t rb = c->last_rb, re = c->last_re, nrows = re - rb;
   if (nrows <= 0) return 0;
-  if (!ensure(c, c->seg, (size_t)(nrows + 1) * 8, "mvp segments")) return -1;
-  hipLaunchKernelGGL(k_segments, dim3((unsigned)((nrows + 1 + 255) / 256)), dim3(256), 0, c->stream,
-                     (int)nrows, (int)rb, P, (const int *)c->out_ci.p, (int64_t *)c->seg.p);
-  BSA_HIP(c, hipGetLastError());
-  const double *pay = (const double *)c->out_pay.p;
+  const unsigned long long pcap = std::max<unsigned long long>(c->cand_cap, (unsigned long long)c->last_conf);
+  if (!ensure(c, c->mvp_pdv, std::max<unsigned long long>(pcap, 1) * sizeof(double4), "mvp pair dv") ||
+      !ensure(c, c->mvp_pfl, std::max<unsigned long long>(pcap, 1), "mvp pair flags"))
+    return -1;
+  if (!seg) {
+    if (!ensure(c, c->seg, (size_t)(nrows + 1) * 4, "mvp segments")) return -1;
+    hipLaunchKernelGGL(k_segments, dim3((unsigned)((nrows + 1 + 255) / 256)), dim3(256), 0, c->stream,
+                       (int)nrows, (int)rb, c->last_conf, (const int *)c->out_ci.p, (unsigned *)c->seg.p);
+    BSA_HIP(c, hipGetLastError());
+    seg = (const unsigned *)c->seg.p;
+  }
   MvpIn in;
+  in.ci = (const int *)c->out_ci.p;
   in.cj = (const int *)c->out_cj.p;
-  in.qdr = pay + 0 * P;
-  in.dist = pay + 1 * P;
-  in.tcpa = pay + 2 * P;
-  in.tlos = pay + 3 * P;
-  in.seg = (const int64_t *)c->seg.p;
+  in.pay = (const double *)c->out_pay.p;
+  in.seg = seg;
   in.gseast = d.gseast;
   in.gsnorth = d.gsnorth;
   in.vs = d.vs;
@@ -229,8 +276,18 @@ int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d) {
   in.o_asase = d.o_asase;
   in.o_asasn = d.o_asasn;
   in.o_tsolv = d.o_tsolv;
-  hipLaunchKernelGGL(k_mvp, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, c->stream,
-                     (int)nrows, (int)rb, p, in);
+  in.pdv = (double4 *)c->mvp_pdv.p;
+  in.pfl = (uint8_t *)c->mvp_pfl.p;
+  in.gate = gate;
+  in.sticky = sticky;
+  in.inconf = inconf;
+  in.active = active;
+  in.nrows = (int)nrows;
+  in.resolve = resolve ? 1 : 0;
+  hipLaunchKernelGGL(k_mvp_pair, dim3(256 * 4), dim3(256), 0, c->stream, (int)rb, p, in);
+  BSA_HIP(c, hipGetLastError());
+  hipLaunchKernelGGL(k_mvp_row, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, c->stream, (int)rb, p,
+                     in);
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -291,7 +348,7 @@ extern "C" int bsa_mvp(bsa_ctx *cc, const bsa_mvp_params *p, const double *gseas
   d.o_asase = d_e;
   d.o_asasn = d_nn;
   d.o_tsolv = nullptr;
-  if (bsa::mvp_device(c, *p, d)) return -1;
+  if (bsa::mvp_device(c, *p, d, nullptr, nullptr, nullptr, nullptr, nullptr, true)) return -1;
   BSA_HIP(c, hipMemcpyAsync(asas_alt, d_alt, nrows * 8, hipMemcpyDeviceToHost, s));
   BSA_HIP(c, hipMemcpyAsync(trk, d_trk, nrows * 8, hipMemcpyDeviceToHost, s));
   BSA_HIP(c, hipMemcpyAsync(tas, d_tas, nrows * 8, hipMemcpyDeviceToHost, s));

@@ -5,11 +5,19 @@
 //     C1  all-gather of the 8 state arrays CD/MVP read for other rows
 //         (lat lon trk gs alt vs gseast gsnorth) over xGMI, one RCCL call
 //     K0-K2 detect(own rows x all columns)          asas.py:481-483
+//     C2  all-reduce(max) of the 2-word gate {candidate overflow, P} (RCCL,
+//         device buffer; skipped on one rank)
 //     K3  MVP on the own rows' pairs, only when some rank has a conflict
-//         (asas.py:486-487 `if self.confpairs`), then asas.active = inconf
+//         (asas.py:486-487 `if self.confpairs`), and asas.active = inconf
 //   every step:
 //     K4' Pilot.APorASAS (no wind, pilot.py:41-63) fused with the kinematic
 //         update (traffic.py:425-483) of the own rows
+//
+// A batch of steps is enqueued without any host synchronisation; the gate is
+// read on the device.  A candidate-list overflow sets a sticky abort flag:
+// every later kernel that writes persistent state (K3, K4') becomes a no-op,
+// so the state stays exactly as before the failed step; the host then grows
+// the buffers and re-runs the batch from that step.
 #include <rccl/rccl.h>
 
 #include "bsa_kin_math.h"
@@ -31,11 +39,15 @@ struct SimDev {
   const double *aptrk, *aptas, *apalt, *apvs, *bank, *eps, *accel;
   const double *atrk, *atas, *avs, *aalt;
   const uint8_t *active;
+  const unsigned *sticky;          // abort flag of the step batch
+  unsigned long long *steps_done;  // steps completed in the batch
 };
 
 // Pilot.APorASAS (winddim 0) + UpdateAirSpeed/GroundSpeed/Position, rows [rb, re)
 __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, SimDev d) {
+  if (*d.sticky) return;
   const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
   if (k >= re) return;
   const bool act = d.active[k] != 0;
   const double ptrk = act ? d.atrk[k] : d.aptrk[k];   // pilot.py:41
@@ -64,12 +76,6 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   d.trk[k] = o.trk;
   d.gse[k] = o.gseast;
   d.gsn[k] = o.gsnorth;
-}
-
-__global__ __launch_bounds__(256) void k_copy_active(int nrows, const uint8_t *__restrict__ inconf,
-                                                     uint8_t *__restrict__ active) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < nrows) active[r] = inconf[r];
 }
 
 // field list of one all-gather: fp64 arrays (full n) + optionally one uint8 array
@@ -123,6 +129,8 @@ static SimDev sim_dev(Ctx *c) {
   d.avs = (const double *)c->s_avs.p;
   d.aalt = (const double *)c->s_aalt.p;
   d.active = (const uint8_t *)c->s_active.p;
+  d.sticky = (const unsigned *)((char *)c->sim_ctl.p + 16);
+  d.steps_done = (unsigned long long *)((char *)c->sim_ctl.p + 24);
   return d;
 }
 
@@ -181,7 +189,7 @@ void sim_release(Ctx *c) {
   DevBuf *all[] = {&c->red, &c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
-                   &c->s_active, &c->g_send, &c->g_recv};
+                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl};
   for (auto *b : all) release(*b);
   if (c->comm) {
     ncclCommDestroy((ncclComm_t)c->comm);
@@ -189,45 +197,37 @@ void sim_release(Ctx *c) {
   }
 }
 
+// one CD step of the batch (enqueue only)
 static int sim_cd(Ctx *c) {
   const bsa_sim_params &p = c->simp;
-  int64_t nc = 0, nl = 0;
   if (sim_gather(c)) return -1;
-  if (detect(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, &nc, &nl)) return -1;
-  c->sim_last_conf = nc;
-  c->sim_last_los = nl;
+  unsigned long long *gate = (unsigned long long *)c->sim_ctl.p;
+  if (detect_enqueue(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, gate)) return -1;
   c->sim_cd_calls++;
-  if (!p.reso) return 0;
-  // asas.py:486-487: resolve only if confpairs is non-empty (globally)
-  double any = (double)nc;
-  if (allreduce(c, &any, 1, ncclSum)) return -1;
-  const int64_t rb = c->sim_rb, nrows = c->sim_re - c->sim_rb;
-  if (any > 0.0) {
-    MvpDev d;
-    d.gseast = (const double *)c->s_gse.p;
-    d.gsnorth = (const double *)c->s_gsn.p;
-    d.vs = (const double *)c->own[5].p;
-    d.alt = (const double *)c->own[4].p;
-    d.trk = (const double *)c->own[2].p;
-    d.gs = (const double *)c->own[3].p;
-    d.selalt = (const double *)c->s_selalt.p;
-    d.apvs = (const double *)c->s_apvs.p;
-    d.noreso = nullptr;
-    d.resooff = nullptr;
-    d.asas_alt = (double *)c->s_aalt.p + rb;
-    d.o_trk = (double *)c->s_atrk.p + rb;
-    d.o_tas = (double *)c->s_atas.p + rb;
-    d.o_vs = (double *)c->s_avs.p + rb;
-    d.o_asase = (float *)c->s_ase.p + rb;
-    d.o_asasn = (float *)c->s_asn.p + rb;
-    d.o_tsolv = nullptr;
-    if (mvp_device(c, p.mvp, d)) return -1;
-  }
-  // asas.active = inconf (build-defined stand-in for ResumeNav)
-  hipLaunchKernelGGL(k_copy_active, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, c->stream,
-                     (int)nrows, (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p + rb);
-  BSA_HIP(c, hipGetLastError());
-  return 0;
+  if (c->comm && c->nranks > 1)
+    BSA_NCCL(c, ncclAllReduce(gate, gate, 2, ncclUint64, ncclMax, (ncclComm_t)c->comm, c->stream));
+  const int64_t rb = c->sim_rb;
+  MvpDev d;
+  d.gseast = (const double *)c->s_gse.p;
+  d.gsnorth = (const double *)c->s_gsn.p;
+  d.vs = (const double *)c->own[5].p;
+  d.alt = (const double *)c->own[4].p;
+  d.trk = (const double *)c->own[2].p;
+  d.gs = (const double *)c->own[3].p;
+  d.selalt = (const double *)c->s_selalt.p;
+  d.apvs = (const double *)c->s_apvs.p;
+  d.noreso = nullptr;
+  d.resooff = nullptr;
+  d.asas_alt = (double *)c->s_aalt.p + rb;
+  d.o_trk = (double *)c->s_atrk.p + rb;
+  d.o_tas = (double *)c->s_atas.p + rb;
+  d.o_vs = (double *)c->s_avs.p + rb;
+  d.o_asase = (float *)c->s_ase.p + rb;
+  d.o_asasn = (float *)c->s_asn.p + rb;
+  d.o_tsolv = nullptr;
+  // K3 (+ gate, + asas.active = inconf) on the detect's own row offsets
+  return mvp_device(c, p.mvp, d, (const unsigned *)c->rowoff.p, gate, (unsigned *)((char *)c->sim_ctl.p + 16),
+                    (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p, p.reso != 0);
 }
 
 }  // namespace bsa
@@ -312,6 +312,9 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   BSA_HIP(c, hipMemsetAsync(c->s_asn.p, 0, (size_t)n * 4, c->stream));
   BSA_HIP(c, hipMemsetAsync(c->s_active.p, 0, n, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
+  if (!bsa::ensure(c, c->sim_ctl, 64, "sim control words")) return -1;
+  BSA_HIP(c, hipMemsetAsync(c->sim_ctl.p, 0, 64, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
   c->simp = *p;
   c->sim_rpr = (n + c->nranks - 1) / c->nranks;
   c->sim_rb = std::min<int64_t>(n, (int64_t)c->rank * c->sim_rpr);
@@ -326,18 +329,37 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
   Ctx *c = (Ctx *)cc;
   if (!c) return -1;
   if (!c->sim_ready) return bsa::fail(c, "bsa_sim_step before bsa_sim_init");
+  if (nsteps < 0) return bsa::fail(c, "negative step count");
   BSA_HIP(c, hipSetDevice(c->device));
   const int64_t rb = c->sim_rb, re = c->sim_re;
-  for (int s = 0; s < nsteps; ++s) {
-    if (c->sim_steps % c->simp.cd_every == 0)
-      if (bsa::sim_cd(c)) return -1;
-    if (re > rb) {
-      hipLaunchKernelGGL(bsa::k_sim_pilot_kin, dim3((unsigned)((re - rb + 255) / 256)), dim3(256), 0,
-                         c->stream, (int)rb, (int)re, c->simp.simdt, bsa::sim_dev(c));
+  const int64_t target = c->sim_steps + nsteps;
+  for (int attempt = 0; c->sim_steps < target; ++attempt) {
+    if (attempt > 6) return bsa::fail(c, "candidate buffer overflow in the resident step (retries exhausted)");
+    const int64_t base = c->sim_steps, base_cd = c->sim_cd_calls;
+    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 16, c->stream));  // sticky, steps_done
+    while (c->sim_steps < target) {
+      if (c->sim_steps % c->simp.cd_every == 0)
+        if (bsa::sim_cd(c)) return -1;
+      const int64_t nb = std::max<int64_t>(1, (re - rb + 255) / 256);
+      hipLaunchKernelGGL(bsa::k_sim_pilot_kin, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb, (int)re,
+                         c->simp.simdt, bsa::sim_dev(c));
       BSA_HIP(c, hipGetLastError());
+      c->sim_gathered = c->nranks == 1;
+      c->sim_steps++;
     }
+    // the batch's only host synchronisation: did every step complete?
+    unsigned long long ctl[2] = {0, 0};
+    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 16, hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    if ((unsigned)ctl[0] == 0) break;
+    // aborted at step base + done: the state is that of the step's start
+    const int64_t done = (int64_t)ctl[1];
+    c->sim_steps = base + done;
+    int64_t cds = 0;
+    for (int64_t k = base; k < base + done; ++k) cds += (k % c->simp.cd_every == 0) ? 1 : 0;
+    c->sim_cd_calls = base_cd + cds;
     c->sim_gathered = c->nranks == 1;
-    c->sim_steps++;
+    c->cand_cap *= 2;
   }
   return 0;
 }
@@ -368,6 +390,14 @@ int bsa_sim_read(bsa_ctx *cc, bsa_sim_out *o) {
 int bsa_sim_stats(bsa_ctx *cc, int64_t *out6) {
   Ctx *c = (Ctx *)cc;
   if (!c || !out6) return -1;
+  if (c->sim_cd_calls > 0 && c->counters.p) {  // counts of the last CD step
+    BSA_HIP(c, hipSetDevice(c->device));
+    bsa::Counters h;
+    BSA_HIP(c, hipMemcpyAsync(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    c->sim_last_conf = (int64_t)h.conf;
+    c->sim_last_los = (int64_t)h.los;
+  }
   out6[0] = c->sim_steps;
   out6[1] = c->sim_cd_calls;
   out6[2] = c->sim_last_conf;

@@ -115,6 +115,14 @@ int bsa_last_tiles(bsa_ctx *ctx, int64_t *kept, int64_t *total, int64_t *groups)
  * [1] prefilter, [2] exact, [3] sort+gather, [4] whole detect. */
 int bsa_last_timings(bsa_ctx *ctx, double *ms5);
 
+/* Timing / statistics accumulation over many detects (benchmarking): reset
+ * forgets every recorded detect; summary waits for the stream and returns the
+ * MEAN stage durations over the detects since the reset (same layout as
+ * bsa_last_timings) and the SUMS stats4 = {64-column prefilter groups swept,
+ * candidates, surviving tile pairs, detects}. */
+int bsa_timing_reset(bsa_ctx *ctx);
+int bsa_timing_summary(bsa_ctx *ctx, double *ms5, int64_t *stats4);
+
 /* ---------------------------------------------------------------- MVP
  * MVP.resolve (bluesky/traffic/asas/MVP.py:14-143) on the device-resident
  * conflict pairs of the last bsa_detect (rows [row_begin,row_end) of it).
