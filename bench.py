@@ -89,7 +89,7 @@ def main():
     pairs = float(n) * n * cd_steps
     value = pairs / dt
     pf_s = tm['prefilter'] * 1e-3
-    tested = ts['groups'] / max(ts['detects'], 1) * 128 * 64   # pair tests the prefilter executed
+    tested = ts['groups'] / max(ts['detects'], 1) * 64 * 16    # pair tests the prefilter executed
     roof = dict(bound='valu', kernel='k_prefilter (fp32 VALU reach test, dominant)',
                 achieved=tested * PF_FLOPS_PER_PAIR / pf_s / 1e12, peak=FP32_PEAK_TFLOPS,
                 unit='TFLOP/s')

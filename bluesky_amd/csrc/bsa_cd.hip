@@ -253,10 +253,14 @@ __device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b)
   return u;
 }
 
-// one workgroup per tile, one wave per group (lane = record): group boxes to
-// gbox, their union to tbox
+// one workgroup per tile, one wave per group (lane = record): 16-record
+// sub-group boxes to sbox (nullable), group boxes to gbox, their union to tbox
+__device__ __forceinline__ float xmin(float v, int o) { return fminf(v, __shfl_xor(v, o)); }
+__device__ __forceinline__ float xmax(float v, int o) { return fmaxf(v, __shfl_xor(v, o)); }
+
 __global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restrict__ P,
-                                                 TileBox *__restrict__ gbox, TileBox *__restrict__ tbox) {
+                                                 TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
+                                                 TileBox *__restrict__ tbox) {
   __shared__ TileBox gb[kGroupsPerTile];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = blockIdx.x * kGroupsPerTile + w;
@@ -273,11 +277,36 @@ __global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restric
     hi[3] = p.hi;
     smax = p.s == p.s ? p.s : INFINITY;
   }
-  for (int q = 0; q < 4; ++q) {
-    lo[q] = wmin(lo[q]);
-    hi[q] = wmax(hi[q]);
+  auto mkbox = [&](int count) {
+    TileBox b;
+    for (int q = 0; q < 3; ++q) {
+      b.lo[q] = lo[q];
+      b.hi[q] = hi[q];
+    }
+    b.vlo = lo[3];
+    b.vhi = hi[3];
+    b.smax = smax;
+    b.pad0 = 0.f;
+    b.count = count;
+    b.pad1 = 0;
+    return b;
+  };
+  for (int o = 1; o < 16; o <<= 1) {  // within each 16-lane sub-group
+    for (int q = 0; q < 4; ++q) {
+      lo[q] = xmin(lo[q], o);
+      hi[q] = xmax(hi[q], o);
+    }
+    smax = xmax(smax, o);
   }
-  smax = wmax(smax);
+  const int sg = g * 4 + (lane >> 4);
+  if (sbox && (lane & 15) == 0 && sg * 16 < cnt) sbox[sg] = mkbox(min(16, cnt - sg * 16));
+  for (int o = 16; o < 64; o <<= 1) {
+    for (int q = 0; q < 4; ++q) {
+      lo[q] = xmin(lo[q], o);
+      hi[q] = xmax(hi[q], o);
+    }
+    smax = xmax(smax, o);
+  }
   if (lane == 0) {
     TileBox b;
     for (int q = 0; q < 3; ++q) {
@@ -350,7 +379,6 @@ __global__ __launch_bounds__(256) void k_tilepairs(int nrt, int nct, const TileB
 // ------------------------------------------------------------------ K1a prefilter
 constexpr int PF_BLOCK = 256;
 constexpr int PF_WAVES = PF_BLOCK / 64;
-static_assert(kTile == 2 * PF_BLOCK, "2 rows per lane");
 
 struct RefineParams {
   float R;      // rpz [m]
@@ -438,14 +466,17 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
   return !(qe * qe + qn * qn > prm.lim2);
 }
 
-constexpr int PF_Q1 = 1024;  // per-wave stage-1 queue: u16 (row_local << 6 | col_in_group)
+constexpr int PF_Q1 = 1024;  // per-wave stage-1 queue: u16 (row_local << 6 | column slot)
 constexpr int PF_Q2 = 128;   // per-wave stage-2 queue: uint2 (sorted row, sorted column)
-constexpr int PF_WROWS = 128;  // rows per wave (2 per lane)
-constexpr int PF_BLOCKS_PER_CU = 4;  // LDS-limited: 10 KB per wave
+constexpr int PF_WROWS = 64;   // rows per wave (one per lane)
+constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
+constexpr int PF_BLOCKS_PER_CU = 5;  // LDS-limited: ~7.5 KB per wave
+constexpr int kSub = 16;         // column sub-group (culling granularity)
+constexpr int kSubsPerTile = kTile / kSub;
 constexpr int kWorkShards = 8;   // one dequeue counter per XCD group
 constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
-static_assert(PF_WAVES * PF_WROWS == kTile, "4 waves x 128 rows = one row block");
-static_assert(PF_Q1 >= 2 * 64 * 8, "one 8-column chunk of survivors fits the stage-1 queue");
+static_assert(kSubsPerTile == 32, "one sub-group per lane of a half wave");
+static_assert(PF_Q1 >= 64 * 8, "one 8-column chunk of survivors fits the stage-1 queue");
 
 __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 *__restrict__ cand,
                                          unsigned long long *__restrict__ count,
@@ -475,9 +506,14 @@ __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 
   } while (0)
 #endif
 
-// K1a: each wave sweeps its 128 rows (2 per lane, in registers) against the
-// 512 columns of a tile pair, one 64-column group at a time; groups whose box
-// cannot interact with the wave's row box are skipped.
+// K1a: each wave sweeps its 64 rows (one per lane, in registers) against the
+// columns of a tile pair that survive culling at 16-column sub-group
+// granularity (lanes 0-31 test the 32 sub-group boxes of the 512-column tile
+// against the wave's row box).  The surviving columns are gathered in
+// batches of 64 (four sub-groups; one coalesced record load per lane, issued
+// one batch ahead), projected and staged in the wave's LDS slot as column
+// PAIRS, from which every lane reads them as broadcasts: each packed fp32
+// instruction tests the lane's row against two columns.
 //
 // Stage 1 works in a plane: rows and columns are projected orthogonally onto
 // the plane spanned by an (fp32-)orthonormal pair E, N (the tangent plane at
@@ -487,50 +523,52 @@ __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 
 // k = s^2/2 - |P|^2/2 the test is linear in the column's values:
 //   acc = (K_i + k_j) + s_i s_j + E_i e_j + N_i n_j = ((s_i + s_j)^2 - |P_i - P_j|^2) / 2
 // (K_i = k_i + kPlaneMargin), plus the vertical interval test
-// lo_j < hi_i and hi_j > lo_i.  The three signs are combined with integer ops
-// (keep iff sign(acc) = 0, sign(lo_j - hi_i) = 1, sign(hi_j - lo_i) = 0;
+// lo_j < hi_i and hi_j > lo_i.  The three signs are combined with one
+// v_bitop3 (keep iff sign(acc) = 0, sign(lo_j - hi_i) = 1, sign(hi_j - lo_i) = 0;
 // the +-0 and NaN cases can only keep a pair, never drop one) and shifted
 // into a per-lane column bit mask with v_alignbit.
 //
-// The column records of a group are loaded with one coalesced vector load
-// per lane (issued one group ahead), projected and staged in the wave's LDS
-// slot, from which every lane reads them as broadcasts.  Survivors of each
-// 8-column chunk go to an LDS queue (DPP prefix sum of the per-lane counts).
-// The queue is drained at the end of every group (or when full) with all 64
-// lanes busy through stage 2 (refine) on LDS-resident inputs (the group's
-// staged columns, the item's staged rows, row unit vectors by ds_bpermute).
-// Stage-2 survivors go to a second queue flushed to HBM with one atomic.
+// Survivors of each 8-column chunk go to an LDS queue (DPP prefix sum of the
+// per-lane counts).  The queue is drained after every batch (or when full)
+// with all 64 lanes busy through stage 2 (refine) on LDS-resident inputs (the
+// batch's staged columns, the item's staged rows, row unit vectors by
+// ds_bpermute).  Stage-2 survivors go to a second queue flushed to HBM with
+// one atomic on the wave's candidate shard.
 template <bool NOPRUNE>
 __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, int nrows,
     const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, int ncols,
-    const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ gbox_c,
+    const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ sbox_c,
     const uint2 *__restrict__ tiles, Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
     uint2 *__restrict__ cand, unsigned long long cap) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ uint2 q2s[PF_WAVES][PF_Q2];
-  __shared__ float4 csa[PF_WAVES][kGroup];    // staged column group: k s e n   (stage 1)
-  __shared__ float2 csb[PF_WAVES][kGroup];    //                      lo hi     (stage 1)
-  __shared__ float4 csx[PF_WAVES][kGroup];    //                      x y z -   (refine)
-  __shared__ float4 csc[PF_WAVES][kGroup];    //                      u v vs alt (refine)
-  __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:         u v vs alt (refine)
+  __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
+  __shared__ float4 cen[PF_WAVES][32];      //                      e e' n n'     (stage 1)
+  __shared__ float4 clh[PF_WAVES][32];      //                      lo lo' hi hi' (stage 1)
+  __shared__ float4 csx[PF_WAVES][64];      // staged columns:      x y z -       (refine)
+  __shared__ float4 csv[PF_WAVES][64];      //                      u v vs alt    (refine)
+  __shared__ unsigned cix[PF_WAVES][64];    //                      sorted column index
+  __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:       u v vs alt    (refine)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned long long ntiles = cnt->tiles;
   unsigned short *q1 = q1s[w];
   uint2 *q2 = q2s[w];
-  float4 *sa = csa[w];
-  float2 *sb = csb[w];
+  float *ska = (float *)cka[w];
+  float *sen = (float *)cen[w];
+  float *slh = (float *)clh[w];
   float4 *sx = csx[w];
-  float4 *sc = csc[w];
+  float4 *sv = csv[w];
+  unsigned *sci = cix[w];
   float4 *rv = rsv[w];
   unsigned n2 = 0;        // wave-uniform
-  unsigned groups = 0;    // 64-column groups swept by this wave (for the roofline)
+  unsigned subs = 0;      // 16-column sub-groups swept by this wave (for the roofline)
   const float qnan = __builtin_nanf("");
-  // Dynamic work distribution: an item is one (tile pair, 128-row slice);
+  // Dynamic work distribution: an item is one (tile pair, 64-row slice);
   // each wave dequeues items from the counter of its XCD group (blockIdx % 8)
   // so no single word takes every dequeue (MI355X_MICROARCH 'dequeue').
-  const unsigned long long nitems = ntiles * PF_WAVES;
+  const unsigned long long nitems = ntiles * PF_ITEMS_PER_TILE;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
@@ -551,23 +589,33 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     }
     if (item >= nitems) break;
     do {  // one item; `break` ends it
-    const uint2 rc = tiles[item / PF_WAVES];
-    const int rbase = (int)rc.x * kTile + (int)(item % PF_WAVES) * PF_WROWS;
+    const uint2 rc = tiles[item / PF_ITEMS_PER_TILE];
+    const int rbase = (int)rc.x * kTile + (int)(item % PF_ITEMS_PER_TILE) * PF_WROWS;
     if (rbase >= nrows) break;
     const int cbase = (int)rc.y * kTile;
-    // column groups of this tile that may interact with the wave's row box
-    const int ng = min(kTile / kGroup, (ncols - cbase + kGroup - 1) / kGroup);
-    TileBox rbx = gbox_r[rbase / kGroup];
-    if (rbase + 64 < nrows) rbx = box_union(rbx, gbox_r[rbase / kGroup + 1]);
-    const bool gk = lane < ng && (NOPRUNE || boxes_may_interact(rbx, gbox_c[cbase / kGroup + lane]));
+    // column sub-groups of this tile that may interact with the wave's row box
+    const int nsub = min(kSubsPerTile, (ncols - cbase + kSub - 1) / kSub);
+    const TileBox rbx = gbox_r[rbase / kGroup];
+    const bool gk = lane < nsub && (NOPRUNE || boxes_may_interact(rbx, sbox_c[cbase / kSub + lane]));
     unsigned gm = (unsigned)__ballot(gk);
     if (!gm) break;
-    groups += (unsigned)__popc(gm);
+    subs += (unsigned)__popc(gm);
 
-    // the next group's column record of this lane (loaded one group ahead)
-    auto load_col = [&](int g, PFRec &r, PFVel &v) {
-      const int j = cbase + g * kGroup + lane;
-      if (j < ncols) {
+    // this lane's slot of the next batch: the (lane / 16)-th remaining
+    // sub-group, column lane % 16 of it (sub-groups taken in ascending order)
+    auto batch_col = [&](unsigned m) -> int {
+      const unsigned q = (unsigned)lane >> 4;
+      for (unsigned t = 0; t < q && m; ++t) m &= m - 1;
+      if (!m) return -1;
+      const int j = cbase + __builtin_ctz(m) * kSub + (lane & 15);
+      return j < ncols ? j : -1;
+    };
+    auto drop4 = [](unsigned m) {
+      for (int t = 0; t < 4 && m; ++t) m &= m - 1;
+      return m;
+    };
+    auto load_col = [&](int j, PFRec &r, PFVel &v) {
+      if (j >= 0) {
         r = pcol[j];
         v = vcol[j];
       } else {
@@ -579,19 +627,24 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
         v.flags = 1;
       }
     };
-    int g = __builtin_ctz(gm);
+    int jn = batch_col(gm);
     PFRec nx;
     PFVel nv;
-    load_col(g, nx, nv);
+    load_col(jn, nx, nv);
 
-    const int ka_row = rbase + lane, kb_row = rbase + 64 + lane;
-    const bool va = ka_row < nrows, vb = kb_row < nrows;
-    PFRec A, B;
-    PFVel AV, BV;
-    if (va) { A = prow[ka_row]; AV = vrow[ka_row]; }
-    else { A.x = A.y = A.z = A.s = A.alt = A.pad = 0.f; A.lo = A.hi = 0.f; AV.u = AV.v = AV.vs = 0.f; AV.flags = 1; }
-    if (vb) { B = prow[kb_row]; BV = vrow[kb_row]; }
-    else { B.x = B.y = B.z = B.s = B.alt = B.pad = 0.f; B.lo = B.hi = 0.f; BV.u = BV.v = BV.vs = 0.f; BV.flags = 1; }
+    const int krow = rbase + lane;
+    const bool va = krow < nrows;
+    PFRec A;
+    PFVel AV;
+    if (va) {
+      A = prow[krow];
+      AV = vrow[krow];
+    } else {
+      A.x = A.y = A.z = A.s = A.alt = A.pad = 0.f;
+      A.lo = A.hi = 0.f;
+      AV.u = AV.v = AV.vs = 0.f;
+      AV.flags = 1;
+    }
     // the item's plane: o = first row of the slice, E / N an orthonormal
     // tangent pair at o (any orthonormal pair is exact-safe; near a pole, or
     // for a non-finite o, the x / y axes)
@@ -616,21 +669,18 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
       e = dx * ex + dy * ey;
       n = dx * nxx + dy * nyy + dz * nzz;
     };
-    float ea, na, eb, nb;
-    project(A.x, A.y, A.z, ea, na);
-    project(B.x, B.y, B.z, eb, nb);
-    const f2 E = {ea, eb}, N = {na, nb}, S = {A.s, B.s};
-    const f2 K = {0.5f * A.s * A.s - 0.5f * (ea * ea + na * na) + kPlaneMargin,
-                  0.5f * B.s * B.s - 0.5f * (eb * eb + nb * nb) + kPlaneMargin};
-    const f2 HI = {A.hi, B.hi}, LO = {A.lo, B.lo};
-    const float rxa = A.x, rya = A.y, rza = A.z, rxb = B.x, ryb = B.y, rzb = B.z;
-    // rows of this item for the refine (u = NaN: never refine)
+    float re_, rn_;
+    project(A.x, A.y, A.z, re_, rn_);
+    const f2 E = {re_, re_}, N = {rn_, rn_}, S = {A.s, A.s};
+    const float kr = 0.5f * A.s * A.s - 0.5f * (re_ * re_ + rn_ * rn_) + kPlaneMargin;
+    const f2 K = {kr, kr};
+    const f2 HI = {A.hi, A.hi}, LO = {A.lo, A.lo};
+    const float rx = A.x, ry = A.y, rz = A.z;
+    // the row of this lane for the refine (u = NaN: never refine)
     rv[lane] = make_float4(AV.flags ? qnan : AV.u, AV.v, AV.vs, A.alt);
-    rv[64 + lane] = make_float4(BV.flags ? qnan : BV.u, BV.v, BV.vs, B.alt);
-    const unsigned rowmask_a = va ? 0xffu : 0u, rowmask_b = vb ? 0xffu : 0u;
-    unsigned n1 = 0;  // wave-uniform
-    int gs = g;       // the group being swept (its columns are staged)
-    unsigned long long colmask = 0;  // valid columns of the swept group
+    const unsigned rowmask = va ? 0xffu : 0u;
+    unsigned n1 = 0;                 // wave-uniform
+    unsigned long long colmask = 0;  // valid slots of the swept batch
 
     auto drain = [&]() {
       __builtin_amdgcn_wave_barrier();
@@ -640,21 +690,16 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
         const unsigned e = q1[k < n1 ? k : b0];
         const unsigned rl = e >> 6, cl = e & 63u;
         // the row's unit vector from its owner lane's registers
-        const int src = (int)((rl & 63u) << 2);
-        const float pxa = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rxa)));
-        const float pxb = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rxb)));
-        const float pya = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rya)));
-        const float pyb = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(ryb)));
-        const float pza = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rza)));
-        const float pzb = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rzb)));
+        const int src = (int)(rl << 2);
+        const float px = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rx)));
+        const float py = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(ry)));
+        const float pz = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rz)));
         bool keep = false;
         unsigned gi = 0, gj = 0;
         if (k < n1) {
-          const bool hb = rl >= 64u;
-          const float4 rpos = make_float4(hb ? pxb : pxa, hb ? pyb : pya, hb ? pzb : pza, 0.f);
           gi = (unsigned)rbase + rl;
-          gj = (unsigned)(cbase + gs * kGroup) + cl;
-          keep = NOPRUNE ? true : pf_refine(rpos, rv[rl], sx[cl], sc[cl], prm);
+          gj = sci[cl];
+          keep = NOPRUNE ? true : pf_refine(make_float4(px, py, pz, 0.f), rv[rl], sx[cl], sv[cl], prm);
         }
         const unsigned long long mk = __ballot(keep);
         if (mk) {
@@ -673,86 +718,85 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
       PF_STAMP(2);
     };
 
-    // survivors of an 8-column chunk arrive as per-lane bit masks (ba: row a,
-    // bb: row b; bit 7 - u = column col0 + u) and are queued once per chunk
-    auto enqueue = [&](unsigned ba, unsigned bb, unsigned col0) {
-      const unsigned c = (unsigned)__popc(ba) + (unsigned)__popc(bb);
+    // survivors of an 8-column chunk arrive as a per-lane bit mask (bit 7 - u
+    // = slot col0 + u) and are queued once per chunk
+    auto enqueue = [&](unsigned bm, unsigned col0) {
+      const unsigned c = (unsigned)__popc(bm);
       const unsigned x = wave_incl_scan(c);
       const unsigned total = __builtin_amdgcn_readlane(x, 63);
       if (total == 0) return;
       if (n1 + total > (unsigned)PF_Q1) drain();
       unsigned pos = n1 + x - c;
-      while (ba) {
-        const unsigned b = 31u - (unsigned)__builtin_clz(ba);
+      while (bm) {
+        const unsigned b = 31u - (unsigned)__builtin_clz(bm);
         q1[pos++] = (unsigned short)(((unsigned)lane << 6) | (col0 + 7u - b));
-        ba ^= 1u << b;
-      }
-      while (bb) {
-        const unsigned b = 31u - (unsigned)__builtin_clz(bb);
-        q1[pos++] = (unsigned short)(((unsigned)(64 + lane) << 6) | (col0 + 7u - b));
-        bb ^= 1u << b;
+        bm ^= 1u << b;
       }
       n1 = __builtin_amdgcn_readfirstlane(n1 + total);
     };
 
     PF_STAMP(0);
     for (;;) {
-      // project and stage the current group (in-order LDS within the wave:
-      // these writes land after the previous group's reads, incl. its drain)
+      // project and stage the current batch (in-order LDS within the wave:
+      // these writes land after the previous batch's reads, incl. its drain)
       {
         float ce, cn;
         project(nx.x, nx.y, nx.z, ce, cn);
         const float ck = 0.5f * nx.s * nx.s - 0.5f * (ce * ce + cn * cn);
-        sa[lane] = make_float4(ck, nx.s, ce, cn);
-        sb[lane] = make_float2(nx.lo, nx.hi);
+        const int pb = (lane >> 1) * 4 + (lane & 1);  // pair lane>>1, half lane&1
+        ska[pb] = ck;
+        ska[pb + 2] = nx.s;
+        sen[pb] = ce;
+        sen[pb + 2] = cn;
+        slh[pb] = nx.lo;
+        slh[pb + 2] = nx.hi;
         sx[lane] = make_float4(nx.x, nx.y, nx.z, 0.f);
-        sc[lane] = make_float4(nv.flags ? qnan : nv.u, nv.v, nv.vs, nx.alt);
-        colmask = __ballot(cbase + g * kGroup + lane < ncols);
+        sv[lane] = make_float4(nv.flags ? qnan : nv.u, nv.v, nv.vs, nx.alt);
+        sci[lane] = (unsigned)jn;
+        colmask = __ballot(jn >= 0);
       }
-      gs = g;
-      gm &= gm - 1;
-      if (gm) {  // prefetch the next group while this one is swept
-        g = __builtin_ctz(gm);
-        load_col(g, nx, nv);
+      gm = drop4(gm);
+      if (gm) {  // prefetch the next batch while this one is swept
+        jn = batch_col(gm);
+        load_col(jn, nx, nv);
       }
-      for (int j0 = 0; j0 < kGroup; j0 += 8) {
-        unsigned ba = 0, bb = 0;
+      // sweep only the chunks holding valid slots
+      const int nchunk = colmask ? (64 - __builtin_clzll(colmask) + 7) >> 3 : 0;
+      for (int ch = 0; ch < nchunk; ++ch) {
+        const int j0 = ch * 8;
+        unsigned bm = 0;
+        float4 pa[4], pe[4], pl[4];
 #pragma unroll
-        for (int h4 = 0; h4 < 8; h4 += 4) {
-          float4 ca[4];
-          float2 cb[4];
+        for (int u = 0; u < 4; ++u) {
+          pa[u] = cka[w][(j0 >> 1) + u];
+          pe[u] = cen[w][(j0 >> 1) + u];
+          pl[u] = clh[w][(j0 >> 1) + u];
+        }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            ca[u] = sa[j0 + h4 + u];
-            cb[u] = sb[j0 + h4 + u];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (NOPRUNE) {
-              ba = (ba << 1) | 1u;
-              bb = (bb << 1) | 1u;
-            } else {
-              f2 acc = K + (f2){ca[u].x, ca[u].x};
-              acc = __builtin_elementwise_fma(S, (f2){ca[u].y, ca[u].y}, acc);
-              acc = __builtin_elementwise_fma(E, (f2){ca[u].z, ca[u].z}, acc);
-              acc = __builtin_elementwise_fma(N, (f2){ca[u].w, ca[u].w}, acc);
-              const f2 dlo = (f2){cb[u].x, cb[u].x} - HI;   // < 0 to keep
-              const f2 dhi = (f2){cb[u].y, cb[u].y} - LO;   // > 0 to keep
-              const unsigned ta = (unsigned)__float_as_int(dlo.x) &
-                                  ~((unsigned)__float_as_int(acc.x) | (unsigned)__float_as_int(dhi.x));
-              const unsigned tb = (unsigned)__float_as_int(dlo.y) &
-                                  ~((unsigned)__float_as_int(acc.y) | (unsigned)__float_as_int(dhi.y));
-              ba = __builtin_amdgcn_alignbit(ba, ta, 31);   // (ba << 1) | (ta >> 31)
-              bb = __builtin_amdgcn_alignbit(bb, tb, 31);
-            }
+        for (int u = 0; u < 4; ++u) {
+          if (NOPRUNE) {
+            bm = (bm << 2) | 3u;
+          } else {
+            f2 acc = K + (f2){pa[u].x, pa[u].y};
+            acc = __builtin_elementwise_fma(S, (f2){pa[u].z, pa[u].w}, acc);
+            acc = __builtin_elementwise_fma(E, (f2){pe[u].x, pe[u].y}, acc);
+            acc = __builtin_elementwise_fma(N, (f2){pe[u].z, pe[u].w}, acc);
+            const f2 dlo = (f2){pl[u].x, pl[u].y} - HI;   // < 0 to keep
+            const f2 dhi = (f2){pl[u].z, pl[u].w} - LO;   // > 0 to keep
+            const unsigned t0 = (unsigned)__float_as_int(dlo.x) &
+                                ~((unsigned)__float_as_int(acc.x) | (unsigned)__float_as_int(dhi.x));
+            const unsigned t1 = (unsigned)__float_as_int(dlo.y) &
+                                ~((unsigned)__float_as_int(acc.y) | (unsigned)__float_as_int(dhi.y));
+            bm = __builtin_amdgcn_alignbit(bm, t0, 31);   // (bm << 1) | (t0 >> 31)
+            bm = __builtin_amdgcn_alignbit(bm, t1, 31);
           }
         }
         const unsigned cm = (unsigned)(colmask >> j0) & 0xffu;
-        // bit 7 - u <-> column j0 + u: reverse the 8 column-valid bits
+        // bit 7 - u <-> slot j0 + u: reverse the 8 slot-valid bits
         const unsigned cmr = __builtin_bitreverse32(cm) >> 24;
-        enqueue(ba & cmr & rowmask_a, bb & cmr & rowmask_b, (unsigned)j0);
+        enqueue(bm & cmr & rowmask, (unsigned)j0);
       }
-      // refine this group's survivors while its columns are staged
+      // refine this batch's survivors while its columns are staged
       if (n1) drain();
       PF_STAMP(1);
       if (!gm) break;
@@ -761,7 +805,7 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
   }
   PF_STAMP(0);
   if (n2) pf_flush(q2, n2, lane, ccand, cshard, ccap);
-  if (lane == 0 && groups) atomicAdd(&cnt->groups, (unsigned long long)groups);
+  if (lane == 0 && subs) atomicAdd(&cnt->groups, (unsigned long long)subs);
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
   if (lane == 0)
@@ -1205,8 +1249,10 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
   const long long ntp = (long long)nrt * nct;
   const int ngr = (int)((nrows + kGroup - 1) / kGroup), ngc = (int)((n + kGroup - 1) / kGroup);
+  const int nsc = (int)((n + kSub - 1) / kSub);
   if (!ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
       !ensure(c, c->gbox_c, ngc * sizeof(TileBox), "column group boxes") ||
+      !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
       !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
     return -1;
   if (!shared && (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
@@ -1215,10 +1261,10 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const TileBox *gbox_r = shared ? (const TileBox *)c->gbox_c.p : (const TileBox *)c->gbox_r.p;
   const TileBox *tbox_r = shared ? (const TileBox *)c->tbox_c.p : (const TileBox *)c->tbox_r.p;
   if (!shared)
-    hipLaunchKernelGGL(k_boxes, dim3(nrt), dim3(kTile), 0, c->stream, (int)nrows, pfrow,
+    hipLaunchKernelGGL(k_boxes, dim3(nrt), dim3(kTile), 0, c->stream, (int)nrows, pfrow, (TileBox *)nullptr,
                        (TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p);
   hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
-                     (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p);
+                     (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p);
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + 255) / 256)), dim3(256), 0, c->stream, nrt, nct,
                      tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p, &dcnt->tiles);
   BSA_HIP(c, hipGetLastError());
@@ -1242,16 +1288,16 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
   const unsigned pf_grid = (unsigned)std::max<long long>(
-      kWorkShards, std::min<long long>(ntp * PF_WAVES, 256 * PF_BLOCKS_PER_CU));
+      kWorkShards, std::min<long long>(ntp * PF_ITEMS_PER_TILE / PF_WAVES + 1, 256 * PF_BLOCKS_PER_CU));
   if (noprune)
     hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
-                       (const TileBox *)c->gbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
+                       (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap);
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
-                       (const TileBox *)c->gbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
+                       (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap);
   BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(ev[2], c->stream));

@@ -95,7 +95,7 @@ struct Counters {
   unsigned long long conf;
   unsigned long long los;
   unsigned long long tiles;
-  unsigned long long groups;  // (128-row x 64-column) groups swept by the prefilter
+  unsigned long long groups;  // (64-row x 16-column) blocks swept by the prefilter
   unsigned long long pad[3];
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];
@@ -125,7 +125,7 @@ struct Ctx {
   DevBuf rowrec, colrec, pfrow, pfcol, pfvrow, pfvcol;
   // spatial order: Morton keys and the sorted-position -> original-index maps
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
-  DevBuf tbox_r, tbox_c, gbox_r, gbox_c, tilepairs, workq;
+  DevBuf tbox_r, tbox_c, gbox_r, gbox_c, sbox_c, tilepairs, workq;
   DevBuf rowcnt, rowoff, lslot;  // K2 counting sort
   // reusable spatial order (any permutation gives identical results)
   bool perm_valid = false, perm_shared = false, perm_distinct = false;
