@@ -51,6 +51,7 @@ SIGNATURES = {
     'bsa_last_tiles': (ctypes.c_int, [_vp, _c_i64p, _c_i64p, _c_i64p]),
     'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_timing_reset': (ctypes.c_int, [_vp]),
+    'bsa_set_candidate_capacity': (ctypes.c_int, [_vp, ctypes.c_int64]),
     'bsa_timing_summary': (ctypes.c_int, [_vp, _c_dp, _c_i64p]),
 }
 
@@ -243,6 +244,11 @@ class Context:
         v = ctypes.c_int64()
         self.check(self.lib.bsa_last_candidates(self.h, ctypes.byref(v)), 'bsa_last_candidates')
         return v.value
+
+    def set_candidate_capacity(self, capacity):
+        """Candidate-list capacity for the next detects (grown on overflow)."""
+        self.check(self.lib.bsa_set_candidate_capacity(self.h, int(capacity)),
+                   'bsa_set_candidate_capacity')
 
     def last_tiles(self):
         kept, total, groups = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

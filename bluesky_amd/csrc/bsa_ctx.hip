@@ -221,6 +221,14 @@ int bsa_last_candidates(bsa_ctx *c, int64_t *n_candidates) {
   return 0;
 }
 
+int bsa_set_candidate_capacity(bsa_ctx *c, int64_t capacity) {
+  if (!c) return -1;
+  if (capacity < 1) return bsa::fail(c, "candidate capacity must be >= 1");
+  const unsigned long long s = bsa::kCandShards;
+  c->cand_cap = ((unsigned long long)capacity + s - 1) / s * s;
+  return 0;
+}
+
 int bsa_last_tiles(bsa_ctx *c, int64_t *kept, int64_t *total, int64_t *groups) {
   if (!c || !kept || !total || !groups) return -1;
   *kept = c->last_tiles;

@@ -359,7 +359,14 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     for (int64_t k = base; k < base + done; ++k) cds += (k % c->simp.cd_every == 0) ? 1 : 0;
     c->sim_cd_calls = base_cd + cds;
     c->sim_gathered = c->nranks == 1;
-    c->cand_cap *= 2;
+    // grow: at least double, and enough for the last detect's demand (its
+    // shard counters keep counting past the capacity)
+    bsa::Counters h;
+    BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
+    unsigned long long worst = 0;
+    for (int q = 0; q < bsa::kCandShards; ++q) worst = std::max(worst, h.cshard[q][0]);
+    c->cand_cap = std::max(2 * c->cand_cap,
+                           (unsigned long long)bsa::kCandShards * (worst + worst / 4 + 1024));
   }
   return 0;
 }

@@ -105,9 +105,14 @@ int bsa_fetch_pairs(bsa_ctx *ctx,
  * conservative prefilter and were evaluated exactly in fp64). */
 int bsa_last_candidates(bsa_ctx *ctx, int64_t *n_candidates);
 
+/* Candidate-list capacity (pairs surviving the prefilter) for the next
+ * detects; rounded up to a multiple of the shard count.  Detects grow it on
+ * overflow (with a retry), so this is a tuning / testing knob only. */
+int bsa_set_candidate_capacity(bsa_ctx *ctx, int64_t capacity);
+
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
  * bounding-box cull, the total number of tile pairs, and the number of
- * (128-row x 64-column) groups the prefilter actually swept. */
+ * (64-row x 16-column) blocks the prefilter actually swept. */
 int bsa_last_tiles(bsa_ctx *ctx, int64_t *kept, int64_t *total, int64_t *groups);
 
 /* Device time of the last detect's stages in milliseconds, measured with
@@ -118,8 +123,8 @@ int bsa_last_timings(bsa_ctx *ctx, double *ms5);
 /* Timing / statistics accumulation over many detects (benchmarking): reset
  * forgets every recorded detect; summary waits for the stream and returns the
  * MEAN stage durations over the detects since the reset (same layout as
- * bsa_last_timings) and the SUMS stats4 = {64-column prefilter groups swept,
- * candidates, surviving tile pairs, detects}. */
+ * bsa_last_timings) and the SUMS stats4 = {(64-row x 16-column) prefilter
+ * blocks swept, candidates, surviving tile pairs, detects}. */
 int bsa_timing_reset(bsa_ctx *ctx);
 int bsa_timing_summary(bsa_ctx *ctx, double *ms5, int64_t *stats4);
 

@@ -115,3 +115,14 @@ def test_full_size_100k_row_sample(ctx):
     util.assert_detect_equal(sub, exp, RPZ, TLA)
     # density-matched box: ~1.4 conflict pairs per aircraft
     assert 0.5 * t.ntraf < len(got['ci']) < 3.0 * t.ntraf
+
+
+def test_detect_overflow_retry_is_exact(ctx):
+    """A tiny candidate list overflows, the detect grows it and retries: the
+    result equals the normal run's exactly."""
+    t = synth.box(3000, 120.0, seed=43)
+    exp = statebased.detect_indices(t, t, synth.RPZ, synth.HPZ, synth.TLOOKAHEAD, ctx=ctx)
+    ctx.set_candidate_capacity(8)
+    got = statebased.detect_indices(t, t, synth.RPZ, synth.HPZ, synth.TLOOKAHEAD, ctx=ctx)
+    for k in ('ci', 'cj', 'li', 'lj', 'qdr', 'dist', 'tcpa', 'tinconf', 'inconf', 'tcpamax'):
+        assert np.array_equal(np.asarray(got[k]), np.asarray(exp[k])), k
