@@ -31,8 +31,21 @@ from bluesky_amd import _lib, dist, resident, synth  # noqa: E402
 FP64_PEAK_TFLOPS = 78.6      # MI355X fp64 vector (spec, FMA = 2 flops)
 FP32_PEAK_TFLOPS = 157.3     # MI355X fp32 vector (MI355X_MICROARCH.md)
 OPS_PER_PAIR = 110           # algorithmic fp64 ops per pair-eval
-PF_FLOPS_PER_PAIR = 14       # prefilter reach test per tested pair
-TILE = 512
+PF_FLOPS_PER_PAIR = 9        # prefilter stage-1 fp32 flops per tested pair:
+                             # acc = K + k (1) + 3 FMA (6); lo - hi, hi - lo (2)
+KIN_BYTES_PER_AC = 234       # K4 algorithmic HBM bytes per aircraft-step
+HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E (spec)
+PMC_JSON = os.path.join(REPO, 'profiles', 'pmc_latest.json')
+
+
+def pmc_figures():
+    """Per-launch memory-side bytes etc. from the committed rocprofv3 --pmc
+    passes of this bench (tools/pmc_roofline.py), or {} if absent."""
+    try:
+        with open(PMC_JSON) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
 
 
 def cpu_baseline(t, rows_sample):
@@ -90,11 +103,32 @@ def main():
     value = pairs / dt
     pf_s = tm['prefilter'] * 1e-3
     tested = ts['groups'] / max(ts['detects'], 1) * 64 * 16    # pair tests the prefilter executed
-    roof = dict(bound='valu', kernel='k_prefilter (fp32 VALU reach test, dominant)',
+    pmc = pmc_figures()
+    pf = pmc.get('k_prefilter', {})
+    roof = dict(bound='valu', kernel='k_prefilter (fp32 packed VALU stage-1 test, dominant)',
                 achieved=tested * PF_FLOPS_PER_PAIR / pf_s / 1e12, peak=FP32_PEAK_TFLOPS,
                 unit='TFLOP/s')
     roof['frac'] = roof['achieved'] / roof['peak']
-    roof['traffic'] = None
+    roof['traffic'] = (pf['hbm_read_bytes'] + pf['hbm_write_bytes']) if 'hbm_write_bytes' in pf else None
+    roof['traffic_source'] = 'profiles/pmc_latest.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch)'
+    if 'lds_bank_conflict_rate' in pf:
+        roof['lds_bank_conflict_rate'] = pf['lds_bank_conflict_rate']
+    kin = pmc.get('k_sim_pilot_kin', {})
+    propagation = None
+    if kin.get('dur_ns'):
+        nrows_r0 = (n + world - 1) // world
+        alg = KIN_BYTES_PER_AC * nrows_r0
+        propagation = dict(kernel='k_sim_pilot_kin', bound='hbm', algorithmic_bytes=alg,
+                           duration_us_profiled=kin['dur_ns'] * 1e-3,
+                           achieved_GBps=alg / kin['dur_ns'], peak_GBps=HBM_PEAK_GBPS,
+                           frac=alg / kin['dur_ns'] / HBM_PEAK_GBPS,
+                           measured_bytes=(kin.get('hbm_read_bytes', 0) + kin.get('hbm_write_bytes', 0)) or None)
+    ex = pmc.get('k_exact', {})
+    exact_fp64 = None
+    if ex.get('fp64_flops'):
+        exact_fp64 = dict(kernel='k_exact', fp64_flops_per_launch=ex['fp64_flops'],
+                          achieved_TFLOPs=ex['fp64_flops'] / (tm['exact'] * 1e-3) / 1e12,
+                          peak_TFLOPs=FP64_PEAK_TFLOPS)
     out = dict(metric='CD pair-evals/s at 100k aircraft (GPU-resident sim step, ASAS every step)',
                value=value, unit='pair-evals/s', n_gpus=world, steps=args.steps, warmup=args.warmup,
                ms_per_step=dt / args.steps * 1e3, higher_is_better=True, scaling='strong',
@@ -110,7 +144,8 @@ def main():
                prefilter_pair_tests_rank0=tested,
                tile_pairs_rank0=ts['tiles'] / max(ts['detects'], 1),
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
-               cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12))
+               cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),
+               propagation=propagation, exact_fp64=exact_fp64)
     if rank == 0 and world == 1 and not args.no_cpu:
         out['cpu_baseline'] = cpu_baseline(t, args.cpu_rows)
         out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']

@@ -1,0 +1,28 @@
+# Full measurement set on the GPU box (one call): parity tests, a kernel-trace
+# --stats profile, the --pmc passes that feed profiles/pmc_latest.json, and the
+# bench line (with the CPU baseline).  Counter passes are separate runs with
+# --kernel-trace only (no sys/runtime trace), each under its own time limit.
+set -u
+TAG=${TAG:-r01}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- \
+    python bench.py --steps 20 --warmup 3 --no-cpu > $OUT/prof_stats.log 2>&1
+rc=$?; echo "stats rc=$rc"; [ $rc -eq 0 ] || exit $rc
+i=0
+for set in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU" \
+           "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_VALU"; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_p$i -o run -- \
+      python bench.py --steps 3 --warmup 1 --no-cpu > $OUT/pmc_p$i.log 2>&1
+  rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+python tools/pmc_roofline.py $OUT/pmc_latest.json $OUT/pmc_p1 $OUT/pmc_p2 $OUT/pmc_p3 $OUT/pmc_p4
+cp $OUT/pmc_latest.json profiles/pmc_latest.json
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err
+rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json
