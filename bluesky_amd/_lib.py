@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get('BSACCEL_LIB', os.path.join(_HERE, 'libbsaccel.so'))
 ABI_VERSION = 1
 FLAG_WITH_DCPA = 1
 FLAG_NOPRUNE = 2
+FLAG_RESORT = 4
+FLAG_KWIK = 8
 
 _c_dp = ctypes.POINTER(ctypes.c_double)
 _c_fp = ctypes.POINTER(ctypes.c_float)

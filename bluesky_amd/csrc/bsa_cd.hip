@@ -156,7 +156,9 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   r.v = gs * cos(trk);
   r.alt = intr.alt[o];
   r.vs = intr.vs[o];
-  for (int q = 0; q < 7; ++q) r.pad[q] = 0.0;
+  r.pad0 = 0.0;
+  r.ilat = intr.lat[o];
+  for (int q = 0; q < 5; ++q) r.pad[q] = 0.0;
   R[k] = r;
   const double lor = lo * kD2R;
   const PFRec p = make_pf(cosl * cos(lor), cosl * sin(lor), sinl, reach_h(rpz, gs, tlap), r.alt,
@@ -199,7 +201,8 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
   c.alt = own.alt[o];
   c.vs = own.vs[o];
   c.eps = (olat == 0.0) ? 0.000001 : 0.0;       // geo.py:128 (column-indexed)
-  for (int q = 0; q < 6; ++q) c.pad[q] = 0.0;
+  c.olat = olat;
+  for (int q = 0; q < 5; ++q) c.pad[q] = 0.0;
   C[k] = c;
   const double lor = lo * kD2R;
   // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
@@ -838,10 +841,37 @@ struct PairResult {
   double qdr, dist, tcpa, tin, dcpa;
 };
 
+// numpy.remainder for float64 (npy_divmod semantics)
+__device__ __forceinline__ double np_rem(double a, double b) {
+  double mod = fmod(a, b);
+  if (mod != 0.0) {
+    if ((b < 0) != (mod < 0)) mod += b;
+  } else {
+    mod = copysign(0.0, b);
+  }
+  return mod;
+}
+
 // One (i, j) entry of StateBasedCD.detect + geo.qdrdist_matrix, i != j.
+// KWIK (opt-in variant, BSA_FLAG_KWIK): geo.kwikqdrdist_matrix (geo.py:347-363)
+// replaces qdrdist_matrix, its metre distance handed over in nm (/ nm) so that
+// StateBasedCD.py:22's `* nm` restores metres -- the reference's own detect
+// with the geo function swapped (tools/make_golden.py captures exactly that).
+template <bool KWIK>
 __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c, double rpz,
                                                 double hpz, double tla) {
   PairResult o;
+  double qdr, dist_nm;
+  if (KWIK) {
+    // [i, j]: dlat = latb[j] - lata[i], cavelat = cos(radians(lata[j] + latb[i]) * 0.5)
+    const double dlat = (c.lat - r.lat) * kD2R;
+    const double dlon = (c.lon - r.lon) * kD2R;
+    const double cavelat = cos(((c.olat + r.ilat) * kD2R) * 0.5);
+    const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
+    const double dist_m = 6371000. * dangle;
+    qdr = np_rem(atan2(dlon * cavelat, dlat) * kR2D, 360.);
+    dist_nm = dist_m / kNM;
+  } else {
   // ---- geo.qdrdist_matrix (geo.py:118-160)
   const double prodla = r.lat * c.lat;
   double rr;
@@ -862,14 +892,15 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
   const double x2 = r.sinlat * c.coslat;
   const double x3 = x2 * cos21;
   const double x = x1 - x3;
-  const double qdr = atan2(y, x) * kR2D;
+  qdr = atan2(y, x) * kR2D;
   const double sin10 = fabs(sin(sin1 / 2.));
   const double sin20 = fabs(sin(sin2 / 2.));
   const double sin1sin1 = sin10 * sin10;
   const double sin2sin2 = sin20 * sin20;
   const double hav = sin1sin1 + (r.coslat * c.coslat) * sin2sin2;
   const double dist_c = 2. * atan2(sqrt(hav), sqrt(1 - hav));
-  const double dist_nm = (rr / kNM) * dist_c;
+  dist_nm = (rr / kNM) * dist_c;
+  }
 
   // ---- StateBasedCD.detect (StateBasedCD.py:22-83), off-diagonal entry
   const double dist = dist_nm * kNM + 0.0;
@@ -919,7 +950,7 @@ __global__ __launch_bounds__(256) void k_exact(
     unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
     unsigned char *__restrict__ cflag, unsigned long long *__restrict__ ckey,
     double *__restrict__ cpay, unsigned char *__restrict__ inconf,
-    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt) {
+    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int kwik) {
   if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
   unsigned long long pre[kCandShards + 1];
   const unsigned long long ncand = cand_prefix(cnt, cap, pre);
@@ -934,7 +965,8 @@ __global__ __launch_bounds__(256) void k_exact(
     const unsigned oi = perm_r[p.x], oj = perm_c[p.y];
     unsigned char flag = 0;
     if (oi != oj) {
-      const PairResult o = eval_pair(R[p.x], C[p.y], rpz, hpz, tla);
+      const PairResult o = kwik ? eval_pair<true>(R[p.x], C[p.y], rpz, hpz, tla)
+                                : eval_pair<false>(R[p.x], C[p.y], rpz, hpz, tla);
       flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
       const int row = (int)oi - rb;
       if (flag) ckey[idx] = ((unsigned long long)oi << 32) | oj;
@@ -1188,8 +1220,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     return 0;
   }
   c->empty_detect = false;
-  const int noprune = (flags & BSA_FLAG_NOPRUNE) ? 1 : 0;
   const bool distinct = c->has_intruder;
+  const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;
+  // KWIK: stage 1 is exact-safe only with the pair's own mean latitude in
+  // cavelat (own == intruder), and the CPA refine's geometry
+  // is the great circle's: a distinct intruder set disables the prefilter,
+  // and the refine keeps every stage-1 survivor.
+  const int noprune = ((flags & BSA_FLAG_NOPRUNE) || (kwik && distinct)) ? 1 : 0;
   DevBuf *I = distinct ? c->intr : c->own;
   SoA6 own{(const double *)c->own[0].p, (const double *)c->own[1].p, (const double *)c->own[2].p,
            (const double *)c->own[3].p, (const double *)c->own[4].p, (const double *)c->own[5].p};
@@ -1284,7 +1321,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     return -1;
   const float T = (float)(tla > 0.0 ? tla : 0.0);
   const float lim = (float)((rpz + kEABS) / (1.0 - kE1));
-  const RefineParams rp{(float)rpz, (float)hpz, T, lim * lim};
+  const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : lim * lim};
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
   const unsigned pf_grid = (unsigned)std::max<long long>(
@@ -1307,7 +1344,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, cap, rpz, hpz, tla, (int)rb, (int)nrows,
                      (unsigned char *)c->cflag.p, (unsigned long long *)c->ckey.p, (double *)c->cpay.p,
                      (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
-                     (unsigned *)c->rowcnt.p);
+                     (unsigned *)c->rowcnt.p, kwik);
   BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(ev[3], c->stream));
   // ---- K2: row offsets, scatter into row segments, per-row rank + gather

@@ -39,7 +39,9 @@ struct alignas(16) RowRec {
   double hemA;            // |lat| * (rwgs84(lat) + a)              geo.py:127
   double u, v;            // int.gs[i] * sin/cos(radians(int.trk[i]))  StateBasedCD.py:35-37
   double alt, vs;         // int.alt[i], int.vs[i]
-  double pad[7];
+  double pad0;
+  double ilat;            // int.lat[i]  (KWIK cavelat, geo.py:355; same offset as ColRec::olat)
+  double pad[5];
 };
 struct alignas(16) ColRec {
   double lat, lon;        // int[j]
@@ -48,7 +50,8 @@ struct alignas(16) ColRec {
   double u, v;            // own.gs[j] * sin/cos(radians(own.trk[j]))  StateBasedCD.py:30-32
   double alt, vs;         // own.alt[j], own.vs[j]
   double eps;             // (own.lat[j] == 0.) * 1e-6                geo.py:128
-  double pad[6];
+  double olat;            // own.lat[j]  (KWIK cavelat, geo.py:355)
+  double pad[5];
 };
 static_assert(sizeof(RowRec) == 128, "RowRec must be one cache line");
 static_assert(sizeof(ColRec) == 128, "ColRec must be one cache line");

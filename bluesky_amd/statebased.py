@@ -34,11 +34,13 @@ def _upload(ctx, ownship, intruder):
 
 
 def detect_indices(ownship, intruder, RPZ, HPZ, tlookahead, with_dcpa=False, ctx=None,
-                   row_begin=0, row_end=-1, noprune=False):
-    """Index-array form: dict(ci, cj, qdr, dist, tcpa, tinconf[, dcpa], li, lj, inconf, tcpamax)."""
+                   row_begin=0, row_end=-1, noprune=False, kwik=False):
+    """Index-array form: dict(ci, cj, qdr, dist, tcpa, tinconf[, dcpa], li, lj, inconf, tcpamax).
+    ``kwik=True``: the opt-in flat-earth variant (``bluesky_amd.kwik``)."""
     ctx = ctx or _lib.default_context()
     _upload(ctx, ownship, intruder)
-    flags = (_lib.FLAG_WITH_DCPA if with_dcpa else 0) | (_lib.FLAG_NOPRUNE if noprune else 0)
+    flags = ((_lib.FLAG_WITH_DCPA if with_dcpa else 0) | (_lib.FLAG_NOPRUNE if noprune else 0) |
+             (_lib.FLAG_KWIK if kwik else 0))
     nc, nl = ctx.detect(RPZ, HPZ, tlookahead, flags, row_begin, row_end)
     return ctx.fetch_pairs(nc, nl, with_dcpa)
 
@@ -59,10 +61,11 @@ def last_detect():
     return _last or None
 
 
-def detect(ownship, intruder, RPZ, HPZ, tlookahead, with_dcpa=False):
+def detect(ownship, intruder, RPZ, HPZ, tlookahead, with_dcpa=False, kwik=False):
     """StateBasedCD.detect drop-in (8-tuple; 9-tuple with ``with_dcpa=True``)."""
     ctx = _lib.default_context()
-    o = detect_indices(ownship, intruder, RPZ, HPZ, tlookahead, with_dcpa=with_dcpa, ctx=ctx)
+    o = detect_indices(ownship, intruder, RPZ, HPZ, tlookahead, with_dcpa=with_dcpa, ctx=ctx,
+                       kwik=kwik)
     ids = np.asarray(ownship.id, dtype=object)
     confpairs = pairs_from_indices(ids, o['ci'], o['cj'])
     lospairs = pairs_from_indices(ids, o['li'], o['lj'])

@@ -41,6 +41,9 @@ typedef struct bsa_ctx bsa_ctx;
 #define BSA_FLAG_NOPRUNE   2 /* test aid: treat every pair as a candidate (disables the exact-safe prefilter) */
 #define BSA_FLAG_RESORT    4 /* recompute the spatial order now (it is otherwise reused for up to
                                 8 calls; results never depend on it, only the speed does) */
+#define BSA_FLAG_KWIK      8 /* opt-in flat-earth variant: geo.kwikqdrdist_matrix
+                                (geo.py:347-363) replaces qdrdist_matrix in StateBasedCD.detect, its
+                                metre distance passed on in nm; qdr in [0, 360) */
 
 /* ---------------------------------------------------------------- lifecycle */
 

@@ -102,7 +102,27 @@ def qdrdist_rows(lat1, lon1, lat2, lon2, rows):
     return qdr, dist
 
 
-def detect_rows(own, intr, RPZ, HPZ, tlookahead, rows, want_dcpa=False):
+RE_KWIK = 6371000.          # geo.py:352
+
+
+def kwikqdrdist_rows(lata, lona, latb, lonb, rows):
+    """``geo.kwikqdrdist_matrix`` (geo.py:347-363) restricted to the rows
+    ``rows``; returns (qdr [deg, 0..360), dist [m]).  Note the transposes as
+    written: ``dlat[i,j] = latb[j] - lata[i]`` but ``cavelat[i,j]`` uses
+    ``lata[j] + latb[i]`` (symmetric only when a == b)."""
+    la = lata[rows][:, None]                                  # lata.T
+    lo = lona[rows][:, None]
+    dlat = np.radians(latb[None, :] - la)                     # geo.py:353
+    dlon = np.radians(lonb[None, :] - lo)                     # geo.py:354
+    cavelat = np.cos(np.radians(lata[None, :] + latb[rows][:, None]) * 0.5)   # geo.py:355
+    dangle = np.sqrt(np.multiply(dlat, dlat) +
+                     np.multiply(np.multiply(dlon, dlon), np.multiply(cavelat, cavelat)))
+    dist = RE_KWIK * dangle
+    qdr = np.degrees(np.arctan2(np.multiply(dlon, cavelat), dlat)) % 360.
+    return qdr, dist
+
+
+def detect_rows(own, intr, RPZ, HPZ, tlookahead, rows, want_dcpa=False, kwik=False):
     """StateBasedCD.detect (StateBasedCD.py:7-103) for the ownship rows ``rows``.
 
     ``own``/``intr`` are mappings (or objects) with numpy fp64 vectors
@@ -115,7 +135,13 @@ def detect_rows(own, intr, RPZ, HPZ, tlookahead, rows, want_dcpa=False):
     rows = np.asarray(rows, dtype=np.int64)
     I = (rows[:, None] == np.arange(n)[None, :]).astype(np.float64)
 
-    qdr, dist = qdrdist_rows(g('lat'), g('lon'), h('lat'), h('lon'), rows)
+    if kwik:
+        # KWIK variant: kwikqdrdist_matrix swapped in for qdrdist_matrix, its
+        # metre distance handed over in nm (bluesky_amd/kwik.py)
+        qdr, dist_m = kwikqdrdist_rows(g('lat'), g('lon'), h('lat'), h('lon'), rows)
+        dist = dist_m / NM
+    else:
+        qdr, dist = qdrdist_rows(g('lat'), g('lon'), h('lat'), h('lon'), rows)
     qdr = np.array(qdr)
     dist = np.array(dist) * NM + 1e9 * I                      # StateBasedCD.py:22
 
@@ -195,15 +221,15 @@ def chunk_rows(n, budget_bytes=2 << 30):
 
 
 def detect_arrays(own, intr, RPZ, HPZ, tlookahead, want_dcpa=False,
-                  rows=None, budget_bytes=2 << 30):
+                  rows=None, budget_bytes=2 << 30, kwik=False):
     """Full (or row-subset) detect as index/value arrays, chunked over rows."""
     n = len(_getter(own)('lat'))
     rows = np.arange(n) if rows is None else np.asarray(rows, dtype=np.int64)
     step = chunk_rows(n, budget_bytes)
     parts = [detect_rows(own, intr, RPZ, HPZ, tlookahead, rows[k:k + step],
-                         want_dcpa) for k in range(0, len(rows), step)]
+                         want_dcpa, kwik) for k in range(0, len(rows), step)]
     if not parts:
-        parts = [detect_rows(own, intr, RPZ, HPZ, tlookahead, rows, want_dcpa)]
+        parts = [detect_rows(own, intr, RPZ, HPZ, tlookahead, rows, want_dcpa, kwik)]
     out = {}
     for key in parts[0]:
         out[key] = np.concatenate([p[key] for p in parts])

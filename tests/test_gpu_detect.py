@@ -10,6 +10,7 @@ from tests import util
 pytestmark = pytest.mark.gpu
 
 CD = util.golden('cd_*.npz')
+KWIK = util.golden('cdkwik_*.npz')
 RPZ, HPZ, TLA = synth.RPZ, synth.HPZ, synth.TLOOKAHEAD
 
 
@@ -126,3 +127,24 @@ def test_detect_overflow_retry_is_exact(ctx):
     got = statebased.detect_indices(t, t, synth.RPZ, synth.HPZ, synth.TLOOKAHEAD, ctx=ctx)
     for k in ('ci', 'cj', 'li', 'lj', 'qdr', 'dist', 'tcpa', 'tinconf', 'inconf', 'tcpamax'):
         assert np.array_equal(np.asarray(got[k]), np.asarray(exp[k])), k
+
+
+@pytest.mark.parametrize('path', KWIK, ids=[util.case_name(p) for p in KWIK])
+def test_kwik_matches_reference_golden(ctx, path):
+    """Opt-in flat-earth variant against the reference's detect with
+    kwikqdrdist_matrix swapped in; pruned run == unpruned run."""
+    own, intr, z = util.load_cd(path)
+    rpz, hpz, tla = float(z['rpz']), float(z['hpz']), float(z['tla'])
+    got = statebased.detect_indices(own, intr, rpz, hpz, tla, ctx=ctx, kwik=True)
+    util.assert_detect_equal(got, z, rpz, tla)
+    full = statebased.detect_indices(own, intr, rpz, hpz, tla, ctx=ctx, kwik=True, noprune=True)
+    for k in got:
+        if got[k] is not None:
+            assert np.array_equal(got[k], full[k]), k
+
+
+def test_kwik_random_box_vs_oracle(ctx):
+    t = synth.box(4000, 300.0, seed=47, lat0=60.0, lon0=20.0)
+    got = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx, kwik=True)
+    exp = ocd.detect_arrays(t, t, RPZ, HPZ, TLA, kwik=True)
+    util.assert_detect_equal(got, exp, RPZ, TLA)

@@ -9,20 +9,21 @@ from bluesky_amd import _lib, kinematics, mvp, resident, statebased, synth
 
 
 def test_register_uses_asas_plugin_api():
-    calls = {}
+    calls = {'cd': [], 'cr': []}
 
     class FakeASAS:
         @classmethod
         def addCDMethod(cls, name, module):
-            calls['cd'] = (name, module)
+            calls['cd'].append((name, module))
 
         @classmethod
         def addCRMethod(cls, name, module):
-            calls['cr'] = (name, module)
+            calls['cr'].append((name, module))
 
     bluesky_amd.register(FakeASAS)
-    assert calls['cd'] == ('GPU', statebased)
-    assert calls['cr'] == ('GPUMVP', mvp)
+    assert calls['cd'] == [('GPU', statebased), ('GPUKWIK', bluesky_amd.kwik)]
+    assert calls['cr'] == [('GPUMVP', mvp)]
+    assert callable(bluesky_amd.kwik.detect)
     assert callable(statebased.detect) and callable(mvp.resolve) and callable(mvp.start)
 
 

@@ -16,10 +16,26 @@ from tests import util
 CD = util.golden('cd_*.npz')
 MVP = util.golden('mvp_*.npz')
 KIN = util.golden('kin_*.npz')
+KWIK = util.golden('cdkwik_*.npz')
 
 
 def test_fixtures_present():
-    assert len(CD) >= 9 and len(MVP) >= 5 and len(KIN) >= 3
+    assert len(CD) >= 9 and len(MVP) >= 5 and len(KIN) >= 3 and len(KWIK) >= 6
+
+
+@pytest.mark.parametrize('path', KWIK, ids=[util.case_name(p) for p in KWIK])
+def test_oracle_kwik_matches_reference(path):
+    """Opt-in KWIK variant: kwikqdrdist_matrix swapped into the reference's detect."""
+    own, intr, z = util.load_cd(path)
+    o = ocd.detect_arrays(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']),
+                          budget_bytes=256 << 20, kwik=True)
+    for k in ('ci', 'cj', 'li', 'lj'):
+        assert np.array_equal(o[k], z[k]), k
+    assert np.array_equal(o['inconf'], z['inconf'])
+    for k, s in (('qdr', 360.0), ('dist', 1e4), ('tcpa', 300.0), ('tinconf', 300.0),
+                 ('tcpamax', 300.0)):
+        ok, msg = util.close(o[k], z[k], s, rtol=1e-12)
+        assert ok, '%s: %s' % (k, msg)
 
 
 @pytest.mark.parametrize('path', CD, ids=[util.case_name(p) for p in CD])

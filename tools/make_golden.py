@@ -10,6 +10,9 @@ and outputs as small ``.npz`` files under ``tests/golden/``:
 * ``mvp_<case>.npz``  -- ``MVP.resolve`` (MVP.py:14-143) for several switch sets
 * ``kin_<case>.npz``  -- ``Traffic.UpdateAirSpeed/GroundSpeed/Position``
                          (traffic.py:425-483)
+* ``cdkwik_<case>.npz`` -- the opt-in KWIK variant: ``StateBasedCD.detect`` with
+                         ``geo.qdrdist_matrix`` swapped for ``geo.kwikqdrdist_matrix``
+                         (geo.py:347-363), its metre distance handed over / nm
 
 It also runs the CPU restatement in ``oracle/`` on the same inputs and
 asserts bit-for-bit equality, so the oracle is pinned at capture time.
@@ -40,6 +43,7 @@ sys.path.insert(0, REF)
 sys.path.insert(0, REPO)
 
 from bluesky.traffic.asas import StateBasedCD, MVP          # noqa: E402
+from bluesky.tools import geo as refgeo                      # noqa: E402
 from bluesky.traffic.traffic import Traffic as RefTraffic    # noqa: E402
 from bluesky.traffic.windsim import WindSim                  # noqa: E402
 from bluesky.tools.aero import ft, nm, kts, fpm              # noqa: E402
@@ -145,6 +149,43 @@ def run_cd(name, own, intr):
     np.savez_compressed(os.path.join(OUT, 'cd_%s.npz' % name), **d)
     print('cd_%-18s N=%5d conf=%6d los=%5d' % (name, own.ntraf, len(ci), len(li)))
     return res
+
+
+def run_kwik(name, own, intr):
+    """KWIK golden: the reference's detect with kwikqdrdist_matrix swapped in."""
+    intr_ = own if intr is None else intr
+    orig = StateBasedCD.geo.qdrdist_matrix
+
+    def kwik_nm(lat1, lon1, lat2, lon2):
+        qdr, dist = refgeo.kwikqdrdist_matrix(lat1, lon1, lat2, lon2)
+        return qdr, dist / nm
+
+    StateBasedCD.geo.qdrdist_matrix = kwik_nm
+    try:
+        res = StateBasedCD.detect(own, intr_, RPZ, HPZ, TLA)
+    finally:
+        StateBasedCD.geo.qdrdist_matrix = orig
+    confpairs, lospairs, inconf, tcpamax, qdr, dist, tcpa, tin = res
+    idmap = {k: i for i, k in enumerate(own.id)}
+    ci, cj = ids_to_idx(confpairs, idmap)
+    li, lj = ids_to_idx(lospairs, idmap)
+    o = ocd.detect_arrays(own, intr_, RPZ, HPZ, TLA, budget_bytes=64 << 20, kwik=True)
+    for k, v in (('ci', ci), ('cj', cj), ('li', li), ('lj', lj),
+                 ('inconf', np.asarray(inconf)), ('tcpamax', np.asarray(tcpamax)),
+                 ('qdr', np.asarray(qdr)), ('dist', np.asarray(dist)),
+                 ('tcpa', np.asarray(tcpa)), ('tinconf', np.asarray(tin))):
+        ok = np.array_equal(o[k], v) if k != 'tcpamax' else np.all(o[k] == v)
+        assert ok, 'oracle != reference for kwik %s/%s' % (name, k)
+    d = dict(lat=own.lat, lon=own.lon, alt=own.alt, trk=own.trk, gs=own.gs, vs=own.vs,
+             same=np.array(intr is None), rpz=RPZ, hpz=HPZ, tla=TLA,
+             ci=ci, cj=cj, li=li, lj=lj, inconf=np.asarray(inconf),
+             tcpamax=np.asarray(tcpamax), qdr=np.asarray(qdr), dist=np.asarray(dist),
+             tcpa=np.asarray(tcpa), tinconf=np.asarray(tin))
+    if intr is not None:
+        d.update(ilat=intr.lat, ilon=intr.lon, ialt=intr.alt, itrk=intr.trk,
+                 igs=intr.gs, ivs=intr.vs)
+    np.savez_compressed(os.path.join(OUT, 'cdkwik_%s.npz' % name), **d)
+    print('cdkwik_%-14s N=%5d conf=%6d los=%5d' % (name, own.ntraf, len(ci), len(li)))
 
 
 # ---------------------------------------------------------------- MVP
@@ -306,9 +347,18 @@ def run_kin(name, n, seed, dt, wind=None):
     print('kin_%-17s N=%5d dt=%g wind=%s' % (name, n, dt, wind))
 
 
+KWIK_CASES = ('box500', 'equator1500', 'antimeridian800', 'polar400', 'edge', 'own_ne_int300')
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     cds = cd_cases()
+    if '--kwik-only' in sys.argv:
+        for name in KWIK_CASES:
+            run_kwik(name, *cds[name])
+        return
+    for name in KWIK_CASES:
+        run_kwik(name, *cds[name])
     results = {}
     for name, (own, intr) in cds.items():
         results[name] = run_cd(name, own, intr)
