@@ -92,7 +92,8 @@ class SimParams(ctypes.Structure):
     """bsa_sim_params (include/bsaccel.h)."""
     _fields_ = [('simdt', ctypes.c_double), ('rpz', ctypes.c_double), ('hpz', ctypes.c_double),
                 ('tla', ctypes.c_double), ('cd_every', ctypes.c_int32), ('reso', ctypes.c_int32),
-                ('mvp', MvpParams)]
+                ('mvp', MvpParams), ('winddim', ctypes.c_int32), ('pad', ctypes.c_int32),
+                ('windnorth', ctypes.c_double), ('windeast', ctypes.c_double)]
 
 
 SIM_STATE_FIELDS = ('lat', 'lon', 'alt', 'tas', 'hdg', 'vs', 'gs', 'trk', 'gseast', 'gsnorth',

@@ -23,6 +23,7 @@ constexpr double kRearth = 6371000.;   // aero.py:28
 constexpr double kFPM = kFT / 60.;     // aero.py:13
 
 __device__ __forceinline__ double npmax(double a, double b) { return (a >= b || a != a) ? a : b; }
+__device__ __forceinline__ double npmin(double a, double b) { return (a <= b || a != a) ? a : b; }
 __device__ __forceinline__ double npsign(double x) {
   return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x));
 }

@@ -43,8 +43,10 @@ struct SimDev {
   unsigned long long *steps_done;  // steps completed in the batch
 };
 
-// Pilot.APorASAS (winddim 0) + UpdateAirSpeed/GroundSpeed/Position, rows [rb, re)
-__global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, SimDev d) {
+// Pilot.APorASAS (pilot.py:28-63; winddim 0 or constant wind) +
+// UpdateAirSpeed/GroundSpeed/Position, rows [rb, re)
+__global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, int winddim, double vwn,
+                                                       double vwe, SimDev d) {
   if (*d.sticky) return;
   const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
@@ -52,10 +54,25 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   const bool act = d.active[k] != 0;
   const double ptrk = act ? d.atrk[k] : d.aptrk[k];   // pilot.py:41
   kin::In s;
-  s.ptas = act ? d.atas[k] : d.aptas[k];              // pilot.py:38,42
+  double asastas = d.atas[k];                         // pilot.py:37-38: no wind, GS = TAS
+  if (winddim > 0) {                                  // pilot.py:31-35: ASAS GS -> TAS
+    const double atas = d.atas[k], atrk = d.atrk[k];
+    const double asastasnorth = atas * cos(atrk * kD2R) - vwn;
+    const double asastaseast = atas * sin(atrk * kD2R) - vwe;
+    asastas = sqrt(asastasnorth * asastasnorth + asastaseast * asastaseast);
+  }
+  s.ptas = act ? asastas : d.aptas[k];                // pilot.py:42
   s.palt = act ? d.aalt[k] : d.apalt[k];              // pilot.py:43
   s.pvs = fabs(act ? d.avs[k] : d.apvs[k]);           // pilot.py:44,48
-  s.phdg = kin::nprem(ptrk, 360.);                    // pilot.py:63
+  if (winddim > 0) {                                  // pilot.py:51-61: wind correction
+    const double Vw = sqrt(vwn * vwn + vwe * vwe);
+    const double winddir = atan2(vwe, vwn);
+    const double drift = ptrk * kD2R - winddir;
+    const double steer = asin(kin::npmin(1.0, kin::npmax(-1.0, Vw * sin(drift) / kin::npmax(0.001, d.tas[k]))));
+    s.phdg = kin::nprem(ptrk + steer * kR2D, 360.);
+  } else {
+    s.phdg = kin::nprem(ptrk, 360.);                  // pilot.py:63
+  }
   s.tas = d.tas[k];
   s.hdg = d.hdg[k];
   s.alt = d.alt[k];
@@ -65,7 +82,7 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   s.bank = d.bank[k];
   s.eps = d.eps[k];
   s.accel = d.accel[k];
-  const kin::Out o = kin::step(s, simdt, 0, 0.0, 0.0);
+  const kin::Out o = kin::step(s, simdt, winddim, vwn, vwe);
   d.tas[k] = o.tas;
   d.hdg[k] = o.hdg;
   d.alt[k] = o.alt;
@@ -342,7 +359,8 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
         if (bsa::sim_cd(c)) return -1;
       const int64_t nb = std::max<int64_t>(1, (re - rb + 255) / 256);
       hipLaunchKernelGGL(bsa::k_sim_pilot_kin, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb, (int)re,
-                         c->simp.simdt, bsa::sim_dev(c));
+                         c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
+                         bsa::sim_dev(c));
       BSA_HIP(c, hipGetLastError());
       c->sim_gathered = c->nranks == 1;
       c->sim_steps++;

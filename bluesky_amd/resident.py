@@ -41,15 +41,18 @@ def initial_state(traf):
 
 def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, reso=True, mar=1.05,
            swresohoriz=True, swresospd=False, swresohdg=False, swresovert=False, swprio=False,
-           priocode='FF1'):
-    """bsa_sim_params; ASAS defaults of asas.py:81-112 with asas_mar from data/default.cfg."""
+           priocode='FF1', wind=None):
+    """bsa_sim_params; ASAS defaults of asas.py:81-112 with asas_mar from data/default.cfg.
+    ``wind=(vnorth, veast)`` [m/s]: constant wind (winddim 1)."""
     mvp = _lib.MvpParams(Rm=rpz * mar, dhm=hpz * mar, dtlookahead=tla, vmin=200.0 * NM / 3600.,
                          vmax=500.0 * NM / 3600., vsmin=-3000. / 60. * FT, vsmax=3000. / 60. * FT,
                          swresohoriz=int(swresohoriz), swresospd=int(swresospd),
                          swresohdg=int(swresohdg), swresovert=int(swresovert), swprio=int(swprio),
                          priocode=_lib.PRIO_CODES.get(priocode, 0), swnoreso=0, swresooff=0)
+    wn, we = (0.0, 0.0) if wind is None else (float(wind[0]), float(wind[1]))
     return _lib.SimParams(simdt=simdt, rpz=rpz, hpz=hpz, tla=tla, cd_every=int(cd_every),
-                          reso=int(bool(reso)), mvp=mvp)
+                          reso=int(bool(reso)), mvp=mvp, winddim=0 if wind is None else 1, pad=0,
+                          windnorth=wn, windeast=we)
 
 
 class ResidentSim:

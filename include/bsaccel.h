@@ -211,7 +211,7 @@ int bsa_comm_allreduce_sum(bsa_ctx *ctx, double *values, int count);
  *   every cd_every steps: [all-gather] -> detect (own rows) -> MVP (own rows,
  *                         only if any rank has a conflict, asas.py:486-487)
  *                         -> asas.active = inconf
- *   every step:           Pilot.APorASAS (no wind, pilot.py:41-63) fused with
+ *   every step:           Pilot.APorASAS (pilot.py:28-63, winddim 0/1) fused with
  *                         UpdateAirSpeed/GroundSpeed/Position (traffic.py:425-483)
  * AP targets, selalt, bank, eps and perf.acceleration() are frozen inputs. */
 typedef struct bsa_sim_params {
@@ -219,6 +219,10 @@ typedef struct bsa_sim_params {
   int32_t cd_every; /* >= 1: CD + MVP every k steps (1 = DTNOLOOK=simdt, 20 = asas_dt/simdt) */
   int32_t reso;     /* 1: MVP resolution + asas.active = inconf; 0: CD only (RESO OFF) */
   bsa_mvp_params mvp;
+  int32_t winddim;  /* 0 = no wind, 1 = constant wind (windfield.py:150-152): the wind branches
+                       of Pilot.APorASAS (pilot.py:31-36,51-61) and UpdateGroundSpeed */
+  int32_t pad;
+  double windnorth, windeast; /* [m/s] */
 } bsa_sim_params;
 
 typedef struct bsa_sim_state {

@@ -5,7 +5,8 @@ TEST INFRASTRUCTURE ONLY (see ``oracle/__init__.py``).
 Order of Traffic.update (bluesky/traffic/traffic.py:383-409) restricted to
 the hot path: asas.update (asas.py:473-504: detect, then MVP.resolve only if
 confpairs is non-empty) every ``cd_every`` steps with ``asas.active =
-inconf``; Pilot.APorASAS without wind (pilot.py:28-63); UpdateAirSpeed /
+inconf``; Pilot.APorASAS (pilot.py:28-63) without wind or with a constant
+wind (``p['wind'] = (vnorth, veast)``, windfield.py:150-152); UpdateAirSpeed /
 UpdateGroundSpeed / UpdatePosition (traffic.py:425-483).
 """
 import numpy as np
@@ -35,15 +36,34 @@ def sim_step(st, p, do_cd):
                 st['asas_alt'] = o['alt']
             st['active'] = np.asarray(r['inconf'], dtype=bool)
     act = st['active']
+    wind = p.get('wind')
+    if wind is not None:                                      # pilot.py:31-35
+        vwn, vwe = np.full(n, wind[0]), np.full(n, wind[1])
+        asastasnorth = st['asas_tas'] * np.cos(np.radians(st['asas_trk'])) - vwn
+        asastaseast = st['asas_tas'] * np.sin(np.radians(st['asas_trk'])) - vwe
+        asastas = np.sqrt(asastasnorth**2 + asastaseast**2)
+    else:
+        asastas = st['asas_tas']
     ptrk = np.where(act, st['asas_trk'], st['ap_trk'])
-    ptas = np.where(act, st['asas_tas'], st['ap_tas'])
+    ptas = np.where(act, asastas, st['ap_tas'])
     palt = np.where(act, st['asas_alt'], st['ap_alt'])
     pvs = np.abs(np.where(act, st['asas_vs'], st['ap_vs']))
-    phdg = ptrk % 360.
+    if wind is not None:                                      # pilot.py:51-61
+        Vw = np.sqrt(vwn * vwn + vwe * vwe)
+        winddir = np.arctan2(vwe, vwn)
+        drift = np.radians(ptrk) - winddir
+        steer = np.arcsin(np.minimum(1.0, np.maximum(-1.0, Vw * np.sin(drift) /
+                                                     np.maximum(0.001, st['tas']))))
+        phdg = (ptrk + np.degrees(steer)) % 360.
+    else:
+        phdg = ptrk % 360.
     s = dict(tas=st['tas'], hdg=st['hdg'], alt=st['alt'], vs=st['vs'], lat=st['lat'], lon=st['lon'],
              ptas=ptas, phdg=phdg, palt=palt, pvs=pvs, bank=st['bank'], eps=st['eps'],
              accel=st['accel'])
-    o = okin.step(s, p['simdt'])
+    if wind is not None:
+        o = okin.step(s, p['simdt'], winddim=1, windnorth=wind[0], windeast=wind[1])
+    else:
+        o = okin.step(s, p['simdt'])
     for k in ('tas', 'hdg', 'alt', 'vs', 'lat', 'lon', 'gs', 'trk', 'gseast', 'gsnorth'):
         st[k] = np.asarray(o[k], dtype=np.float64)
     assert len(st['lat']) == n

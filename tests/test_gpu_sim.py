@@ -21,6 +21,7 @@ SCALES = dict(lat=90.0, lon=180.0, alt=1e4, tas=300.0, hdg=360.0, vs=20.0, gs=30
 
 def oracle_params(p, reso=True):
     return dict(simdt=p.simdt, rpz=p.rpz, hpz=p.hpz, tla=p.tla, reso=reso,
+                wind=(p.windnorth, p.windeast) if p.winddim else None,
                 mvp=omvp.params_from_settings(p.rpz, p.hpz, p.tla, p.mvp.Rm / p.rpz,
                                               bool(p.mvp.swresohoriz), bool(p.mvp.swresospd),
                                               bool(p.mvp.swresohdg), bool(p.mvp.swresovert)))
@@ -40,11 +41,13 @@ def compare(got, exp, step):
     assert np.array_equal(got['active'], exp['active']), 'step %d active' % step
 
 
-@pytest.mark.parametrize('cd_every,steps,hv', [(1, 4, False), (3, 7, False), (1, 3, True)])
-def test_resident_steps_match_oracle(ctx, cd_every, steps, hv):
+@pytest.mark.parametrize('cd_every,steps,hv,wind', [(1, 4, False, None), (3, 7, False, None),
+                                                    (1, 3, True, None), (1, 4, False, (-7.5, 12.0)),
+                                                    (2, 5, True, (3.0, -20.0))])
+def test_resident_steps_match_oracle(ctx, cd_every, steps, hv, wind):
     t = synth.box(1500, 60.0, seed=23)
     init = resident.initial_state(t)
-    p = resident.params(cd_every=cd_every, swresohoriz=not hv)
+    p = resident.params(cd_every=cd_every, swresohoriz=not hv, wind=wind)
     sim = resident.ResidentSim(init, p, ctx=ctx)
     op = oracle_params(p)
     prev = dict(init)
