@@ -92,7 +92,7 @@ class SimParams(ctypes.Structure):
     """bsa_sim_params (include/bsaccel.h)."""
     _fields_ = [('simdt', ctypes.c_double), ('rpz', ctypes.c_double), ('hpz', ctypes.c_double),
                 ('tla', ctypes.c_double), ('cd_every', ctypes.c_int32), ('reso', ctypes.c_int32),
-                ('mvp', MvpParams), ('winddim', ctypes.c_int32), ('pad', ctypes.c_int32),
+                ('mvp', MvpParams), ('winddim', ctypes.c_int32), ('resume_nav', ctypes.c_int32),
                 ('windnorth', ctypes.c_double), ('windeast', ctypes.c_double)]
 
 
@@ -123,6 +123,8 @@ SIGNATURES.update({
     'bsa_sim_step': (ctypes.c_int, [_vp, ctypes.c_int]),
     'bsa_sim_read': (ctypes.c_int, [_vp, ctypes.POINTER(SimOut)]),
     'bsa_sim_stats': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_sim_asas_stats': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_sim_resopairs': (ctypes.c_int, [_vp, _c_i32p, _c_i32p, ctypes.c_int64, _c_i64p]),
 })
 
 UNIQUE_ID_BYTES = 128
@@ -352,6 +354,26 @@ class Context:
         self.check(self.lib.bsa_sim_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_stats')
         return dict(steps=int(v[0]), cd_calls=int(v[1]), n_conf=int(v[2]), n_los=int(v[3]),
                     row_begin=int(v[4]), row_end=int(v[5]))
+
+    def sim_asas_stats(self):
+        """ASAS bookkeeping counts after the last CD call (resume_nav on); the
+        unique / cumulative counts are None with several ranks."""
+        v = np.zeros(6, np.int64)
+        self.check(self.lib.bsa_sim_asas_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_asas_stats')
+        opt = lambda x: None if x < 0 else int(x)
+        return dict(resopairs=int(v[0]), confpairs_unique=opt(v[1]), lospairs_unique=opt(v[2]),
+                    confpairs_all=opt(v[3]), lospairs_all=opt(v[4]), active=int(v[5]))
+
+    def sim_resopairs(self):
+        """This rank's resopairs as (idx1, idx2) int32 arrays, idx1-major."""
+        cnt = np.zeros(1, np.int64)
+        a = b = np.empty(0, np.int32)
+        while True:
+            self.check(self.lib.bsa_sim_resopairs(self.h, ptr(a, _c_i32p), ptr(b, _c_i32p), len(a),
+                                                  ptr(cnt, _c_i64p)), 'bsa_sim_resopairs')
+            if cnt[0] <= len(a):
+                return a[:cnt[0]], b[:cnt[0]]
+            a, b = np.empty(int(cnt[0]), np.int32), np.empty(int(cnt[0]), np.int32)
 
     # ---------------------------------------------------------------- kinematics
     KIN_OUT =('ax', 'delspd', 'cas', 'mach', 'gsnorth', 'gseast', 'gs', 'trk', 'coslat', 'az')

@@ -1,0 +1,348 @@
+// ASAS.update bookkeeping and ResumeNav on the device (asas.py:409-504) for
+// the resident sim step, opt-in (bsa_sim_params.resume_nav).
+//
+// resopairs is kept as CSR over the rank's own rows (row = idx1 - rb, sorted
+// idx2 per row).  Per CD call, after K3:
+//   before MVP (bk_count; MVP changes none of the state these read):
+//   k_bk_count   one lane per row: merge the row's resopairs with the row's
+//                new confpairs (K2 output, sorted), evaluate ResumeNav's
+//                past-CPA / horizontal-LoS / bouncing test per pair
+//                (asas.py:424-452), count the kept pairs
+//   scan         kept counts -> next CSR
+//   k_bk_check   next CSR larger than its buffer -> gate bit 1: the step
+//                aborts before MVP touches asas state (all ranks, through the
+//                gate all-reduce); the host grows the buffer and retries
+//   after MVP (bk_apply):
+//   k_bk_write   same merge + test, write the kept pairs and asas.active
+//                (true iff any of the row's pairs is kept; rows without
+//                resopairs keep their value, as in the reference)
+//   k_bk_unique  (one rank) |confpairs_unique|, |lospairs_unique| and the
+//                growth of confpairs_all / lospairs_all (asas.py:494-502):
+//                pair (i, j) is the representative of {i, j} when i < j or
+//                (j, i) is not a pair; it is new when neither (i, j) nor
+//                (j, i) was a pair of the previous call
+//   k_bk_commit  copy the next CSR and this call's pair lists over the
+//                persistent ones
+// Every kernel is a no-op once the step batch is aborted (sticky flag), so a
+// retried step finds the bookkeeping as it was at the step's start.  The
+// reference iterates a Python set in ResumeNav, so an aircraft whose pairs
+// disagree ends with whichever pair its hash order visits last; the device
+// (and oracle/asas.py) use "active iff any kept pair" (DESIGN.md 3.8).
+#include <hipcub/hipcub.hpp>
+
+#include "bsa_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace bsa {
+
+struct BkIn {
+  int rb, nrows;
+  const unsigned *rptr;    // resopairs CSR (persistent), nrows + 1
+  const unsigned *rcol;
+  const unsigned *cptr;    // this call's conflict rows: K2 row offsets, nrows + 1
+  const int *ccol;         // K2 cj (original column index, ascending per row)
+  const double *lat, *lon, *gse, *gsn, *trk;  // full-N state
+  double R, Rm;
+  const unsigned long long *gate;
+  const unsigned *sticky;
+  unsigned *cnt;           // kept per row (count pass)
+  const unsigned *nptr;    // next CSR pointers (write pass)
+  unsigned *ncol;
+  uint8_t *active;         // full-N
+  unsigned long long *stats;
+};
+
+__device__ __forceinline__ bool bk_aborted(const unsigned long long *gate, const unsigned *sticky) {
+  return sticky[0] != 0 || gate[0] != 0;
+}
+
+// ResumeNav's decision for resopair (i, j), asas.py:424-452
+__device__ __forceinline__ bool bk_keep(const BkIn &in, int i, int j) {
+  const double re = 6371000.;
+  const double d0 = re * (((in.lon[j] - in.lon[i]) * kD2R) * cos(0.5 * ((in.lat[j] + in.lat[i]) * kD2R)));
+  const double d1 = re * ((in.lat[j] - in.lat[i]) * kD2R);
+  const double v0 = in.gse[j] - in.gse[i], v1 = in.gsn[j] - in.gsn[i];
+  const bool past_cpa = d0 * v0 + d1 * v1 > 0.0;
+  const double hdist = sqrt(d0 * d0 + d1 * d1);
+  const bool hor_los = hdist < in.R;
+  const bool bouncing = fabs(in.trk[i] - in.trk[j]) < 30.0 && hdist < in.Rm;
+  return !past_cpa || hor_los || bouncing;
+}
+
+// walk the sorted union of row r's resopairs and new confpairs
+template <typename F>
+__device__ __forceinline__ void bk_merge(const BkIn &in, int r, F f) {
+  unsigned a = in.rptr[r], ae = in.rptr[r + 1];
+  unsigned b = in.cptr[r], be = in.cptr[r + 1];
+  while (a < ae || b < be) {
+    unsigned j;
+    if (b >= be || (a < ae && in.rcol[a] < (unsigned)in.ccol[b])) {
+      j = in.rcol[a++];
+    } else if (a >= ae || (unsigned)in.ccol[b] < in.rcol[a]) {
+      j = (unsigned)in.ccol[b++];
+    } else {  // in both
+      j = in.rcol[a++];
+      ++b;
+    }
+    f(j);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bk_count(BkIn in) {
+  if (bk_aborted(in.gate, in.sticky)) return;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > in.nrows) return;
+  unsigned kept = 0;
+  if (r < in.nrows) {
+    const int i = in.rb + r;
+    bk_merge(in, r, [&](unsigned j) { kept += bk_keep(in, i, (int)j) ? 1u : 0u; });
+  }
+  in.cnt[r] = kept;  // cnt[nrows] = 0: the exclusive scan's last entry is the total
+}
+
+__global__ void k_bk_check(int nrows, const unsigned *nptr, unsigned long long ncap, unsigned long long *gate,
+                           const unsigned *sticky, unsigned long long *demand) {
+  if (bk_aborted(gate, sticky)) return;
+  const unsigned long long total = nptr[nrows];
+  if (total > ncap) {
+    gate[0] = 2;
+    *demand = total > *demand ? total : *demand;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bk_write(BkIn in) {
+  if (bk_aborted(in.gate, in.sticky)) return;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r == 0) {
+    in.stats[0] = in.nptr[in.nrows];
+    in.stats[1] = 0;  // per-call unique counts (k_bk_unique adds)
+    in.stats[2] = 0;
+  }
+  if (r >= in.nrows) return;
+  const int i = in.rb + r;
+  unsigned pos = in.nptr[r];
+  bool any = false, seen = false;
+  bk_merge(in, r, [&](unsigned j) {
+    seen = true;
+    if (bk_keep(in, i, (int)j)) {
+      in.ncol[pos++] = j;
+      any = true;
+    }
+  });
+  if (seen) in.active[i] = any ? 1 : 0;
+}
+
+// is (r, c) in the CSR (ptr over rows 0.., ascending cols)?
+__device__ __forceinline__ bool csr_has(const unsigned *ptr, const int *col, int r, int c) {
+  const unsigned e = ptr[r + 1];
+  unsigned lo = ptr[r], hi = e;
+  while (lo < hi) {
+    const unsigned mid = (lo + hi) >> 1;
+    if (col[mid] < c) lo = mid + 1; else hi = mid;
+  }
+  return lo < e && col[lo] == c;
+}
+
+struct BkUniq {
+  const int *ci, *cj;         // this call's pairs (row-major)
+  const unsigned *ptr;        // this call's row offsets (conf: rowoff; los: lptr)
+  const unsigned *np;         // device pair count
+  const unsigned *pptr;       // previous call's CSR
+  const int *pcol;
+  unsigned long long *uniq, *all;
+};
+
+__global__ __launch_bounds__(256) void k_bk_unique(BkUniq u, const unsigned long long *gate, const unsigned *sticky) {
+  if (bk_aborted(gate, sticky)) return;
+  const unsigned P = *u.np;
+  const unsigned lane = threadIdx.x & 63;
+  for (unsigned x = blockIdx.x * blockDim.x + threadIdx.x; x - lane < P; x += gridDim.x * blockDim.x) {
+    bool rep = false, fresh = false;
+    if (x < P) {
+      const int i = u.ci[x], j = u.cj[x];
+      rep = i < j || !csr_has(u.ptr, u.cj, j, i);
+      if (rep) fresh = !(csr_has(u.pptr, u.pcol, i, j) || csr_has(u.pptr, u.pcol, j, i));
+    }
+    const unsigned long long mr = __ballot(rep), mf = __ballot(fresh);
+    if (lane == 0) {
+      if (mr) atomicAdd(u.uniq, (unsigned long long)__popcll(mr));
+      if (mf) atomicAdd(u.all, (unsigned long long)__popcll(mf));
+    }
+  }
+}
+
+// LoS row pointers from K2's offsets: lptr[r] = rowoff[nrows + 1 + r] - P
+__global__ __launch_bounds__(256) void k_bk_lptr(int nrows, const unsigned *rowoff, unsigned *lptr,
+                                                 const unsigned long long *gate, const unsigned *sticky) {
+  if (bk_aborted(gate, sticky)) return;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r <= nrows) lptr[r] = rowoff[nrows + 1 + r] - rowoff[nrows];
+}
+
+// next CSR -> persistent; this call's pair CSRs -> "previous"
+struct BkCommit {
+  int nrows;
+  const unsigned *nptr, *ncol;
+  unsigned *rptr, *rcol;
+  const unsigned *cptr, *lptr;   // this call (conf rowoff, los pointers)
+  const int *ccol, *lcol;
+  unsigned *pcptr, *plptr;
+  int *pccol, *plcol;
+  int uniq;                      // keep the previous-call lists (one rank)
+};
+
+__global__ __launch_bounds__(256) void k_bk_commit(BkCommit m, const unsigned long long *gate,
+                                                   const unsigned *sticky) {
+  if (bk_aborted(gate, sticky)) return;
+  const unsigned R = m.nptr[m.nrows];
+  const unsigned P = m.uniq ? m.cptr[m.nrows] : 0u, L = m.uniq ? m.lptr[m.nrows] : 0u;
+  const unsigned stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  for (unsigned k = t0; k <= (unsigned)m.nrows; k += stride) {
+    m.rptr[k] = m.nptr[k];
+    if (m.uniq) {
+      m.pcptr[k] = m.cptr[k];
+      m.plptr[k] = m.lptr[k];
+    }
+  }
+  for (unsigned k = t0; k < R; k += stride) m.rcol[k] = m.ncol[k];
+  for (unsigned k = t0; k < P; k += stride) m.pccol[k] = m.ccol[k];
+  for (unsigned k = t0; k < L; k += stride) m.plcol[k] = m.lcol[k];
+}
+
+static BkIn bk_in(Ctx *c, const BkDev &d) {
+  BkIn in;
+  in.rb = (int)c->last_rb;
+  in.nrows = (int)(c->last_re - c->last_rb);
+  in.rptr = (const unsigned *)c->bk_rptr.p;
+  in.rcol = (const unsigned *)c->bk_rcol.p;
+  in.cptr = (const unsigned *)c->rowoff.p;
+  in.ccol = (const int *)c->out_cj.p;
+  in.lat = d.lat;
+  in.lon = d.lon;
+  in.gse = d.gse;
+  in.gsn = d.gsn;
+  in.trk = d.trk;
+  in.R = c->simp.rpz;        // asas.R
+  in.Rm = c->simp.mvp.Rm;    // asas.R * asas.mar (MVP.py:24)
+  in.gate = d.gate;
+  in.sticky = d.sticky;
+  in.cnt = (unsigned *)c->bk_cnt.p;
+  in.nptr = (const unsigned *)c->bk_nptr.p;
+  in.ncol = (unsigned *)c->bk_ncol.p;
+  in.active = d.active;
+  in.stats = (unsigned long long *)c->bk_stats.p;
+  return in;
+}
+
+// capacity of the resopairs CSR (an overflow aborts the step and regrows)
+static unsigned long long bk_ncap(Ctx *c) { return c->bk_cap; }
+
+int bk_count(Ctx *c, const BkDev &d) {
+  const int64_t nrows = c->last_re - c->last_rb, n = c->n;
+  if (nrows <= 0) return 0;
+  if (c->bk_cap == 0) c->bk_cap = std::max<unsigned long long>(c->cand_cap, 1 << 16);
+  const unsigned long long ncap = bk_ncap(c);
+  const size_t lcap = (size_t)std::max(c->cand_cap, c->los_cap) * 4;
+  if (!ensure_keep(c, c->bk_rptr, (size_t)(nrows + 1) * 4, "resopairs rows") ||
+      !ensure_keep(c, c->bk_rcol, (size_t)ncap * 4, "resopairs") ||
+      !ensure(c, c->bk_nptr, (size_t)(nrows + 1) * 4, "resopairs next rows") ||
+      !ensure(c, c->bk_ncol, (size_t)ncap * 4, "resopairs next") ||
+      !ensure(c, c->bk_cnt, (size_t)(nrows + 1) * 4, "resopairs counts") ||
+      !ensure(c, c->bk_lptr, (size_t)(nrows + 1) * 4, "los rows") ||
+      !ensure_keep(c, c->bk_pcptr, (size_t)(n + 1) * 4, "previous conflict rows") ||
+      !ensure_keep(c, c->bk_plptr, (size_t)(n + 1) * 4, "previous los rows") ||
+      !ensure_keep(c, c->bk_pccol, (size_t)c->cand_cap * 4, "previous conflicts") ||
+      !ensure_keep(c, c->bk_plcol, lcap, "previous los") ||
+      !ensure_keep(c, c->bk_stats, 8 * 8, "bookkeeping stats"))
+    return -1;
+  if (!c->bk_ready) {  // empty sets
+    BSA_HIP(c, hipMemsetAsync(c->bk_rptr.p, 0, (size_t)(nrows + 1) * 4, c->stream));
+    BSA_HIP(c, hipMemsetAsync(c->bk_pcptr.p, 0, (size_t)(n + 1) * 4, c->stream));
+    BSA_HIP(c, hipMemsetAsync(c->bk_plptr.p, 0, (size_t)(n + 1) * 4, c->stream));
+    BSA_HIP(c, hipMemsetAsync(c->bk_stats.p, 0, 8 * 8, c->stream));
+    c->bk_ready = true;
+  }
+  const BkIn in = bk_in(c, d);
+  hipLaunchKernelGGL(k_bk_count, dim3((unsigned)((nrows + 1 + 255) / 256)), dim3(256), 0, c->stream, in);
+  BSA_HIP(c, hipGetLastError());
+  size_t tmp = 0;
+  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (const unsigned *)c->bk_cnt.p,
+                                              (unsigned *)c->bk_nptr.p, (int)(nrows + 1), c->stream));
+  if (!ensure(c, c->bk_tmp, std::max<size_t>(tmp, 16), "bookkeeping scan scratch")) return -1;
+  tmp = c->bk_tmp.bytes;
+  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->bk_tmp.p, tmp, (const unsigned *)c->bk_cnt.p,
+                                              (unsigned *)c->bk_nptr.p, (int)(nrows + 1), c->stream));
+  hipLaunchKernelGGL(k_bk_check, dim3(1), dim3(1), 0, c->stream, (int)nrows, (const unsigned *)c->bk_nptr.p,
+                     ncap, d.gate, (const unsigned *)d.sticky, d.demand);
+  BSA_HIP(c, hipGetLastError());
+  return 0;
+}
+
+int bk_apply(Ctx *c, const BkDev &d) {
+  const int64_t nrows = c->last_re - c->last_rb;
+  if (nrows <= 0) return 0;
+  const bool uniq = c->nranks == 1;
+  const BkIn in = bk_in(c, d);
+  const unsigned nb = (unsigned)((nrows + 255) / 256);
+  hipLaunchKernelGGL(k_bk_write, dim3(nb), dim3(256), 0, c->stream, in);
+  BSA_HIP(c, hipGetLastError());
+  hipLaunchKernelGGL(k_bk_lptr, dim3((unsigned)((nrows + 1 + 255) / 256)), dim3(256), 0, c->stream,
+                     (int)nrows, (const unsigned *)c->rowoff.p, (unsigned *)c->bk_lptr.p, d.gate,
+                     (const unsigned *)d.sticky);
+  BSA_HIP(c, hipGetLastError());
+  unsigned long long *st = (unsigned long long *)c->bk_stats.p;
+  if (uniq) {
+    BkUniq u;
+    u.ci = (const int *)c->out_ci.p;
+    u.cj = (const int *)c->out_cj.p;
+    u.ptr = (const unsigned *)c->rowoff.p;
+    u.np = (const unsigned *)c->rowoff.p + nrows;
+    u.pptr = (const unsigned *)c->bk_pcptr.p;
+    u.pcol = (const int *)c->bk_pccol.p;
+    u.uniq = st + 1;
+    u.all = st + 3;
+    hipLaunchKernelGGL(k_bk_unique, dim3(256), dim3(256), 0, c->stream, u, (const unsigned long long *)d.gate,
+                       (const unsigned *)d.sticky);
+    u.ci = (const int *)c->out_li.p;
+    u.cj = (const int *)c->out_lj.p;
+    u.ptr = (const unsigned *)c->bk_lptr.p;
+    u.np = (const unsigned *)c->bk_lptr.p + nrows;
+    u.pptr = (const unsigned *)c->bk_plptr.p;
+    u.pcol = (const int *)c->bk_plcol.p;
+    u.uniq = st + 2;
+    u.all = st + 4;
+    hipLaunchKernelGGL(k_bk_unique, dim3(256), dim3(256), 0, c->stream, u, (const unsigned long long *)d.gate,
+                       (const unsigned *)d.sticky);
+    BSA_HIP(c, hipGetLastError());
+  }
+  BkCommit m;
+  m.nrows = (int)nrows;
+  m.nptr = (const unsigned *)c->bk_nptr.p;
+  m.ncol = (const unsigned *)c->bk_ncol.p;
+  m.rptr = (unsigned *)c->bk_rptr.p;
+  m.rcol = (unsigned *)c->bk_rcol.p;
+  m.cptr = (const unsigned *)c->rowoff.p;
+  m.lptr = (const unsigned *)c->bk_lptr.p;
+  m.ccol = (const int *)c->out_cj.p;
+  m.lcol = (const int *)c->out_lj.p;
+  m.pcptr = (unsigned *)c->bk_pcptr.p;
+  m.plptr = (unsigned *)c->bk_plptr.p;
+  m.pccol = (int *)c->bk_pccol.p;
+  m.plcol = (int *)c->bk_plcol.p;
+  m.uniq = uniq ? 1 : 0;
+  hipLaunchKernelGGL(k_bk_commit, dim3(512), dim3(256), 0, c->stream, m, (const unsigned long long *)d.gate,
+                     (const unsigned *)d.sticky);
+  BSA_HIP(c, hipGetLastError());
+  return 0;
+}
+
+void bk_release(Ctx *c) {
+  DevBuf *all[] = {&c->bk_rptr, &c->bk_rcol, &c->bk_nptr, &c->bk_ncol, &c->bk_cnt, &c->bk_lptr,
+                   &c->bk_pcptr, &c->bk_plptr, &c->bk_pccol, &c->bk_plcol, &c->bk_stats, &c->bk_tmp};
+  for (auto *b : all) release(*b);
+  c->bk_ready = false;
+  c->bk_cap = 0;
+}
+
+}  // namespace bsa

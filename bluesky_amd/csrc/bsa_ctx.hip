@@ -45,6 +45,26 @@ bool ensure(Ctx *c, DevBuf &b, size_t bytes, const char *what) {
   return true;
 }
 
+// like ensure, but a grown buffer keeps its contents (persistent device state)
+bool ensure_keep(Ctx *c, DevBuf &b, size_t bytes, const char *what) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return true;
+  DevBuf nb;
+  if (!ensure(c, nb, bytes, what)) return false;
+  if (b.p) {
+    hipError_t e = hipMemcpyAsync(nb.p, b.p, b.bytes, hipMemcpyDeviceToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      fail(c, "copy on growth of %s: %s", what, hipGetErrorString(e));
+      release(nb);
+      return false;
+    }
+    release(b);
+  }
+  b = nb;
+  return true;
+}
+
 void release(DevBuf &b) {
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
@@ -226,6 +246,7 @@ int bsa_set_candidate_capacity(bsa_ctx *c, int64_t capacity) {
   if (capacity < 1) return bsa::fail(c, "candidate capacity must be >= 1");
   const unsigned long long s = bsa::kCandShards;
   c->cand_cap = ((unsigned long long)capacity + s - 1) / s * s;
+  if (c->bk_cap) c->bk_cap = (unsigned long long)capacity;  // resident-sim resopairs (grows the same way)
   return 0;
 }
 

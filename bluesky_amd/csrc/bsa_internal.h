@@ -113,6 +113,7 @@ struct DevBuf {
 
 struct Ctx;
 bool ensure(Ctx *c, DevBuf &b, size_t bytes, const char *what);
+bool ensure_keep(Ctx *c, DevBuf &b, size_t bytes, const char *what);  // grows, keeps contents
 void release(DevBuf &b);
 
 struct Ctx {
@@ -181,7 +182,15 @@ struct Ctx {
   DevBuf s_aptrk, s_aptas, s_apalt, s_apvs, s_selalt, s_bank, s_eps, s_accel;  // frozen
   DevBuf s_atrk, s_atas, s_avs, s_aalt, s_ase, s_asn, s_active;  // ASAS (full n)
   DevBuf g_send, g_recv;                                    // all-gather staging
-  DevBuf sim_ctl;  // [0,16) gate {overflow, P}; [16,20) sticky abort; [24,32) steps done
+  DevBuf sim_ctl;  // [0,16) gate {overflow, P}; [16,20) sticky abort; [24,32) steps done;
+                   // [32,40) resopairs demand on a bookkeeping overflow
+  // ASAS bookkeeping (bsa_asas.hip, resume_nav = 1): resopairs CSR over own
+  // rows (+ next), per-row kept counts, LoS row pointers of the last call,
+  // previous call's conflict / LoS CSR (one rank), stats
+  DevBuf bk_rptr, bk_rcol, bk_nptr, bk_ncol, bk_cnt, bk_lptr, bk_pcptr, bk_plptr, bk_pccol, bk_plcol;
+  DevBuf bk_stats, bk_tmp;
+  unsigned long long bk_cap = 0;  // resopairs capacity (pairs)
+  bool bk_ready = false;
 };
 
 // device pointers for the MVP kernel (full-N traffic arrays, per-row outputs)
@@ -204,6 +213,20 @@ struct KinDev {
   uint8_t *swhdgsel, *swaltsel;
 };
 int kin_device(Ctx *c, int64_t n, double simdt, int winddim, double vn, double ve, const KinDev &d);
+
+// ASAS bookkeeping of one CD call (bsa_asas.hip): bk_count before the gate
+// all-reduce and MVP (may raise the gate's bit 1 on resopairs overflow),
+// bk_apply after MVP.  State arrays are full-N device arrays.
+struct BkDev {
+  const double *lat, *lon, *gse, *gsn, *trk;
+  uint8_t *active;
+  unsigned long long *gate;
+  unsigned *sticky;
+  unsigned long long *demand;
+};
+int bk_count(Ctx *c, const BkDev &d);
+int bk_apply(Ctx *c, const BkDev &d);
+void bk_release(Ctx *c);
 
 // error helpers
 int fail(Ctx *c, const char *fmt, ...);

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_mvp_row(int rb, bsa_mvp_params p, MvpIn
     const bool abort = in.sticky[0] != 0 || in.gate[0] != 0;
     if (r == 0 && in.gate[0] != 0) in.sticky[0] = 1u;
     if (abort || r >= in.nrows || !in.resolve) return;  // RESO off: asas stays inactive
-    in.active[rb + r] = in.inconf[r];  // build-defined stand-in for ResumeNav
+    if (in.inconf) in.active[rb + r] = in.inconf[r];  // stand-in for ResumeNav unless resume_nav
     // asas.py:486-487: resolve only if confpairs is non-empty (over all ranks)
     if (in.gate[1] == 0) return;
   } else if (r >= in.nrows) {

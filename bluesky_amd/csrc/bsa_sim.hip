@@ -208,6 +208,7 @@ void sim_release(Ctx *c) {
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
                    &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl};
   for (auto *b : all) release(*b);
+  bk_release(c);
   if (c->comm) {
     ncclCommDestroy((ncclComm_t)c->comm);
     c->comm = nullptr;
@@ -221,6 +222,19 @@ static int sim_cd(Ctx *c) {
   unsigned long long *gate = (unsigned long long *)c->sim_ctl.p;
   if (detect_enqueue(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, gate)) return -1;
   c->sim_cd_calls++;
+  unsigned *sticky = (unsigned *)((char *)c->sim_ctl.p + 16);
+  BkDev bk;
+  bk.lat = (const double *)c->own[0].p;
+  bk.lon = (const double *)c->own[1].p;
+  bk.gse = (const double *)c->s_gse.p;
+  bk.gsn = (const double *)c->s_gsn.p;
+  bk.trk = (const double *)c->own[2].p;
+  bk.active = (uint8_t *)c->s_active.p;
+  bk.gate = gate;
+  bk.sticky = sticky;
+  bk.demand = (unsigned long long *)((char *)c->sim_ctl.p + 32);
+  // ASAS bookkeeping, first half: kept-pair counts (may flag a resopairs overflow in the gate)
+  if (p.resume_nav && bk_count(c, bk)) return -1;
   if (c->comm && c->nranks > 1)
     BSA_NCCL(c, ncclAllReduce(gate, gate, 2, ncclUint64, ncclMax, (ncclComm_t)c->comm, c->stream));
   const int64_t rb = c->sim_rb;
@@ -242,9 +256,12 @@ static int sim_cd(Ctx *c) {
   d.o_asase = (float *)c->s_ase.p + rb;
   d.o_asasn = (float *)c->s_asn.p + rb;
   d.o_tsolv = nullptr;
-  // K3 (+ gate, + asas.active = inconf) on the detect's own row offsets
-  return mvp_device(c, p.mvp, d, (const unsigned *)c->rowoff.p, gate, (unsigned *)((char *)c->sim_ctl.p + 16),
-                    (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p, p.reso != 0);
+  // K3 (+ gate, + asas.active = inconf unless ResumeNav runs) on the detect's own row offsets
+  if (mvp_device(c, p.mvp, d, (const unsigned *)c->rowoff.p, gate, sticky,
+                 p.resume_nav ? nullptr : (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p, p.reso != 0))
+    return -1;
+  // second half: resopairs rewrite, ResumeNav's asas.active, unique / cumulative counts
+  return p.resume_nav ? bk_apply(c, bk) : 0;
 }
 
 }  // namespace bsa
@@ -332,7 +349,9 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   if (!bsa::ensure(c, c->sim_ctl, 64, "sim control words")) return -1;
   BSA_HIP(c, hipMemsetAsync(c->sim_ctl.p, 0, 64, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
+  if (p->resume_nav != 0 && p->resume_nav != 1) return bsa::fail(c, "resume_nav must be 0 or 1");
   c->simp = *p;
+  c->bk_ready = false;  // empty resopairs / previous pair sets
   c->sim_rpr = (n + c->nranks - 1) / c->nranks;
   c->sim_rb = std::min<int64_t>(n, (int64_t)c->rank * c->sim_rpr);
   c->sim_re = std::min<int64_t>(n, c->sim_rb + c->sim_rpr);
@@ -353,7 +372,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
   for (int attempt = 0; c->sim_steps < target; ++attempt) {
     if (attempt > 6) return bsa::fail(c, "candidate buffer overflow in the resident step (retries exhausted)");
     const int64_t base = c->sim_steps, base_cd = c->sim_cd_calls;
-    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 16, c->stream));  // sticky, steps_done
+    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 24, c->stream));  // sticky, steps_done, demand
     while (c->sim_steps < target) {
       if (c->sim_steps % c->simp.cd_every == 0)
         if (bsa::sim_cd(c)) return -1;
@@ -366,8 +385,8 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
       c->sim_steps++;
     }
     // the batch's only host synchronisation: did every step complete?
-    unsigned long long ctl[2] = {0, 0};
-    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 16, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long ctl[3] = {0, 0, 0};
+    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 24, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
     if ((unsigned)ctl[0] == 0) break;
     // aborted at step base + done: the state is that of the step's start
@@ -377,8 +396,13 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     for (int64_t k = base; k < base + done; ++k) cds += (k % c->simp.cd_every == 0) ? 1 : 0;
     c->sim_cd_calls = base_cd + cds;
     c->sim_gathered = c->nranks == 1;
-    // grow: at least double, and enough for the last detect's demand (its
-    // shard counters keep counting past the capacity)
+    if (ctl[2] > 0) {  // this rank's resopairs outgrew their buffer
+      c->bk_cap = std::max(2 * c->bk_cap, ctl[2] + ctl[2] / 4 + 1024);
+      continue;
+    }
+    // candidate overflow (here or on another rank): grow at least double, and
+    // enough for the last detect's demand (its shard counters keep counting
+    // past the capacity)
     bsa::Counters h;
     BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
     unsigned long long worst = 0;
@@ -429,6 +453,54 @@ int bsa_sim_stats(bsa_ctx *cc, int64_t *out6) {
   out6[3] = c->sim_last_los;
   out6[4] = c->sim_rb;
   out6[5] = c->sim_re;
+  return 0;
+}
+
+int bsa_sim_asas_stats(bsa_ctx *cc, int64_t *out6) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !out6) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_asas_stats before bsa_sim_init");
+  if (!c->simp.resume_nav) return bsa::fail(c, "ASAS bookkeeping is off (resume_nav = 0)");
+  BSA_HIP(c, hipSetDevice(c->device));
+  unsigned long long st[8] = {0};
+  if (c->bk_ready) BSA_HIP(c, hipMemcpyAsync(st, c->bk_stats.p, 64, hipMemcpyDeviceToHost, c->stream));
+  const int64_t rb = c->sim_rb, nr = c->sim_re - c->sim_rb;
+  std::vector<uint8_t> act((size_t)std::max<int64_t>(nr, 1));
+  if (nr > 0) BSA_HIP(c, hipMemcpyAsync(act.data(), (uint8_t *)c->s_active.p + rb, nr, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  int64_t na = 0;
+  for (int64_t k = 0; k < nr; ++k) na += act[k] ? 1 : 0;
+  const bool one = c->nranks == 1;
+  out6[0] = (int64_t)st[0];
+  for (int k = 1; k < 5; ++k) out6[k] = one ? (int64_t)st[k] : -1;
+  out6[5] = na;
+  return 0;
+}
+
+int bsa_sim_resopairs(bsa_ctx *cc, int32_t *idx1, int32_t *idx2, int64_t cap, int64_t *count) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !count) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_resopairs before bsa_sim_init");
+  if (!c->simp.resume_nav) return bsa::fail(c, "ASAS bookkeeping is off (resume_nav = 0)");
+  if (cap > 0 && (!idx1 || !idx2)) return bsa::fail(c, "NULL resopairs buffer");
+  BSA_HIP(c, hipSetDevice(c->device));
+  *count = 0;
+  if (!c->bk_ready) return 0;
+  const int64_t nr = c->last_re - c->last_rb;
+  std::vector<unsigned> ptr((size_t)nr + 1);
+  BSA_HIP(c, hipMemcpyAsync(ptr.data(), c->bk_rptr.p, (size_t)(nr + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  const int64_t total = ptr[(size_t)nr];
+  *count = total;
+  if (total > cap || total == 0) return 0;
+  std::vector<unsigned> col((size_t)total);
+  BSA_HIP(c, hipMemcpyAsync(col.data(), c->bk_rcol.p, (size_t)total * 4, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  for (int64_t r = 0; r < nr; ++r)
+    for (unsigned k = ptr[(size_t)r]; k < ptr[(size_t)r + 1]; ++k) {
+      idx1[k] = (int32_t)(c->last_rb + r);
+      idx2[k] = (int32_t)col[k];
+    }
   return 0;
 }
 

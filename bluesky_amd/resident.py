@@ -2,7 +2,8 @@
 
 State lives in HBM across steps; the host only launches.  One step:
 CD + MVP every ``cd_every`` steps (asas.update, asas.py:473-504, with
-``asas.active = inconf`` standing in for ResumeNav), then Pilot.APorASAS
+``asas.active = inconf`` standing in for ResumeNav, or with ``resume_nav`` the
+device-side resopairs bookkeeping + ResumeNav), then Pilot.APorASAS
 (no wind) fused with the kinematic update (traffic.py:397-409).
 With several ranks (one process per GPU) each rank owns a contiguous row
 block and the replicated state is all-gathered over RCCL before each CD.
@@ -41,9 +42,11 @@ def initial_state(traf):
 
 def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, reso=True, mar=1.05,
            swresohoriz=True, swresospd=False, swresohdg=False, swresovert=False, swprio=False,
-           priocode='FF1', wind=None):
+           priocode='FF1', wind=None, resume_nav=False):
     """bsa_sim_params; ASAS defaults of asas.py:81-112 with asas_mar from data/default.cfg.
-    ``wind=(vnorth, veast)`` [m/s]: constant wind (winddim 1)."""
+    ``wind=(vnorth, veast)`` [m/s]: constant wind (winddim 1).  ``resume_nav``: ASAS.update's
+    resopairs bookkeeping and ResumeNav's asas.active (asas.py:409-504) instead of
+    ``active = inconf``."""
     mvp = _lib.MvpParams(Rm=rpz * mar, dhm=hpz * mar, dtlookahead=tla, vmin=200.0 * NM / 3600.,
                          vmax=500.0 * NM / 3600., vsmin=-3000. / 60. * FT, vsmax=3000. / 60. * FT,
                          swresohoriz=int(swresohoriz), swresospd=int(swresospd),
@@ -51,7 +54,8 @@ def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, res
                          priocode=_lib.PRIO_CODES.get(priocode, 0), swnoreso=0, swresooff=0)
     wn, we = (0.0, 0.0) if wind is None else (float(wind[0]), float(wind[1]))
     return _lib.SimParams(simdt=simdt, rpz=rpz, hpz=hpz, tla=tla, cd_every=int(cd_every),
-                          reso=int(bool(reso)), mvp=mvp, winddim=0 if wind is None else 1, pad=0,
+                          reso=int(bool(reso)), mvp=mvp, winddim=0 if wind is None else 1,
+                          resume_nav=int(bool(resume_nav)),
                           windnorth=wn, windeast=we)
 
 
@@ -74,3 +78,9 @@ class ResidentSim:
 
     def stats(self):
         return self.ctx.sim_stats()
+
+    def asas_stats(self):
+        return self.ctx.sim_asas_stats()
+
+    def resopairs(self):
+        return self.ctx.sim_resopairs()

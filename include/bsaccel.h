@@ -110,7 +110,9 @@ int bsa_last_candidates(bsa_ctx *ctx, int64_t *n_candidates);
 
 /* Candidate-list capacity (pairs surviving the prefilter) for the next
  * detects; rounded up to a multiple of the shard count.  Detects grow it on
- * overflow (with a retry), so this is a tuning / testing knob only. */
+ * overflow (with a retry), so this is a tuning / testing knob only.  Once the
+ * resident sim's ASAS bookkeeping has started it also sets the resopairs
+ * capacity (grown the same way). */
 int bsa_set_candidate_capacity(bsa_ctx *ctx, int64_t capacity);
 
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
@@ -210,7 +212,8 @@ int bsa_comm_allreduce_sum(bsa_ctx *ctx, double *values, int count);
  * The synthetic sim step of SURVEY.md 8d with all state resident in HBM:
  *   every cd_every steps: [all-gather] -> detect (own rows) -> MVP (own rows,
  *                         only if any rank has a conflict, asas.py:486-487)
- *                         -> asas.active = inconf
+ *                         -> asas.active = inconf, or (resume_nav = 1) the ASAS
+ *                         bookkeeping + ResumeNav (asas.py:409-504) on the device
  *   every step:           Pilot.APorASAS (pilot.py:28-63, winddim 0/1) fused with
  *                         UpdateAirSpeed/GroundSpeed/Position (traffic.py:425-483)
  * AP targets, selalt, bank, eps and perf.acceleration() are frozen inputs. */
@@ -221,7 +224,9 @@ typedef struct bsa_sim_params {
   bsa_mvp_params mvp;
   int32_t winddim;  /* 0 = no wind, 1 = constant wind (windfield.py:150-152): the wind branches
                        of Pilot.APorASAS (pilot.py:31-36,51-61) and UpdateGroundSpeed */
-  int32_t pad;
+  int32_t resume_nav; /* 1: ASAS.update bookkeeping on the device: resopairs, ResumeNav's
+                         asas.active (asas.py:409-471) and the unique / cumulative pair
+                         counts (asas.py:490-502); 0: asas.active = inconf */
   double windnorth, windeast; /* [m/s] */
 } bsa_sim_params;
 
@@ -247,6 +252,16 @@ int bsa_sim_read(bsa_ctx *ctx, bsa_sim_out *o);
 /* [0] steps done, [1] CD calls, [2] conflicts and [3] LoS pairs of the last
  * CD call (this rank's rows), [4] this rank's row_begin, [5] row_end. */
 int bsa_sim_stats(bsa_ctx *ctx, int64_t *out6);
+/* ASAS bookkeeping after the last CD call (resume_nav = 1; replaces
+ * ASAS.update's Python sets, asas.py:490-502):
+ * [0] |resopairs| of this rank's rows, [1] |confpairs_unique|,
+ * [2] |lospairs_unique|, [3] len(confpairs_all), [4] len(lospairs_all),
+ * [5] number of active aircraft of this rank's rows.  [1]-[4] need the
+ * whole pair set and are -1 with several ranks. */
+int bsa_sim_asas_stats(bsa_ctx *ctx, int64_t *out6);
+/* This rank's resopairs (idx1 ascending, then idx2), at most cap pairs;
+ * *count = total (call again with a larger buffer when *count > cap). */
+int bsa_sim_resopairs(bsa_ctx *ctx, int32_t *idx1, int32_t *idx2, int64_t cap, int64_t *count);
 
 #ifdef __cplusplus
 }

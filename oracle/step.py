@@ -7,7 +7,10 @@ the hot path: asas.update (asas.py:473-504: detect, then MVP.resolve only if
 confpairs is non-empty) every ``cd_every`` steps with ``asas.active =
 inconf``; Pilot.APorASAS (pilot.py:28-63) without wind or with a constant
 wind (``p['wind'] = (vnorth, veast)``, windfield.py:150-152); UpdateAirSpeed /
-UpdateGroundSpeed / UpdatePosition (traffic.py:425-483).
+UpdateGroundSpeed / UpdatePosition (traffic.py:425-483).  With a
+``Bookkeeping`` (oracle/asas.py) the CD step instead runs ASAS.update's
+resopairs bookkeeping and ResumeNav (asas.py:409-504) and takes asas.active
+from it.
 """
 import numpy as np
 
@@ -16,9 +19,10 @@ from . import mvp as omvp
 from . import statebased as ocd
 
 
-def sim_step(st, p, do_cd):
+def sim_step(st, p, do_cd, bk=None):
     """One step on the dict ``st`` (keys of bluesky_amd.resident.initial_state
-    plus asas_trk/asas_tas/asas_vs/asas_alt/active).  Returns the new dict."""
+    plus asas_trk/asas_tas/asas_vs/asas_alt/active).  Returns the new dict.
+    ``bk``: an oracle.asas.Bookkeeping, updated in place on CD steps."""
     st = {k: np.array(v, copy=True) for k, v in st.items()}
     n = len(st['lat'])
     if do_cd:
@@ -34,7 +38,13 @@ def sim_step(st, p, do_cd):
                                         st['asas_alt'].copy(), p['mvp'])
                 st['asas_trk'], st['asas_tas'], st['asas_vs'] = o['trk'], o['tas'], o['vs']
                 st['asas_alt'] = o['alt']
-            st['active'] = np.asarray(r['inconf'], dtype=bool)
+            if bk is None:
+                st['active'] = np.asarray(r['inconf'], dtype=bool)
+        if bk is not None:
+            bk.active = np.asarray(st['active'], dtype=bool).copy()
+            bk.update(zip(r['ci'], r['cj']), zip(r['li'], r['lj']), st['lat'], st['lon'],
+                      st['gseast'], st['gsnorth'], st['trk'], p['rpz'], p['mvp']['Rm'])
+            st['active'] = bk.active.copy()
     act = st['active']
     wind = p.get('wind')
     if wind is not None:                                      # pilot.py:31-35

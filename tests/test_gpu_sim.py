@@ -129,3 +129,61 @@ def test_resident_overflow_retry_is_exact(ctx):
         assert np.array_equal(got[k], exp[k]), k
     assert (st['steps'], st['cd_calls'], st['n_conf']) == (exp_stats['steps'], exp_stats['cd_calls'],
                                                           exp_stats['n_conf'])
+
+
+@pytest.mark.parametrize('cd_every,steps,simdt', [(1, 8, 2.0), (2, 9, 1.5)])
+def test_resident_resume_nav_matches_oracle(ctx, cd_every, steps, simdt):
+    """resume_nav: device resopairs / ResumeNav / unique counts (asas.py:409-504)
+    against oracle/asas.py (pinned to the reference's ASAS.update, tests/golden/
+    asas_*.npz) composed into the step; resopairs compared as exact sets."""
+    from oracle import asas as oasas
+    t = synth.box(1500, 60.0, seed=43)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=simdt, cd_every=cd_every, resume_nav=True)
+    sim = resident.ResidentSim(init, p, ctx=ctx)
+    op = oracle_params(p)
+    bk = oasas.Bookkeeping(t.ntraf)
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(t.ntraf), active=np.zeros(t.ntraf, bool))
+    dropped = 0
+    for k in range(steps):
+        cd = k % cd_every == 0
+        exp = ostep.sim_step(prev, op, do_cd=cd, bk=bk)
+        sim.step(1)
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        if cd:
+            dropped += sum(1 for v in bk.last_keep.values() if not v)
+            i, j = sim.resopairs()
+            assert list(zip(i.tolist(), j.tolist())) == sorted(bk.resopairs), 'step %d resopairs' % k
+            st = sim.asas_stats()
+            assert st == dict(resopairs=len(bk.resopairs), confpairs_unique=len(bk.confpairs_unique),
+                              lospairs_unique=len(bk.lospairs_unique), confpairs_all=bk.confpairs_all,
+                              lospairs_all=bk.lospairs_all, active=int(exp['active'].sum())), k
+        prev = got
+    assert len(bk.resopairs) > 0 and dropped > 0, (len(bk.resopairs), dropped)
+
+
+def test_resident_resume_nav_overflow_retry_is_exact(ctx):
+    """Resopairs buffer forced far too small mid-run: the step aborts before MVP,
+    grows the buffer and re-runs; bitwise equal to an undisturbed run."""
+    from bluesky_amd import _lib
+    t = synth.box(2000, 80.0, seed=47)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=1.0, resume_nav=True)
+    ref = resident.ResidentSim(init, p, ctx=ctx)
+    ref.step(6)
+    exp, exp_bk, exp_reso = ref.read(), ref.asas_stats(), ref.resopairs()
+    c2 = _lib.Context(0)
+    sim = resident.ResidentSim(init, p, ctx=c2)
+    sim.step(2)
+    c2.set_candidate_capacity(16)   # also the resopairs capacity once bookkeeping runs
+    sim.step(4)
+    got, got_bk, got_reso = sim.read(), sim.asas_stats(), sim.resopairs()
+    for k in exp:
+        assert np.array_equal(got[k], exp[k]), k
+    assert got_bk == exp_bk and exp_bk['resopairs'] > 16
+    assert np.array_equal(got_reso[0], exp_reso[0]) and np.array_equal(got_reso[1], exp_reso[1])
+    assert sim.stats()['steps'] == 6
+    c2.close()

@@ -17,10 +17,34 @@ CD = util.golden('cd_*.npz')
 MVP = util.golden('mvp_*.npz')
 KIN = util.golden('kin_*.npz')
 KWIK = util.golden('cdkwik_*.npz')
+ASAS = util.golden('asas_*.npz')
 
 
 def test_fixtures_present():
-    assert len(CD) >= 9 and len(MVP) >= 5 and len(KIN) >= 3 and len(KWIK) >= 6
+    assert len(CD) >= 9 and len(MVP) >= 5 and len(KIN) >= 3 and len(KWIK) >= 6 and len(ASAS) >= 3
+
+
+@pytest.mark.parametrize('path', ASAS, ids=[util.case_name(p) for p in ASAS])
+def test_oracle_asas_bookkeeping_matches_reference(path):
+    """ASAS.update's resopairs / unique / cumulative bookkeeping and ResumeNav's
+    asas.active (asas.py:409-504), replayed over the reference's recorded calls.
+    active is compared where the reference's result does not depend on set
+    iteration order (aircraft whose resopairs agree, oracle/asas.py)."""
+    from oracle import asas as oasas
+    z = np.load(path)
+    n = int(z['n'])
+    bk = oasas.Bookkeeping(n)
+    for k in range(int(z['ncalls'])):
+        keep = bk.update(zip(z['ci%d' % k], z['cj%d' % k]), zip(z['li%d' % k], z['lj%d' % k]),
+                         z['lat%d' % k], z['lon%d' % k], z['gseast'], z['gsnorth'], z['trk'],
+                         float(z['rpz']), float(z['rm']))
+        assert sorted(bk.resopairs) == list(zip(z['reso_i%d' % k].tolist(), z['reso_j%d' % k].tolist())), k
+        counts = [len(bk.confpairs_unique), len(bk.lospairs_unique), bk.confpairs_all, bk.lospairs_all]
+        assert counts == z['counts%d' % k].tolist(), k
+        amb = np.array(bk.ambiguous(keep), dtype=np.int64)
+        assert np.array_equal(amb, z['ambiguous%d' % k]), k
+        una = np.setdiff1d(np.arange(n), amb)
+        assert np.array_equal(bk.active[una], z['active%d' % k][una]), k
 
 
 @pytest.mark.parametrize('path', KWIK, ids=[util.case_name(p) for p in KWIK])

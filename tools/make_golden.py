@@ -10,6 +10,9 @@ and outputs as small ``.npz`` files under ``tests/golden/``:
 * ``mvp_<case>.npz``  -- ``MVP.resolve`` (MVP.py:14-143) for several switch sets
 * ``kin_<case>.npz``  -- ``Traffic.UpdateAirSpeed/GroundSpeed/Position``
                          (traffic.py:425-483)
+* ``asas_<case>.npz``  -- ``ASAS.update``'s bookkeeping + ``ResumeNav``
+                         (asas.py:409-504) over a few CD calls, run by the
+                         reference's own ``ASAS.update`` on a stand-in ``bs.traf``
 * ``cdkwik_<case>.npz`` -- the opt-in KWIK variant: ``StateBasedCD.detect`` with
                          ``geo.qdrdist_matrix`` swapped for ``geo.kwikqdrdist_matrix``
                          (geo.py:347-363), its metre distance handed over / nm
@@ -347,6 +350,69 @@ def run_kin(name, n, seed, dt, wind=None):
     print('kin_%-17s N=%5d dt=%g wind=%s' % (name, n, dt, wind))
 
 
+def run_asas(name, traf, ncalls=4, dt=20.0):
+    """Reference ASAS.update (asas.py:473-504) incl. ResumeNav on a stand-in
+    bs.traf; state advanced along straight tracks between CD calls."""
+    import bluesky as bs
+    from bluesky.traffic.asas.asas import ASAS
+    from oracle import asas as oasas
+    n = traf.ntraf
+    lat, lon = traf.lat.copy(), traf.lon.copy()
+    gse = traf.gs * np.sin(np.radians(traf.trk))
+    gsn = traf.gs * np.cos(np.radians(traf.trk))
+    idmap = {k: i for i, k in enumerate(traf.id)}
+
+    class Route:
+        def findact(self, i):
+            return -1
+
+    ft_ = types.SimpleNamespace(ntraf=n, id=traf.id, trk=traf.trk, gs=traf.gs, alt=traf.alt,
+                                vs=traf.vs, gseast=gse, gsnorth=gsn,
+                                ap=types.SimpleNamespace(route=[Route() for _ in range(n)]))
+    ft_.id2idx = lambda ids: [idmap.get(x, -1) for x in ids]
+    saved = getattr(bs, 'traf', None)
+    bs.traf = ft_
+    res = {}
+    me = types.SimpleNamespace(swasas=True, tasas=0.0, dtasas=1.0, R=RPZ, dh=HPZ, Rm=RPZ * 1.05,
+                               dtlookahead=TLA, resopairs=set(), confpairs_unique=set(),
+                               lospairs_unique=set(), confpairs_all=[], lospairs_all=[],
+                               active=np.zeros(n, dtype=bool))
+    me.cd = types.SimpleNamespace(detect=StateBasedCD.detect)
+    me.cr = types.SimpleNamespace(resolve=lambda asas, tr: None)
+    me.ResumeNav = lambda: ASAS.ResumeNav(me)
+    bk = oasas.Bookkeeping(n)
+    out = dict(n=n, ncalls=ncalls, rpz=RPZ, hpz=HPZ, tla=TLA, rm=RPZ * 1.05)
+    try:
+        for k in range(ncalls):
+            ft_.lat, ft_.lon = lat.copy(), lon.copy()
+            ASAS.update(me, float(k))
+            ci, cj = ids_to_idx(me.confpairs, idmap)
+            li, lj = ids_to_idx(me.lospairs, idmap)
+            keep = bk.update(zip(ci, cj), zip(li, lj), ft_.lat, ft_.lon, gse, gsn, traf.trk,
+                             RPZ, RPZ * 1.05)
+            amb = np.array(bk.ambiguous(keep), dtype=np.int64)
+            reso = sorted((idmap[a], idmap[b]) for a, b in me.resopairs)
+            assert reso == sorted(bk.resopairs), 'oracle resopairs != reference'
+            assert len(me.confpairs_unique) == len(bk.confpairs_unique)
+            assert len(me.lospairs_unique) == len(bk.lospairs_unique)
+            assert (len(me.confpairs_all), len(me.lospairs_all)) == (bk.confpairs_all, bk.lospairs_all)
+            una = np.setdiff1d(np.arange(n), amb)
+            assert np.array_equal(me.active[una], bk.active[una]), 'oracle active != reference'
+            r = np.array(reso, dtype=np.int64).reshape(-1, 2)
+            out.update({'lat%d' % k: ft_.lat, 'lon%d' % k: ft_.lon, 'ci%d' % k: ci, 'cj%d' % k: cj,
+                        'li%d' % k: li, 'lj%d' % k: lj, 'reso_i%d' % k: r[:, 0], 'reso_j%d' % k: r[:, 1],
+                        'active%d' % k: me.active.copy(), 'ambiguous%d' % k: amb,
+                        'counts%d' % k: np.array([len(me.confpairs_unique), len(me.lospairs_unique),
+                                                  len(me.confpairs_all), len(me.lospairs_all)])})
+            lat = lat + np.degrees(dt * gsn / 6371000.)
+            lon = lon + np.degrees(dt * gse / np.cos(np.radians(lat)) / 6371000.)
+    finally:
+        bs.traf = saved
+    out.update(trk=traf.trk, gs=traf.gs, alt=traf.alt, vs=traf.vs, gseast=gse, gsnorth=gsn)
+    np.savez_compressed(os.path.join(OUT, 'asas_%s.npz' % name), **out)
+    print('asas_%-16s N=%5d calls=%d final resopairs=%d' % (name, n, ncalls, len(me.resopairs)))
+
+
 KWIK_CASES = ('box500', 'equator1500', 'antimeridian800', 'polar400', 'edge', 'own_ne_int300')
 
 
@@ -356,6 +422,11 @@ def main():
     if '--kwik-only' in sys.argv:
         for name in KWIK_CASES:
             run_kwik(name, *cds[name])
+        return
+    if '--asas-only' in sys.argv:
+        run_asas('box500', cds['box500'][0])
+        run_asas('box2000', cds['box2000'][0])
+        run_asas('edge', cds['edge'][0])
         return
     for name in KWIK_CASES:
         run_kwik(name, *cds[name])
