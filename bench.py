@@ -102,7 +102,7 @@ def main():
     pairs = float(n) * n * cd_steps
     value = pairs / dt
     pf_s = tm['prefilter'] * 1e-3
-    tested = ts['groups'] / max(ts['detects'], 1) * 64 * 16    # pair tests the prefilter executed
+    tested = ts['groups'] / max(ts['detects'], 1) * _lib.PF_BLOCK_PAIRS    # pair tests the prefilter executed
     pmc = pmc_figures()
     pf = pmc.get('k_prefilter', {})
     roof = dict(bound='valu', kernel='k_prefilter (fp32 packed VALU stage-1 test, dominant)',

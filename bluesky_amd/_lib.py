@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('BSACCEL_LIB', os.path.join(_HERE, 'libbsaccel.so'))
 
 ABI_VERSION = 1
+PF_BLOCK_PAIRS = 512   # BSA_PF_BLOCK_PAIRS: stage-1 pair tests per swept prefilter block
 FLAG_WITH_DCPA = 1
 FLAG_NOPRUNE = 2
 FLAG_RESORT = 4

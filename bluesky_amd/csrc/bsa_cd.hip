@@ -66,18 +66,45 @@ __device__ __forceinline__ unsigned expand10(unsigned v) {
   v = (v | (v << 2)) & 0x09249249u;
   return v;
 }
-__device__ __forceinline__ unsigned morton_latlon(double latd, double lond) {
+// Spatial order key: 3-D Hilbert index (10 bits per axis, Skilling's
+// transpose form) of the unit position vector.  Consecutive keys are always
+// adjacent cells (no Z-order jumps), so the 64-row groups and 8-column
+// sub-groups cut from the sorted order have tighter boxes: ~15% fewer stage-1
+// pair tests than Morton order at the 100k box (tools/cull_sim.py).  Any order
+// gives identical results; only the culling efficiency depends on it.
+__device__ __forceinline__ unsigned curve_key(double latd, double lond) {
   const double la = latd * kD2R, lo = lond * kD2R;
   const double cl = cos(la);
   const double p[3] = {cl * cos(lo), cl * sin(lo), sin(la)};
-  unsigned key = 0;
+  unsigned X[3];
   for (int k = 0; k < 3; ++k) {
     if (!(p[k] == p[k]) || isinf(p[k])) return 0xffffffffu;
     int q = (int)((p[k] + 1.0) * 512.0);
-    q = q < 0 ? 0 : (q > 1023 ? 1023 : q);
-    key |= expand10((unsigned)q) << (2 - k);
+    X[k] = (unsigned)(q < 0 ? 0 : (q > 1023 ? 1023 : q));
   }
-  return key;
+  // axes -> transposed Hilbert index
+  for (unsigned Q = 1u << 9; Q > 1u; Q >>= 1) {
+    const unsigned P = Q - 1u;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (X[i] & Q) {
+        X[0] ^= P;
+      } else {
+        const unsigned t = (X[0] ^ X[i]) & P;
+        X[0] ^= t;
+        X[i] ^= t;
+      }
+    }
+  }
+  X[1] ^= X[0];
+  X[2] ^= X[1];
+  unsigned t = 0;
+  for (unsigned Q = 1u << 9; Q > 1u; Q >>= 1)
+    if (X[2] & Q) t ^= Q - 1u;
+  X[0] ^= t;
+  X[1] ^= t;
+  X[2] ^= t;
+  return (expand10(X[0]) << 2) | (expand10(X[1]) << 1) | expand10(X[2]);
 }
 
 __global__ __launch_bounds__(256) void k_keys(int cnt, int base, const double *__restrict__ lat,
@@ -87,7 +114,7 @@ __global__ __launch_bounds__(256) void k_keys(int cnt, int base, const double *_
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const int o = base + k;
-  key[k] = morton_latlon(lat[o], lon[o]);
+  key[k] = curve_key(lat[o], lon[o]);
   idx[k] = (unsigned)o;
 }
 
@@ -240,6 +267,8 @@ __device__ __forceinline__ float wmax(float v) {
 constexpr int kGroup = 64;
 static_assert(kTile % kGroup == 0, "tiles are whole groups");
 constexpr int kGroupsPerTile = kTile / kGroup;
+constexpr int kSub = 8;  // column sub-group (culling granularity; one stage-1 chunk)
+static_assert(kGroup % kSub == 0 && (kSub & (kSub - 1)) == 0, "sub-groups tile a group");
 
 __device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b) {
   TileBox u;
@@ -294,16 +323,16 @@ __global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restric
     b.pad1 = 0;
     return b;
   };
-  for (int o = 1; o < 16; o <<= 1) {  // within each 16-lane sub-group
+  for (int o = 1; o < kSub; o <<= 1) {  // within each kSub-lane sub-group
     for (int q = 0; q < 4; ++q) {
       lo[q] = xmin(lo[q], o);
       hi[q] = xmax(hi[q], o);
     }
     smax = xmax(smax, o);
   }
-  const int sg = g * 4 + (lane >> 4);
-  if (sbox && (lane & 15) == 0 && sg * 16 < cnt) sbox[sg] = mkbox(min(16, cnt - sg * 16));
-  for (int o = 16; o < 64; o <<= 1) {
+  const int sg = g * (kGroup / kSub) + lane / kSub;
+  if (sbox && (lane & (kSub - 1)) == 0 && sg * kSub < cnt) sbox[sg] = mkbox(min(kSub, cnt - sg * kSub));
+  for (int o = kSub; o < 64; o <<= 1) {
     for (int q = 0; q < 4; ++q) {
       lo[q] = xmin(lo[q], o);
       hi[q] = xmax(hi[q], o);
@@ -473,12 +502,12 @@ constexpr int PF_Q1 = 1024;  // per-wave stage-1 queue: u16 (row_local << 6 | co
 constexpr int PF_Q2 = 128;   // per-wave stage-2 queue: uint2 (sorted row, sorted column)
 constexpr int PF_WROWS = 64;   // rows per wave (one per lane)
 constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
-constexpr int PF_BLOCKS_PER_CU = 5;  // LDS-limited: ~7.5 KB per wave
-constexpr int kSub = 16;         // column sub-group (culling granularity)
+constexpr int PF_BLOCKS_PER_CU = 5;  // LDS-limited (~7.8 KB per wave) and BSA_PF_WAVES_PER_EU
 constexpr int kSubsPerTile = kTile / kSub;
 constexpr int kWorkShards = 8;   // one dequeue counter per XCD group
 constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
-static_assert(kSubsPerTile == 32, "one sub-group per lane of a half wave");
+static_assert(kSubsPerTile == 64, "one sub-group box per lane");
+constexpr int kSubsPerBatch = 64 / kSub;  // sub-groups per 64-column batch
 static_assert(PF_Q1 >= 64 * 8, "one 8-column chunk of survivors fits the stage-1 queue");
 
 __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 *__restrict__ cand,
@@ -510,10 +539,10 @@ __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 
 #endif
 
 // K1a: each wave sweeps its 64 rows (one per lane, in registers) against the
-// columns of a tile pair that survive culling at 16-column sub-group
-// granularity (lanes 0-31 test the 32 sub-group boxes of the 512-column tile
-// against the wave's row box).  The surviving columns are gathered in
-// batches of 64 (four sub-groups; one coalesced record load per lane, issued
+// columns of a tile pair that survive culling at 8-column sub-group
+// granularity (each lane tests one of the 64 sub-group boxes of the
+// 512-column tile against the wave's row box).  The surviving columns are
+// gathered in batches of 64 (eight sub-groups; one coalesced record load per lane, issued
 // one batch ahead), projected and staged in the wave's LDS slot as column
 // PAIRS, from which every lane reads them as broadcasts: each packed fp32
 // instruction tests the lane's row against two columns.
@@ -538,7 +567,14 @@ __device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 
 // ds_bpermute).  Stage-2 survivors go to a second queue flushed to HBM with
 // one atomic on the wave's candidate shard.
 template <bool NOPRUNE>
-__global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
+// 5 waves per SIMD = PF_BLOCKS_PER_CU resident workgroups (the LDS limit):
+// caps the kernel at 96 VGPRs (a few spill to scratch; measured 2% faster
+// than 4 waves per SIMD at 102 VGPRs)
+#ifndef BSA_PF_WAVES_PER_EU
+#define BSA_PF_WAVES_PER_EU 5
+#endif
+#define PF_OCC __attribute__((amdgpu_waves_per_eu(BSA_PF_WAVES_PER_EU, 8)))
+__global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, int nrows,
     const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, int ncols,
     const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ sbox_c,
@@ -566,11 +602,13 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
   unsigned *sci = cix[w];
   float4 *rv = rsv[w];
   unsigned n2 = 0;        // wave-uniform
-  unsigned subs = 0;      // 16-column sub-groups swept by this wave (for the roofline)
+  unsigned subs = 0;      // 8-column sub-groups swept by this wave (for the roofline)
   const float qnan = __builtin_nanf("");
   // Dynamic work distribution: an item is one (tile pair, 64-row slice);
   // each wave dequeues items from the counter of its XCD group (blockIdx % 8)
   // so no single word takes every dequeue (MI355X_MICROARCH 'dequeue').
+  // (Giving each XCD a contiguous eighth of the tile pairs for L2 locality
+  // measured slower: 231 vs 224 us at box100k.)
   const unsigned long long nitems = ntiles * PF_ITEMS_PER_TILE;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
@@ -600,21 +638,21 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     const int nsub = min(kSubsPerTile, (ncols - cbase + kSub - 1) / kSub);
     const TileBox rbx = gbox_r[rbase / kGroup];
     const bool gk = lane < nsub && (NOPRUNE || boxes_may_interact(rbx, sbox_c[cbase / kSub + lane]));
-    unsigned gm = (unsigned)__ballot(gk);
+    unsigned long long gm = __ballot(gk);
     if (!gm) break;
-    subs += (unsigned)__popc(gm);
+    subs += (unsigned)__popcll(gm);
 
-    // this lane's slot of the next batch: the (lane / 16)-th remaining
-    // sub-group, column lane % 16 of it (sub-groups taken in ascending order)
-    auto batch_col = [&](unsigned m) -> int {
-      const unsigned q = (unsigned)lane >> 4;
+    // this lane's slot of the next batch: the (lane / kSub)-th remaining
+    // sub-group, column lane % kSub of it (sub-groups taken in ascending order)
+    auto batch_col = [&](unsigned long long m) -> int {
+      const unsigned q = (unsigned)lane / kSub;
       for (unsigned t = 0; t < q && m; ++t) m &= m - 1;
       if (!m) return -1;
-      const int j = cbase + __builtin_ctz(m) * kSub + (lane & 15);
+      const int j = cbase + __builtin_ctzll(m) * kSub + (lane & (kSub - 1));
       return j < ncols ? j : -1;
     };
-    auto drop4 = [](unsigned m) {
-      for (int t = 0; t < 4 && m; ++t) m &= m - 1;
+    auto drop_batch = [](unsigned long long m) {
+      for (int t = 0; t < kSubsPerBatch && m; ++t) m &= m - 1;
       return m;
     };
     auto load_col = [&](int j, PFRec &r, PFVel &v) {
@@ -651,7 +689,11 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
     // the item's plane: o = first row of the slice, E / N an orthonormal
     // tangent pair at o (any orthonormal pair is exact-safe; near a pole, or
     // for a non-finite o, the x / y axes)
-    const PFRec O = prow[rbase];
+    // (wave-uniform: kept in SGPRs)
+    PFRec O = prow[rbase];
+    O.x = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(O.x)));
+    O.y = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(O.y)));
+    O.z = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(O.z)));
     float ex = 1.f, ey = 0.f, nxx = 0.f, nyy = 1.f, nzz = 0.f;
     {
       const float rho2 = O.x * O.x + O.y * O.y;
@@ -758,7 +800,7 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
         sci[lane] = (unsigned)jn;
         colmask = __ballot(jn >= 0);
       }
-      gm = drop4(gm);
+      gm = drop_batch(gm);
       if (gm) {  // prefetch the next batch while this one is swept
         jn = batch_col(gm);
         load_col(jn, nx, nv);
@@ -768,15 +810,18 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
       for (int ch = 0; ch < nchunk; ++ch) {
         const int j0 = ch * 8;
         unsigned bm = 0;
-        float4 pa[4], pe[4], pl[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          pa[u] = cka[w][(j0 >> 1) + u];
-          pe[u] = cen[w][(j0 >> 1) + u];
-          pl[u] = clh[w][(j0 >> 1) + u];
+        for (int h = 0; h < 4; h += 2) {
+        // two column pairs per load group (register pressure: occupancy)
+        float4 pa[2], pe[2], pl[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          pa[u] = cka[w][(j0 >> 1) + h + u];
+          pe[u] = cen[w][(j0 >> 1) + h + u];
+          pl[u] = clh[w][(j0 >> 1) + h + u];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 2; ++u) {
           if (NOPRUNE) {
             bm = (bm << 2) | 3u;
           } else {
@@ -793,6 +838,8 @@ __global__ __launch_bounds__(PF_BLOCK) void k_prefilter(
             bm = __builtin_amdgcn_alignbit(bm, t0, 31);   // (bm << 1) | (t0 >> 31)
             bm = __builtin_amdgcn_alignbit(bm, t1, 31);
           }
+        }
+        __builtin_amdgcn_sched_barrier(0);
         }
         const unsigned cm = (unsigned)(colmask >> j0) & 0xffu;
         // bit 7 - u <-> slot j0 + u: reverse the 8 slot-valid bits

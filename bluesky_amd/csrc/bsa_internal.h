@@ -98,7 +98,7 @@ struct Counters {
   unsigned long long conf;
   unsigned long long los;
   unsigned long long tiles;
-  unsigned long long groups;  // (64-row x 16-column) blocks swept by the prefilter
+  unsigned long long groups;  // (64-row x 8-column) blocks swept by the prefilter
   unsigned long long pad[3];
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];

@@ -117,7 +117,9 @@ int bsa_set_candidate_capacity(bsa_ctx *ctx, int64_t capacity);
 
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
  * bounding-box cull, the total number of tile pairs, and the number of
- * (64-row x 16-column) blocks the prefilter actually swept. */
+ * (64-row x 8-column) blocks the prefilter actually swept (each block is
+ * BSA_PF_BLOCK_PAIRS stage-1 pair tests). */
+#define BSA_PF_BLOCK_PAIRS 512
 int bsa_last_tiles(bsa_ctx *ctx, int64_t *kept, int64_t *total, int64_t *groups);
 
 /* Device time of the last detect's stages in milliseconds, measured with
