@@ -73,12 +73,16 @@ def main():
     ap.add_argument('--cd-every', type=int, default=1)
     ap.add_argument('--cpu-rows', type=int, default=256)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--reuse', type=float, nargs=2, default=None, metavar=('SIGMA_H', 'SIGMA_V'),
+                    help='candidate-list reuse budgets [m] (bsa_set_candidate_reuse); default off')
     args = ap.parse_args()
 
     rank, world, local = dist.env_rank_world()
     if world != args.gpus:
         world = max(world, 1)
     ctx = _lib.Context(local)
+    if args.reuse:
+        ctx.set_candidate_reuse(True, args.reuse[0], args.reuse[1])
     t = synth.workload(args.workload, n=args.n, seed=7)
     n = t.ntraf
     sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=args.cd_every),
@@ -138,6 +142,8 @@ def main():
                            rpz_m=synth.RPZ, hpz_m=synth.HPZ, tlookahead_s=synth.TLOOKAHEAD,
                            simdt_s=0.05, parallelism='rows%d' % world),
                sim_steps_per_s=args.steps / dt,
+               reuse=(dict(sigma_h_m=args.reuse[0], sigma_v_m=args.reuse[1], **ctx.reuse_stats())
+                      if args.reuse else None),
                roofline=roof,
                kernels_ms_rank0=dict(k0_prep=tm['prep'], prefilter=tm['prefilter'], exact=tm['exact'],
                                      k2_sort=tm['sort'], detect_total=tm['total']),

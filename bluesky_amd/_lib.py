@@ -52,6 +52,9 @@ SIGNATURES = {
                                        _c_i32p, _c_i32p, _c_u8p, _c_dp]),
     'bsa_last_candidates': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_last_tiles': (ctypes.c_int, [_vp, _c_i64p, _c_i64p, _c_i64p]),
+    'bsa_set_candidate_reuse': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_double]),
+    'bsa_reuse_stats': (ctypes.c_int, [_vp, _c_i64p, _c_i64p]),
+    'bsa_reuse_budget_use': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_timing_reset': (ctypes.c_int, [_vp]),
     'bsa_set_candidate_capacity': (ctypes.c_int, [_vp, ctypes.c_int64]),
@@ -255,6 +258,22 @@ class Context:
         """Candidate-list capacity for the next detects (grown on overflow)."""
         self.check(self.lib.bsa_set_candidate_capacity(self.h, int(capacity)),
                    'bsa_set_candidate_capacity')
+
+    def set_candidate_reuse(self, on=True, sigma_h=800.0, sigma_v=60.0):
+        """bsa_set_candidate_reuse: keep the candidate list across detects while
+        every aircraft's drift stays inside its budgets (exact either way)."""
+        self.check(self.lib.bsa_set_candidate_reuse(self.h, int(bool(on)), float(sigma_h), float(sigma_v)),
+                   'bsa_set_candidate_reuse')
+
+    def reuse_stats(self):
+        b, d = ctypes.c_int64(), ctypes.c_int64()
+        self.check(self.lib.bsa_reuse_stats(self.h, ctypes.byref(b), ctypes.byref(d)), 'bsa_reuse_stats')
+        return dict(builds=b.value, detects=d.value)
+
+    def reuse_budget_use(self):
+        u = np.zeros(2)
+        self.check(self.lib.bsa_reuse_budget_use(self.h, ptr(u)), 'bsa_reuse_budget_use')
+        return float(u[0]), float(u[1])
 
     def last_tiles(self):
         kept, total, groups = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

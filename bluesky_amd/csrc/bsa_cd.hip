@@ -136,7 +136,8 @@ __device__ __forceinline__ double reach_v(double hpz, double vs, double alt, dou
 // lo / hi = alt -/+ h rounded to fp32 (error
 // <= 1e-3 m at flight levels, inside h's 0.5 m + 1e-6 |alt| margin); a
 // non-finite h keeps the pair vertically (lo = -INF, hi = +INF).
-__device__ __forceinline__ PFRec make_pf(double px, double py, double pz, float s, double alt, double h) {
+__device__ __forceinline__ PFRec make_pf(double px, double py, double pz, float s, double alt, double h,
+                                         float sv = 0.f) {
   PFRec p;
   p.x = (float)px;
   p.y = (float)py;
@@ -150,7 +151,7 @@ __device__ __forceinline__ PFRec make_pf(double px, double py, double pz, float 
     p.hi = INFINITY;
   }
   p.alt = (float)alt;
-  p.pad = 0.f;
+  p.pad = sv;  // vertical budget of a reusable list (0 otherwise), read by the refine
   return p;
 }
 
@@ -201,53 +202,122 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   PV[k] = v;
 }
 
+// Candidate-list reuse.  A list built with every aircraft's
+// reach inflated by its budgets (horizontal sh, vertical sv) stays a superset
+// of the exact list while every aircraft's drift since the build stays inside
+// them: drift_h = |dchord| * kRS * L + |dvel| * T, drift_v = |dalt| + |dvs| * T
+// (L bounds the rotation of the refine's local basis, chord <= kRefineChord).
+struct ReuseParams {
+  const Snap *build;  // snapshot of the last build (nullptr: reuse off)
+  Snap *cur;          // this detect's state (becomes the snapshot on a build)
+  unsigned *ctl;      // [0] build flag (set here on a budget overrun), [1] detects since build
+  float *use;         // per wave: largest horizontal / vertical budget fraction used
+  float sh_chord;     // horizontal budget in chord units (added to the stage-1 reach)
+  double sh;          // horizontal budget [m, refine units]
+  double sv_default, sv_min, sv_max, ktarget;
+  int valid;          // the snapshot belongs to this perm / parameters
+};
+constexpr double kRefineChord = 0.03;  // the refine keeps (without refining) pairs with a longer chord
+
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
 __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__restrict__ perm,
                                                    SoA6 own, SoA6 intr, int distinct, int shared,
                                                    double rpz, double hpz, double tla,
                                                    ColRec *__restrict__ C, PFRec *__restrict__ PC,
-                                                   PFVel *__restrict__ PV) {
+                                                   PFVel *__restrict__ PV, ReuseParams rz) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= cnt) return;
-  const int o = (int)perm[k];
-  const double tlap = tla > 0.0 ? tla : 0.0;
-  const double la = intr.lat[o], lo = intr.lon[o];
-  const double rad = la * kD2R;
-  const double sinl = sin(rad), cosl = cos(rad);
-  const double trk = own.trk[o] * kD2R;
-  const double gs = own.gs[o];
-  const double olat = own.lat[o];
-  ColRec c;
-  c.lat = la;
-  c.lon = lo;
-  c.sinlat = sinl;
-  c.coslat = cosl;
-  c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);
-  c.u = gs * sin(trk);                           // StateBasedCD.py:31-32
-  c.v = gs * cos(trk);
-  c.alt = own.alt[o];
-  c.vs = own.vs[o];
-  c.eps = (olat == 0.0) ? 0.000001 : 0.0;       // geo.py:128 (column-indexed)
-  c.olat = olat;
-  for (int q = 0; q < 5; ++q) c.pad[q] = 0.0;
-  C[k] = c;
-  const double lor = lo * kD2R;
-  // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
-  // when own != intruder (geo.py:128): never prune such a column horizontally
-  // nor refine it.
-  const bool quirk = distinct && olat == 0.0;
-  const PFRec p = make_pf(cosl * cos(lor), cosl * sin(lor), sinl,
-                          quirk ? INFINITY : reach_h(rpz, gs, tlap), c.alt,
-                          reach_v(hpz, c.vs, c.alt, tlap));
-  PFVel v;
-  v.u = (float)c.u;
-  v.v = (float)c.v;
-  v.vs = (float)c.vs;
-  v.flags = (quirk || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) ? 1u : 0u;
-  // shared records also serve as rows: add the rows' pole flag (k_prep_rows)
-  if (shared && !(cosl > 1e-2)) v.flags = 1u;
-  PC[k] = p;
-  PV[k] = v;
+  bool over = false;       // reuse: this aircraft overran a budget
+  float use_h = 0.f, use_v = 0.f;
+  if (k < cnt) {
+    const int o = (int)perm[k];
+    const double tlap = tla > 0.0 ? tla : 0.0;
+    const double la = intr.lat[o], lo = intr.lon[o];
+    const double rad = la * kD2R;
+    const double sinl = sin(rad), cosl = cos(rad);
+    const double trk = own.trk[o] * kD2R;
+    const double gs = own.gs[o];
+    const double olat = own.lat[o];
+    ColRec c;
+    c.lat = la;
+    c.lon = lo;
+    c.sinlat = sinl;
+    c.coslat = cosl;
+    c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);
+    c.u = gs * sin(trk);                           // StateBasedCD.py:31-32
+    c.v = gs * cos(trk);
+    c.alt = own.alt[o];
+    c.vs = own.vs[o];
+    c.eps = (olat == 0.0) ? 0.000001 : 0.0;       // geo.py:128 (column-indexed)
+    c.olat = olat;
+    for (int q = 0; q < 5; ++q) c.pad[q] = 0.0;
+    C[k] = c;
+    const double lor = lo * kD2R;
+    // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
+    // when own != intruder (geo.py:128): never prune such a column horizontally
+    // nor refine it.
+    const bool quirk = distinct && olat == 0.0;
+    const double px = cosl * cos(lor), py = cosl * sin(lor), pz = sinl;
+    float sv = 0.f, sadd = 0.f;
+    if (rz.build) {  // reuse (shared records only): budget check against the last build
+      double svn = rz.sv_default;
+      if (rz.valid) {
+        const Snap b = rz.build[k];
+        const double dx = px - b.x, dy = py - b.y, dz = pz - b.z;
+        const double dch = sqrt(dx * dx + dy * dy + dz * dz);
+        const double rho = fmin(sqrt(px * px + py * py), sqrt(b.x * b.x + b.y * b.y));
+        // |dE| + |dN| <= (pi/2) |dr| (1 + 2 / rho): the refine basis turns with the row
+        const double L = 1.0 + 1.5708 * kRefineChord * (1.0 + 2.0 / rho);
+        const double du = c.u - b.u, dv = c.v - b.v;
+        const double dh = (dch * 6378137.0 * L + sqrt(du * du + dv * dv) * tlap) * 1.001 + 1e-3;
+        const double dvv = (fabs(c.alt - b.alt) + fabs(c.vs - b.vs) * tlap) * 1.001 + 1e-3;
+        over = !(dh <= rz.sh) || !(dvv <= (double)b.sv);  // (NaN -> rebuild)
+        use_h = (float)fmin(dh / rz.sh, 1e30);
+        use_v = (float)fmin(dvv / (double)b.sv, 1e30);
+        if (!(use_h >= 0.f)) use_h = 1e30f;
+        if (!(use_v >= 0.f)) use_v = 1e30f;
+        // next budget: this aircraft's vertical drift rate over ktarget detects
+        const double age = (double)rz.ctl[1] + 1.0;
+        svn = fmin(rz.sv_max, fmax(rz.sv_min, 2.0 * (dvv / age) * rz.ktarget));
+      }
+      sv = (float)svn;
+      Snap sn;
+      sn.x = px;
+      sn.y = py;
+      sn.z = pz;
+      sn.u = c.u;
+      sn.v = c.v;
+      sn.alt = c.alt;
+      sn.vs = c.vs;
+      sn.sv = sv;
+      sn.pad = 0.f;
+      rz.cur[k] = sn;
+      sadd = rz.sh_chord;
+    }
+    const PFRec p = make_pf(px, py, pz, quirk ? INFINITY : reach_h(rpz, gs, tlap) + sadd, c.alt,
+                            reach_v(hpz, c.vs, c.alt, tlap) + (double)sv, sv);
+    PFVel v;
+    v.u = (float)c.u;
+    v.v = (float)c.v;
+    v.vs = (float)c.vs;
+    v.flags = (quirk || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) ? 1u : 0u;
+    // shared records also serve as rows: add the rows' pole flag (k_prep_rows)
+    if (shared && !(cosl > 1e-2)) v.flags = 1u;
+    PC[k] = p;
+    PV[k] = v;
+  }
+  if (rz.build) {  // one store per wave, no atomics
+    const unsigned long long ob = __ballot(over);
+    for (int o = 32; o > 0; o >>= 1) {
+      use_h = fmaxf(use_h, __shfl_xor(use_h, o));
+      use_v = fmaxf(use_v, __shfl_xor(use_v, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      if (ob) rz.ctl[0] = 1u;
+      const int wv = k >> 6;
+      rz.use[2 * wv] = use_h;
+      rz.use[2 * wv + 1] = use_v;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ K0c tile boxes
@@ -285,6 +355,13 @@ __device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b)
   return u;
 }
 
+// Counters words that belong to the candidate list (kept across detects by reuse)
+__device__ __forceinline__ bool list_word(int k) {
+  constexpr int kCand = (int)(offsetof(Counters, cand) / 8), kTiles = (int)(offsetof(Counters, tiles) / 8);
+  constexpr int kGroups = (int)(offsetof(Counters, groups) / 8), kStamp = (int)(offsetof(Counters, stamp) / 8);
+  return k == kCand || k == kTiles || k == kGroups || k >= kStamp;
+}
+
 // one workgroup per tile, one wave per group (lane = record): 16-record
 // sub-group boxes to sbox (nullable), group boxes to gbox, their union to tbox
 __device__ __forceinline__ float xmin(float v, int o) { return fminf(v, __shfl_xor(v, o)); }
@@ -292,8 +369,15 @@ __device__ __forceinline__ float xmax(float v, int o) { return fmaxf(v, __shfl_x
 
 __global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restrict__ P,
                                                  TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
-                                                 TileBox *__restrict__ tbox) {
+                                                 TileBox *__restrict__ tbox, const unsigned *__restrict__ build,
+                                                 Counters *__restrict__ reset) {
   __shared__ TileBox gb[kGroupsPerTile];
+  if (build && !build[0]) return;  // reused candidate list: no sweep this detect
+  if (reset && blockIdx.x == 0) {  // reuse build: start from an empty candidate list
+    constexpr int kWords = (int)(sizeof(Counters) / 8);
+    for (int k = threadIdx.x; k < kWords; k += blockDim.x)
+      if (list_word(k)) reinterpret_cast<unsigned long long *>(reset)[k] = 0;
+  }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = blockIdx.x * kGroupsPerTile + w;
   const int k = g * kGroup + lane;
@@ -382,7 +466,9 @@ __device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileB
 __global__ __launch_bounds__(256) void k_tilepairs(int nrt, int nct, const TileBox *__restrict__ rb,
                                                    const TileBox *__restrict__ cb, int noprune,
                                                    uint2 *__restrict__ out,
-                                                   unsigned long long *__restrict__ count) {
+                                                   unsigned long long *__restrict__ count,
+                                                   const unsigned *__restrict__ build) {
+  if (build && !build[0]) return;
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = id < (long long)nrt * nct;
   bool keep = false;
@@ -460,7 +546,7 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, const float4 &cp,
                                           const float4 &cv, const RefineParams &prm) {
   const float dx = cp.x - rp.x, dy = cp.y - rp.y, dz = cp.z - rp.z;
-  if (dx * dx + dy * dy + dz * dz > 0.04f) return true;   // > ~1270 km: keep, no refine
+  if (dx * dx + dy * dy + dz * dz > (float)(kRefineChord * kRefineChord)) return true;  // > ~190 km: keep
   // chord projected on the row's local east / north basis
   //   e = (-y, x, 0) / rho,  n = (-z x / rho, -z y / rho, rho),  rho = cos(lat)
   // (from the fp32 unit vector; |lat| > ~89.4 deg rows are flagged)
@@ -473,6 +559,7 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
   const float vv = ve * ve + vn * vn;
   if (!(vv >= 4e-6f)) return true;                         // reference may clamp dv2; NaN
   const float dalt = cv.w - rv.w;                          // own.alt[j] - int.alt[i]
+  const float H = prm.H + (rp.w + cp.w);                   // + vertical budgets (reuse; else 0)
   const float dvs = cv.z - rv.z;
   const float adv = __builtin_fabsf(dvs);
   float t0 = 0.f, t1 = prm.T;
@@ -480,12 +567,12 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
   // window edge or the closest-approach time, and the margins below are
   // many orders of magnitude wider than 1 ulp
   if (adv < 1e-3f) {
-    if (__builtin_fabsf(dalt) >= prm.H + 1e-3f * prm.T + 2.f + 1e-5f * __builtin_fabsf(dalt)) return false;
+    if (__builtin_fabsf(dalt) >= H + 1e-3f * prm.T + 2.f + 1e-5f * __builtin_fabsf(dalt)) return false;
   } else {
     const float inv = __builtin_amdgcn_rcpf(dvs);
-    const float ta = (-prm.H - dalt) * inv, tb = (prm.H - dalt) * inv;
+    const float ta = (-H - dalt) * inv, tb = (H - dalt) * inv;
     const float lo = fminf(ta, tb), hi = fmaxf(ta, tb);
-    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + prm.H)) * __builtin_fabsf(inv) +
+    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + H)) * __builtin_fabsf(inv) +
                     1e-4f * fmaxf(__builtin_fabsf(lo), __builtin_fabsf(hi));
     t0 = fmaxf(lo - d, 0.f);
     t1 = fminf(hi + d, prm.T);
@@ -580,7 +667,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ sbox_c,
     const uint2 *__restrict__ tiles, Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
-    uint2 *__restrict__ cand, unsigned long long cap) {
+    uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ uint2 q2s[PF_WAVES][PF_Q2];
   __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
@@ -590,6 +677,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ float4 csv[PF_WAVES][64];      //                      u v vs alt    (refine)
   __shared__ unsigned cix[PF_WAVES][64];    //                      sorted column index
   __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:       u v vs alt    (refine)
+  if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned long long ntiles = cnt->tiles;
   unsigned short *q1 = q1s[w];
@@ -720,7 +808,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const float kr = 0.5f * A.s * A.s - 0.5f * (re_ * re_ + rn_ * rn_) + kPlaneMargin;
     const f2 K = {kr, kr};
     const f2 HI = {A.hi, A.hi}, LO = {A.lo, A.lo};
-    const float rx = A.x, ry = A.y, rz = A.z;
+    const float rx = A.x, ry = A.y, rz = A.z, rsig = A.pad;
     // the row of this lane for the refine (u = NaN: never refine)
     rv[lane] = make_float4(AV.flags ? qnan : AV.u, AV.v, AV.vs, A.alt);
     const unsigned rowmask = va ? 0xffu : 0u;
@@ -739,12 +827,13 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         const float px = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rx)));
         const float py = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(ry)));
         const float pz = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rz)));
+        const float psg = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rsig)));
         bool keep = false;
         unsigned gi = 0, gj = 0;
         if (k < n1) {
           gi = (unsigned)rbase + rl;
           gj = sci[cl];
-          keep = NOPRUNE ? true : pf_refine(make_float4(px, py, pz, 0.f), rv[rl], sx[cl], sv[cl], prm);
+          keep = NOPRUNE ? true : pf_refine(make_float4(px, py, pz, psg), rv[rl], sx[cl], sv[cl], prm);
         }
         const unsigned long long mk = __ballot(keep);
         if (mk) {
@@ -795,7 +884,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         sen[pb + 2] = cn;
         slh[pb] = nx.lo;
         slh[pb + 2] = nx.hi;
-        sx[lane] = make_float4(nx.x, nx.y, nx.z, 0.f);
+        sx[lane] = make_float4(nx.x, nx.y, nx.z, nx.pad);
         sv[lane] = make_float4(nv.flags ? qnan : nv.u, nv.v, nv.vs, nx.alt);
         sci[lane] = (unsigned)jn;
         colmask = __ballot(jn >= 0);
@@ -997,8 +1086,16 @@ __global__ __launch_bounds__(256) void k_exact(
     unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
     unsigned char *__restrict__ cflag, unsigned long long *__restrict__ ckey,
     double *__restrict__ cpay, unsigned char *__restrict__ inconf,
-    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int kwik) {
+    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int kwik,
+    unsigned *__restrict__ rctl, const Snap *__restrict__ snap_cur, Snap *__restrict__ snap_build, int nsnap) {
   if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
+  if (rctl) {  // reuse: after a build this detect's state becomes the snapshot
+    const bool built = rctl[0] != 0;
+    const int k0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (built)
+      for (int k = k0; k < nsnap; k += gridDim.x * blockDim.x) snap_build[k] = snap_cur[k];
+    if (k0 == 0) rctl[1] = built ? 0u : rctl[1] + 1u;
+  }
   unsigned long long pre[kCandShards + 1];
   const unsigned long long ncand = cand_prefix(cnt, cap, pre);
   const unsigned long long ccap = cap / kCandShards;
@@ -1128,7 +1225,8 @@ __global__ __launch_bounds__(256) void k_rowsort(int nrows, Counters *__restrict
                                                  int *__restrict__ cj, double *__restrict__ out,
                                                  int *__restrict__ li, int *__restrict__ lj,
                                                  unsigned long long *__restrict__ stats,
-                                                 unsigned long long *__restrict__ gate) {
+                                                 unsigned long long *__restrict__ gate,
+                                                 const unsigned *__restrict__ build) {
   const bool ovf = cand_overflow(cnt, cap);
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned P = rowoff[nrows], L = rowoff[2 * nrows + 1] - P;
@@ -1138,9 +1236,13 @@ __global__ __launch_bounds__(256) void k_rowsort(int nrows, Counters *__restrict
     cnt->conf = ovf ? 0 : P;
     cnt->los = ovf ? 0 : L;
     cnt->cand = ncand;
-    stats[0] += cnt->groups;
+    const bool built = !build || build[0];  // a reused list swept nothing this detect
+    if (built) {
+      stats[0] += cnt->groups;
+      stats[2] += cnt->tiles;
+      stats[4] += 1;
+    }
     stats[1] += ncand;
-    stats[2] += cnt->tiles;
     stats[3] += 1;
     if (gate) {
       gate[0] = ovf ? 1 : 0;
@@ -1164,9 +1266,11 @@ __global__ __launch_bounds__(256) void k_rowsort(int nrows, Counters *__restrict
                });
 }
 
-// Zero the per-detect state: counters (but `tiles` unless full), the dequeue
+// Zero the per-detect state: counters (but `tiles` unless full; with keep,
+// nothing of the candidate list: its counts, tiles and groups), the dequeue
 // shards and the per-row outputs / counts.  Grid-stride, one word per lane.
-__global__ __launch_bounds__(256) void k_zero(int nrows, int full, Counters *__restrict__ cnt,
+__global__ __launch_bounds__(256) void k_zero(int nrows, int full, int keep, unsigned *__restrict__ rctl,
+                                              int rforce, Counters *__restrict__ cnt,
                                               unsigned long long *__restrict__ work,
                                               unsigned char *__restrict__ inconf,
                                               unsigned long long *__restrict__ tcpamax,
@@ -1174,8 +1278,13 @@ __global__ __launch_bounds__(256) void k_zero(int nrows, int full, Counters *__r
   constexpr int kWords = (int)(sizeof(Counters) / 8);
   constexpr int kTilesWord = (int)(offsetof(Counters, tiles) / 8);
   const int m = max(max(2 * (nrows + 1), kWorkShards * kWorkStride), kWords);
+  if (rctl && blockIdx.x == 0 && threadIdx.x == 0) {  // reuse: build this detect? (force: age 0)
+    rctl[0] = rforce ? 1u : 0u;
+    if (rforce) rctl[1] = 0u;
+  }
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
-    if (k < kWords && (full || k != kTilesWord)) reinterpret_cast<unsigned long long *>(cnt)[k] = 0;
+    if (k < kWords && (full || k != kTilesWord) && !(keep && list_word(k)))
+      reinterpret_cast<unsigned long long *>(cnt)[k] = 0;
     if (k < kWorkShards * kWorkStride) work[k] = 0;
     if (k < nrows) {
       inconf[k] = 0;
@@ -1247,26 +1356,6 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->rowcnt, (size_t)(2 * (nrows + 1)) * 4, "row counts") ||
       !ensure(c, c->rowoff, (size_t)(2 * (nrows + 1)) * 4, "row offsets"))
     return -1;
-  hipEvent_t *ev = nullptr;
-  if (next_events(c, &ev)) return -1;
-  BSA_HIP(c, hipEventRecord(ev[0], c->stream));
-  Counters *dcnt = (Counters *)c->counters.p;
-  {
-    const int64_t m = std::max<int64_t>(2 * (nrows + 1), 256);
-    hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>(blocks_for(m, 256), 1024)), dim3(256), 0,
-                       c->stream, (int)nrows, 1, dcnt, (unsigned long long *)c->workq.p,
-                       (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
-                       (unsigned *)c->rowcnt.p);
-    BSA_HIP(c, hipGetLastError());
-  }
-  if (n == 0 || nrows == 0) {
-    if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
-    for (int e = 1; e < 5; ++e) BSA_HIP(c, hipEventRecord(ev[e], c->stream));
-    c->ev_valid = true;
-    c->empty_detect = true;
-    return 0;
-  }
-  c->empty_detect = false;
   const bool distinct = c->has_intruder;
   const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;
   // KWIK: stage 1 is exact-safe only with the pair's own mean latitude in
@@ -1274,6 +1363,34 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // is the great circle's: a distinct intruder set disables the prefilter,
   // and the refine keeps every stage-1 survivor.
   const int noprune = ((flags & BSA_FLAG_NOPRUNE) || (kwik && distinct)) ? 1 : 0;
+  // rows share the column order and records when own == intruder and the
+  // whole range is detected; only then can the candidate list be reused
+  const bool shared = !distinct && rb == 0 && re == n;
+  const bool reuse = c->reuse_on && shared && !noprune && !kwik && n > 0;
+  if (!reuse) c->reuse_valid = false;
+  hipEvent_t *ev = nullptr;
+  if (next_events(c, &ev)) return -1;
+  BSA_HIP(c, hipEventRecord(ev[0], c->stream));
+  Counters *dcnt = (Counters *)c->counters.p;
+  // K0z: zero the per-detect state (launched once the reuse decision is known)
+  auto zero = [&](bool keep, unsigned *rctl, int rforce) -> int {
+    const int64_t m = std::max<int64_t>(2 * (nrows + 1), 256);
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>(blocks_for(m, 256), 1024)), dim3(256), 0,
+                       c->stream, (int)nrows, 1, keep ? 1 : 0, rctl, rforce, dcnt,
+                       (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
+                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p);
+    BSA_HIP(c, hipGetLastError());
+    return 0;
+  };
+  if (n == 0 || nrows == 0) {
+    if (zero(false, nullptr, 0)) return -1;
+    if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
+    for (int e = 1; e < 5; ++e) BSA_HIP(c, hipEventRecord(ev[e], c->stream));
+    c->ev_valid = true;
+    c->empty_detect = true;
+    return 0;
+  }
+  c->empty_detect = false;
   DevBuf *I = distinct ? c->intr : c->own;
   SoA6 own{(const double *)c->own[0].p, (const double *)c->own[1].p, (const double *)c->own[2].p,
            (const double *)c->own[3].p, (const double *)c->own[4].p, (const double *)c->own[5].p};
@@ -1283,12 +1400,48 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // ---- K0a spatial order.  Any permutation gives identical results (the
   // output is re-sorted canonically), so the order is reused for up to
   // kResortEvery calls on the same shape: aircraft move ~km between calls,
-  // tiles span ~100 km.  Rows share the column order (and the records) when
-  // own == intruder and the whole range is detected.
-  const bool shared = !distinct && rb == 0 && re == n;
+  // tiles span ~100 km (with a reusable list: 64 calls, and every re-sort
+  // rebuilds the list).
   const bool resort = !c->perm_valid || c->perm_n != n || c->perm_rb != rb || c->perm_re != re ||
                       c->perm_shared != shared || c->perm_distinct != distinct ||
-                      (flags & BSA_FLAG_RESORT) || c->perm_age >= kResortEvery;
+                      (flags & BSA_FLAG_RESORT) || c->perm_age >= (reuse ? kResortEveryReuse : kResortEvery);
+  // ---- candidate-list reuse: the list of the last build stays valid for
+  // this perm / parameters / buffers unless an aircraft overran its budget
+  // (decided on the device by K0b; ctl[0] = build this detect)
+  if (c->cand_cap == 0)
+    c->cand_cap = (unsigned long long)kCandShards * (unsigned long long)std::max<int64_t>(1 << 17, 4 * nrows);
+  const unsigned long long cap = c->cand_cap;
+  if (!ensure(c, c->cand, cap * sizeof(uint2), "candidate pairs")) return -1;
+  ReuseParams rz{};
+  bool rvalid = false;
+  if (reuse) {
+    if (!ensure(c, c->snap_build, (size_t)n * sizeof(Snap), "reuse snapshot") ||
+        !ensure(c, c->snap_cur, (size_t)n * sizeof(Snap), "reuse state") ||
+        !ensure(c, c->reuse_use, (size_t)((n + 63) / 64) * 8, "reuse budget use") ||
+        !ensure(c, c->reuse_ctl, 16, "reuse control"))
+      return -1;
+    const double key[4] = {rpz, hpz, tla, (double)flags};
+    rvalid = c->reuse_valid && !resort && c->reuse_n == n && c->reuse_cap == cap &&
+             c->reuse_candp == c->cand.p && memcmp(key, c->reuse_key, sizeof key) == 0;
+    rz.build = (const Snap *)c->snap_build.p;
+    rz.cur = (Snap *)c->snap_cur.p;
+    rz.ctl = (unsigned *)c->reuse_ctl.p;
+    rz.use = (float *)c->reuse_use.p;
+    rz.sh = c->reuse_sh;
+    rz.sh_chord = (float)(c->reuse_sh / 6.3e6) * 1.000001f;
+    rz.sv_default = c->reuse_sv;
+    rz.sv_min = 1.0;
+    rz.sv_max = 4.0 * c->reuse_sv;
+    rz.ktarget = 16.0;
+    rz.valid = rvalid ? 1 : 0;
+    c->reuse_valid = true;  // optimistic: an overflow invalidates it (detect_finish / sim retry)
+    memcpy(c->reuse_key, key, sizeof key);
+    c->reuse_n = n;
+    c->reuse_cap = cap;
+    c->reuse_candp = c->cand.p;
+  }
+  const unsigned *build = reuse ? (const unsigned *)c->reuse_ctl.p : nullptr;
+  if (zero(reuse, reuse ? (unsigned *)c->reuse_ctl.p : nullptr, rvalid ? 0 : 1)) return -1;
   if (resort) {
     if (spatial_order(c, (int)n, 0, intr.lat, intr.lon, c->key_c, c->idx_c, c->key_c2, c->perm_c)) return -1;
     if (!shared &&
@@ -1306,6 +1459,14 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const unsigned *perm_r = (const unsigned *)(shared ? c->perm_c.p : c->perm_r.p);
   const unsigned *perm_c = (const unsigned *)c->perm_c.p;
 
+  // ---- buffers sized by the candidate capacity (every pair list <= candidates)
+  if (!ensure(c, c->cflag, cap, "candidate flags") || !ensure(c, c->ckey, cap * 8, "candidate keys") ||
+      !ensure(c, c->cpay, cap * 5 * 8, "candidate payload") ||
+      !ensure(c, c->ckey2, cap * 8, "conflict keys") || !ensure(c, c->cval2, cap * 4, "conflict slots") ||
+      !ensure(c, c->lkey2, cap * 8, "los keys") || !ensure(c, c->out_ci, cap * 4, "ci") ||
+      !ensure(c, c->out_cj, cap * 4, "cj") || !ensure(c, c->out_pay, cap * 5 * 8, "conflict outputs") ||
+      !ensure(c, c->out_li, cap * 4, "li") || !ensure(c, c->out_lj, cap * 4, "lj"))
+    return -1;
   // ---- K0b records in sorted order (shared: the column records serve as
   // row records too; RowRec and ColRec agree field for field up to `vs`)
   if (!ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
@@ -1327,8 +1488,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   }
   hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n, perm_c, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
-                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p);
+                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, rz);
   BSA_HIP(c, hipGetLastError());
+
   // ---- K0c/K0d group / tile boxes and the tile-pair work list
   const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
   const long long ntp = (long long)nrt * nct;
@@ -1346,28 +1508,17 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const TileBox *tbox_r = shared ? (const TileBox *)c->tbox_c.p : (const TileBox *)c->tbox_r.p;
   if (!shared)
     hipLaunchKernelGGL(k_boxes, dim3(nrt), dim3(kTile), 0, c->stream, (int)nrows, pfrow, (TileBox *)nullptr,
-                       (TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p);
+                       (TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p, build, (Counters *)nullptr);
   hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
-                     (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p);
+                     (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build,
+                     reuse ? dcnt : (Counters *)nullptr);
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + 255) / 256)), dim3(256), 0, c->stream, nrt, nct,
-                     tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p, &dcnt->tiles);
+                     tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p, &dcnt->tiles, build);
   BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(ev[1], c->stream));
 
-  // ---- buffers sized by the candidate capacity (every pair list <= candidates)
-  if (c->cand_cap == 0)
-    c->cand_cap = (unsigned long long)kCandShards * (unsigned long long)std::max<int64_t>(1 << 17, 4 * nrows);
-  const unsigned long long cap = c->cand_cap;
-  if (!ensure(c, c->cand, cap * sizeof(uint2), "candidate pairs") ||
-      !ensure(c, c->cflag, cap, "candidate flags") || !ensure(c, c->ckey, cap * 8, "candidate keys") ||
-      !ensure(c, c->cpay, cap * 5 * 8, "candidate payload") ||
-      !ensure(c, c->ckey2, cap * 8, "conflict keys") || !ensure(c, c->cval2, cap * 4, "conflict slots") ||
-      !ensure(c, c->lkey2, cap * 8, "los keys") || !ensure(c, c->out_ci, cap * 4, "ci") ||
-      !ensure(c, c->out_cj, cap * 4, "cj") || !ensure(c, c->out_pay, cap * 5 * 8, "conflict outputs") ||
-      !ensure(c, c->out_li, cap * 4, "li") || !ensure(c, c->out_lj, cap * 4, "lj"))
-    return -1;
   const float T = (float)(tla > 0.0 ? tla : 0.0);
-  const float lim = (float)((rpz + kEABS) / (1.0 - kE1));
+  const float lim = (float)((rpz + kEABS + (reuse ? 2.0 * c->reuse_sh : 0.0)) / (1.0 - kE1));
   const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : lim * lim};
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
@@ -1377,12 +1528,12 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
                        (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build);
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
                        (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build);
   BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(ev[2], c->stream));
   // ---- K1b exact evaluation: grid-stride over the device-side count, one
@@ -1391,7 +1542,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, cap, rpz, hpz, tla, (int)rb, (int)nrows,
                      (unsigned char *)c->cflag.p, (unsigned long long *)c->ckey.p, (double *)c->cpay.p,
                      (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
-                     (unsigned *)c->rowcnt.p, kwik);
+                     (unsigned *)c->rowcnt.p, kwik, reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
+                     (const Snap *)c->snap_cur.p, (Snap *)c->snap_build.p, (int)n);
   BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(ev[3], c->stream));
   // ---- K2: row offsets, scatter into row segments, per-row rank + gather
@@ -1413,7 +1565,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      (const unsigned *)c->rowoff.p, (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
                      (const double *)c->cpay.p, (unsigned long long *)c->lkey2.p, (int *)c->out_ci.p,
                      (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
-                     (unsigned long long *)c->stats.p, gate);
+                     (unsigned long long *)c->stats.p, gate, build);
   BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(ev[4], c->stream));
   c->ev_valid = true;
@@ -1439,6 +1591,7 @@ int detect_finish(Ctx *c, bool *retry) {
   }
   if (worst > c->cand_cap / kCandShards) {
     c->cand_cap = (unsigned long long)kCandShards * (worst + worst / 4 + 1024);
+    c->reuse_valid = false;
     *retry = true;
     return 0;
   }

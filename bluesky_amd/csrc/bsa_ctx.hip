@@ -142,7 +142,7 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
                         &c->gbox_r, &c->gbox_c, &c->sbox_c, &c->workq, &c->rowcnt, &c->rowoff, &c->lslot,
                         &c->cflag, &c->stats,
-                        &c->tilepairs};
+                        &c->tilepairs, &c->snap_build, &c->snap_cur, &c->reuse_ctl, &c->reuse_use};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);
   for (int k = 0; k < 6; ++k) {
@@ -247,6 +247,47 @@ int bsa_set_candidate_capacity(bsa_ctx *c, int64_t capacity) {
   const unsigned long long s = bsa::kCandShards;
   c->cand_cap = ((unsigned long long)capacity + s - 1) / s * s;
   if (c->bk_cap) c->bk_cap = (unsigned long long)capacity;  // resident-sim resopairs (grows the same way)
+  return 0;
+}
+
+int bsa_set_candidate_reuse(bsa_ctx *c, int on, double sigma_h, double sigma_v) {
+  if (!c) return -1;
+  if (on && !(sigma_h > 0.0 && sigma_h < 1e6 && sigma_v > 0.0 && sigma_v < 1e5))
+    return bsa::fail(c, "reuse budgets must be positive (sigma_h < 1000 km, sigma_v < 100 km)");
+  c->reuse_on = on != 0;
+  if (on) {
+    c->reuse_sh = sigma_h;
+    c->reuse_sv = sigma_v;
+  }
+  c->reuse_valid = false;  // the next detect builds
+  return 0;
+}
+
+int bsa_reuse_stats(bsa_ctx *c, int64_t *builds, int64_t *detects) {
+  if (!c || !builds || !detects) return -1;
+  unsigned long long st[8] = {0};
+  if (c->stats.p) {
+    BSA_HIP(c, hipSetDevice(c->device));
+    BSA_HIP(c, hipMemcpyAsync(st, c->stats.p, sizeof(st), hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  *builds = (int64_t)st[4];
+  *detects = (int64_t)st[3];
+  return 0;
+}
+
+int bsa_reuse_budget_use(bsa_ctx *c, double *use2) {
+  if (!c || !use2) return -1;
+  use2[0] = use2[1] = 0.0;
+  if (!c->reuse_use.p || c->reuse_n <= 0) return 0;
+  BSA_HIP(c, hipSetDevice(c->device));
+  std::vector<float> u((size_t)((c->reuse_n + 63) / 64) * 2);
+  BSA_HIP(c, hipMemcpyAsync(u.data(), c->reuse_use.p, u.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  for (size_t k = 0; k < u.size(); k += 2) {
+    use2[0] = std::max(use2[0], (double)u[k]);
+    use2[1] = std::max(use2[1], (double)u[k + 1]);
+  }
   return 0;
 }
 

@@ -77,6 +77,18 @@ struct alignas(16) PFVel {
 };
 static_assert(sizeof(PFVel) == 16, "PFVel must be 16 B");
 
+// Candidate-list reuse (BSA reuse mode): state of one
+// aircraft (sorted position) when the candidate list was last built, and its
+// vertical budget [m].  The unit vector and velocity are fp64.
+struct alignas(16) Snap {
+  double x, y, z;   // unit position vector
+  double u, v;      // gs * sin / cos(trk)
+  double alt, vs;
+  float sv;         // vertical budget of this build [m]
+  float pad;
+};
+static_assert(sizeof(Snap) == 64, "Snap must be 64 B");
+
 // axis-aligned bounds of a group / tile of sorted PFRecs (culling)
 struct alignas(16) TileBox {
   float lo[3], hi[3];   // unit-vector bounds
@@ -88,6 +100,7 @@ static_assert(sizeof(TileBox) == 48, "TileBox must be 48 B");
 
 constexpr int kTile = 512;  // rows per row block == columns per column tile
 constexpr int kResortEvery = 8;  // detect calls between spatial re-sorts
+constexpr int kResortEveryReuse = 64;  // ... with a reusable candidate list (a re-sort rebuilds it)
 constexpr int kEvSets = 4096;    // detect timing event sets kept between resets
 
 constexpr int kCandShards = 8;  // candidate list shards (one counter each, 128 B apart)
@@ -157,12 +170,22 @@ struct Ctx {
   int last_flags = 0;
   bool have_pairs = false;
 
+  // candidate-list reuse across detects (shared own == intruder only)
+  bool reuse_on = false;
+  double reuse_sh = 800.0, reuse_sv = 60.0;   // horizontal budget, default / max vertical budget [m]
+  bool reuse_valid = false;                   // a list + snapshot exist for the current perm / params
+  double reuse_key[4] = {0, 0, 0, 0};         // rpz hpz tla flags of the list
+  int64_t reuse_n = -1;
+  unsigned long long reuse_cap = 0;
+  void *reuse_candp = nullptr;
+  DevBuf snap_build, snap_cur, reuse_ctl, reuse_use;  // ctl: [0] build flag, [1] detects since build
+
   // detect timing: one set of 5 events per detect since the last reset
   std::vector<hipEvent_t> evpool;
   int ev_sets = 0, ev_last = 0;
   bool ev_valid = false;
   bool empty_detect = false;
-  DevBuf stats;  // accumulated per-detect statistics {groups, candidates, tiles, detects}
+  DevBuf stats;  // accumulated per-detect statistics {groups, candidates, tiles, detects, list builds}
 
   // MVP / kinematics staging (host-buffer entry points)
   DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl;

@@ -390,6 +390,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     BSA_HIP(c, hipStreamSynchronize(c->stream));
     if ((unsigned)ctl[0] == 0) break;
     // aborted at step base + done: the state is that of the step's start
+    c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
     const int64_t done = (int64_t)ctl[1];
     c->sim_steps = base + done;
     int64_t cds = 0;

@@ -115,6 +115,22 @@ int bsa_last_candidates(bsa_ctx *ctx, int64_t *n_candidates);
  * capacity (grown the same way). */
 int bsa_set_candidate_capacity(bsa_ctx *ctx, int64_t capacity);
 
+/* Candidate-list reuse across detects (own == intruder, whole row range, not
+ * KWIK / NOPRUNE).  A detect that builds the list inflates
+ * every aircraft's reach by a horizontal budget sigma_h [m] and a vertical
+ * budget (sigma_v [m] at first, then adapted per aircraft to its own drift
+ * rate, up to 4 sigma_v); later detects skip the sweep (K0c/K0d/K1a) and
+ * re-evaluate that list exactly, until some aircraft's drift since the build
+ * (position, velocity, altitude, vertical speed) exceeds its budget, a
+ * re-sort, a parameter change or an overflow -- checked on the device, so the
+ * results are identical to a full detect.  Off by default. */
+int bsa_set_candidate_reuse(bsa_ctx *ctx, int on, double sigma_h, double sigma_v);
+/* List builds and detects since the last bsa_timing_reset. */
+int bsa_reuse_stats(bsa_ctx *ctx, int64_t *builds, int64_t *detects);
+/* Largest fraction of its horizontal [0] / vertical [1] budget any aircraft
+ * had used at the last detect (> 1 triggered a build; 0 after a forced one). */
+int bsa_reuse_budget_use(bsa_ctx *ctx, double *use2);
+
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
  * bounding-box cull, the total number of tile pairs, and the number of
  * (64-row x 8-column) blocks the prefilter actually swept (each block is
