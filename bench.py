@@ -63,6 +63,48 @@ def cpu_baseline(t, rows_sample):
                           os.environ.get('OPENBLAS_NUM_THREADS', 'unset'), os.cpu_count()))
 
 
+def timed_steps(ctx, sim, warmup, steps):
+    """Run warmup + steps resident sim steps; the timed batch's wall time, max over ranks."""
+    sim.step(warmup)
+    ctx.allreduce_max([0.0])
+    ctx.sync()
+    ctx.timing_reset()
+    t0 = time.perf_counter()
+    sim.step(steps)
+    ctx.sync()
+    ctx.allreduce_max([0.0])
+    return float(ctx.allreduce_max([time.perf_counter() - t0])[0])
+
+
+def variants(ctx, t, rank, world, warmup):
+    """Secondary lines on the same workload (not the headline value):
+    - reference_cadence: CD + MVP every 20th step (asas_dt 1 s / simdt 0.05 s,
+      SURVEY.md 8d), kinematics every step;
+    - candidate_reuse: ASAS every step with the candidate list kept across
+      detects under per-aircraft drift budgets (bitwise equal
+      results, tests/test_gpu_reuse.py)."""
+    n = t.ntraf
+    out = {}
+    steps = 40
+    sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=20), ctx=ctx,
+                               rank=rank, world=world)
+    dt = timed_steps(ctx, sim, warmup, steps)
+    out['reference_cadence'] = dict(cd_every=20, steps=steps, ms_per_step=dt / steps * 1e3,
+                                    sim_steps_per_s=steps / dt)
+    sh, sv = 1500.0, 300.0
+    ctx.set_candidate_reuse(True, sh, sv)
+    try:
+        sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx,
+                                   rank=rank, world=world)
+        dt = timed_steps(ctx, sim, warmup, steps)
+        out['candidate_reuse'] = dict(sigma_h_m=sh, sigma_v_m=sv, steps=steps, ms_per_step=dt / steps * 1e3,
+                                      sim_steps_per_s=steps / dt, pair_evals_per_s=float(n) * n * steps / dt,
+                                      **ctx.reuse_stats())
+    finally:
+        ctx.set_candidate_reuse(False, sh, sv)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -75,6 +117,8 @@ def main():
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--reuse', type=float, nargs=2, default=None, metavar=('SIGMA_H', 'SIGMA_V'),
                     help='candidate-list reuse budgets [m] (bsa_set_candidate_reuse); default off')
+    ap.add_argument('--no-variants', action='store_true',
+                    help='skip the secondary lines (reference CD cadence, candidate-list reuse)')
     args = ap.parse_args()
 
     rank, world, local = dist.env_rank_world()
@@ -152,6 +196,8 @@ def main():
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),
                propagation=propagation, exact_fp64=exact_fp64)
+    if not args.no_variants and not args.reuse:
+        out['variants'] = variants(ctx, t, rank, world, args.warmup)
     if rank == 0 and world == 1 and not args.no_cpu:
         out['cpu_baseline'] = cpu_baseline(t, args.cpu_rows)
         out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']

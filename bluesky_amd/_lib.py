@@ -19,6 +19,7 @@ FLAG_WITH_DCPA = 1
 FLAG_NOPRUNE = 2
 FLAG_RESORT = 4
 FLAG_KWIK = 8
+FLAG_STAGE1_T0 = 16
 
 _c_dp = ctypes.POINTER(ctypes.c_double)
 _c_fp = ctypes.POINTER(ctypes.c_float)

@@ -72,10 +72,7 @@ __device__ __forceinline__ unsigned expand10(unsigned v) {
 // sub-groups cut from the sorted order have tighter boxes: ~15% fewer stage-1
 // pair tests than Morton order at the 100k box (tools/cull_sim.py).  Any order
 // gives identical results; only the culling efficiency depends on it.
-__device__ __forceinline__ unsigned curve_key(double latd, double lond) {
-  const double la = latd * kD2R, lo = lond * kD2R;
-  const double cl = cos(la);
-  const double p[3] = {cl * cos(lo), cl * sin(lo), sin(la)};
+__device__ __forceinline__ unsigned curve_key(const double p[3]) {
   unsigned X[3];
   for (int k = 0; k < 3; ++k) {
     if (!(p[k] == p[k]) || isinf(p[k])) return 0xffffffffu;
@@ -107,14 +104,28 @@ __device__ __forceinline__ unsigned curve_key(double latd, double lond) {
   return (expand10(X[0]) << 2) | (expand10(X[1]) << 1) | expand10(X[2]);
 }
 
+// f > 0 (midpoint stage 1): key of the stage-1 point m = p + f (u e + v n)
+// (make_pf_mid), so that sorted groups stay compact around the points the
+// boxes bound; any order gives identical results
 __global__ __launch_bounds__(256) void k_keys(int cnt, int base, const double *__restrict__ lat,
-                                              const double *__restrict__ lon,
+                                              const double *__restrict__ lon, const double *__restrict__ trk,
+                                              const double *__restrict__ gs, double f,
                                               unsigned *__restrict__ key,
                                               unsigned *__restrict__ idx) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const int o = base + k;
-  key[k] = curve_key(lat[o], lon[o]);
+  const double la = lat[o] * kD2R, lo = lon[o] * kD2R;
+  const double cl = cos(la), sl = sin(la), co = cos(lo), so = sin(lo);
+  double p[3] = {cl * co, cl * so, sl};
+  if (f > 0.0) {
+    const double t = trk[o] * kD2R, g = gs[o];
+    const double u = g * sin(t), v = g * cos(t);
+    const double m[3] = {p[0] + f * (-u * so - v * sl * co), p[1] + f * (u * co - v * sl * so), p[2] + f * (v * cl)};
+    if (isfinite(m[0]) && isfinite(m[1]) && isfinite(m[2]))
+      for (int q = 0; q < 3; ++q) p[q] = m[q];
+  }
+  key[k] = curve_key(p);
   idx[k] = (unsigned)o;
 }
 
@@ -155,6 +166,53 @@ __device__ __forceinline__ PFRec make_pf(double px, double py, double pz, float 
   return p;
 }
 
+// Midpoint stage 1.  A conflict or LoS of a pair needs a
+// t* in [0, T] (T = max(tla, 0)) with |D + dV t*| <= R and |dalt + dvs t*| <= H
+// in the reference's flat frame at the row (D: its dx / dy, dV: du / dv;
+// also when dv2 / dvs were clamped, see 3.2).  Hence |D + dV T/2| <= R + |dV| T/2
+// and |dalt + dvs T/2| <= H + |dvs| T/2: every aircraft is tested at its
+// position half-way through the look-ahead, m = p + (T/2) (u e + v n) / R_S
+// (e, n its own east / north unit vectors), with half the speed reach.  In
+// the row's tangent frame m_j - m_i = B_i (p_est + dV T/2) / R_S
+// + (T/2) (B_j - B_i) V_j / R_S - (1 - cos c) p_i, where p_est is the chord's
+// tangent part (the reference's D = sigma p_est, |1 - sigma| < 0.012 for the
+// chords involved), ||B_j - B_i|| <= chord (pi/2 + (1 + pi/2) / rho'), and
+// 1 - cos c = chord^2 / 2.  A conflicting pair has chord <= cmax (its dist is
+// <= R + (|V_i| + |V_j|) T with every |V| <= kVcap), so
+//   s = [(R/2 + |V| T/2)(1 + 1e-5) + 0.012 (R/2 + |V| T) + |V| (T/2) kb cmax] / 6.3e6
+//       + cmax^2 / 4 + 1e-6
+// per aircraft bounds |m_j - m_i| / 2 for every such pair.  Aircraft faster
+// than kVcap, with a non-finite velocity, or within cmax of a pole-ish
+// latitude (rho' = cos(lat) - cmax < 0.05) get s = INF (never pruned
+// horizontally).  Vertically a = alt + vs T/2, h = H/2 + (|vs| + 1.5e-6) T/2
+// (+ the same rounding margins as reach_v; 1.5e-6 covers the dvs clamp).
+constexpr double kVcap = 400.0;  // [m/s]
+__device__ __forceinline__ PFRec make_pf_mid(double px, double py, double pz, double sinl, double cosl,
+                                             double coslo, double sinlo, double u, double v, double gs,
+                                             double alt, double vs, double rpz, double hpz, double tlap) {
+  const double ag = fabs(gs) + 0.5e-3;
+  const double ht = 0.5 * tlap;
+  const double cmax = (rpz + (ag + kVcap + 0.5e-3) * tlap) * (1.0 + 1e-5) / 6.35e6;
+  const double rhop = cosl - cmax;
+  double mx = px, my = py, mz = pz;
+  float s = INFINITY;
+  if (fabs(gs) <= kVcap && isfinite(u) && isfinite(v) && rhop >= 0.05 && cmax <= 0.1) {
+    const double kb = 1.5707963267948966 + 2.5707963267948966 / rhop;
+    const double sm = ((0.5 * rpz + ag * ht) * (1.0 + 1e-5) + 0.012 * (0.5 * rpz + ag * tlap) +
+                       ag * ht * kb * cmax) / 6.3e6 + 0.25 * cmax * cmax + 1e-6;
+    const double f = ht / 6371000.0;
+    mx = px + f * (-u * sinlo - v * sinl * coslo);
+    my = py + f * (u * coslo - v * sinl * sinlo);
+    mz = pz + f * (v * cosl);
+    s = (sm < 0.5) ? (float)sm : INFINITY;
+  }
+  const double am = alt + vs * ht;
+  const double h = (0.5 * hpz + (fabs(vs) + 1.5e-6) * ht) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(am);
+  PFRec p = make_pf(mx, my, mz, s, am, h);
+  p.alt = (float)alt;
+  return p;
+}
+
 struct SoA6 {
   const double *lat, *lon, *trk, *gs, *alt, *vs;
 };
@@ -164,7 +222,8 @@ struct SoA6 {
 __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__restrict__ perm,
                                                    SoA6 own, SoA6 intr, double rpz, double hpz,
                                                    double tla, RowRec *__restrict__ R,
-                                                   PFRec *__restrict__ PR, PFVel *__restrict__ PV) {
+                                                   PFRec *__restrict__ PR, PFVel *__restrict__ PV,
+                                                   float4 *__restrict__ PP, int mid) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const int o = (int)perm[k];
@@ -189,8 +248,11 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   for (int q = 0; q < 5; ++q) r.pad[q] = 0.0;
   R[k] = r;
   const double lor = lo * kD2R;
-  const PFRec p = make_pf(cosl * cos(lor), cosl * sin(lor), sinl, reach_h(rpz, gs, tlap), r.alt,
-                          reach_v(hpz, r.vs, r.alt, tlap));
+  const double coslo = cos(lor), sinlo = sin(lor);
+  const double px = cosl * coslo, py = cosl * sinlo, pz = sinl;
+  const PFRec p = mid ? make_pf_mid(px, py, pz, sinl, cosl, coslo, sinlo, r.u, r.v, gs, r.alt, r.vs, rpz, hpz, tlap)
+                      : make_pf(px, py, pz, reach_h(rpz, gs, tlap), r.alt, reach_v(hpz, r.vs, r.alt, tlap));
+  PP[k] = make_float4((float)px, (float)py, (float)pz, 0.f);
   PFVel v;
   v.u = (float)r.u;
   v.v = (float)r.v;
@@ -224,7 +286,8 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
                                                    SoA6 own, SoA6 intr, int distinct, int shared,
                                                    double rpz, double hpz, double tla,
                                                    ColRec *__restrict__ C, PFRec *__restrict__ PC,
-                                                   PFVel *__restrict__ PV, ReuseParams rz) {
+                                                   PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
+                                                   ReuseParams rz) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
@@ -256,7 +319,8 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
     // when own != intruder (geo.py:128): never prune such a column horizontally
     // nor refine it.
     const bool quirk = distinct && olat == 0.0;
-    const double px = cosl * cos(lor), py = cosl * sin(lor), pz = sinl;
+    const double coslo = cos(lor), sinlo = sin(lor);
+    const double px = cosl * coslo, py = cosl * sinlo, pz = sinl;
     float sv = 0.f, sadd = 0.f;
     if (rz.build) {  // reuse (shared records only): budget check against the last build
       double svn = rz.sv_default;
@@ -293,8 +357,12 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
       rz.cur[k] = sn;
       sadd = rz.sh_chord;
     }
-    const PFRec p = make_pf(px, py, pz, quirk ? INFINITY : reach_h(rpz, gs, tlap) + sadd, c.alt,
+    // (midpoint mode is never combined with reuse: the host passes mid = 0 then)
+    PFRec p = mid ? make_pf_mid(px, py, pz, sinl, cosl, coslo, sinlo, c.u, c.v, gs, c.alt, c.vs, rpz, hpz, tlap)
+                  : make_pf(px, py, pz, reach_h(rpz, gs, tlap) + sadd, c.alt,
                             reach_v(hpz, c.vs, c.alt, tlap) + (double)sv, sv);
+    if (quirk) p.s = INFINITY;
+    PP[k] = make_float4((float)px, (float)py, (float)pz, 0.f);
     PFVel v;
     v.u = (float)c.u;
     v.v = (float)c.v;
@@ -662,8 +730,8 @@ template <bool NOPRUNE>
 #endif
 #define PF_OCC __attribute__((amdgpu_waves_per_eu(BSA_PF_WAVES_PER_EU, 8)))
 __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
-    const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, int nrows,
-    const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, int ncols,
+    const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, const float4 *__restrict__ pprow, int nrows,
+    const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, const float4 *__restrict__ ppcol, int ncols,
     const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ sbox_c,
     const uint2 *__restrict__ tiles, Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
@@ -743,10 +811,11 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       for (int t = 0; t < kSubsPerBatch && m; ++t) m &= m - 1;
       return m;
     };
-    auto load_col = [&](int j, PFRec &r, PFVel &v) {
+    auto load_col = [&](int j, PFRec &r, PFVel &v, float4 &q) {
       if (j >= 0) {
         r = pcol[j];
         v = vcol[j];
+        q = ppcol[j];
       } else {
         r.x = r.y = r.z = r.s = qnan;
         r.lo = INFINITY;
@@ -754,25 +823,30 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         r.alt = r.pad = 0.f;
         v.u = v.v = v.vs = qnan;
         v.flags = 1;
+        q = make_float4(qnan, qnan, qnan, 0.f);
       }
     };
     int jn = batch_col(gm);
     PFRec nx;
     PFVel nv;
-    load_col(jn, nx, nv);
+    float4 np;
+    load_col(jn, nx, nv, np);
 
     const int krow = rbase + lane;
     const bool va = krow < nrows;
     PFRec A;
     PFVel AV;
+    float4 AP;
     if (va) {
       A = prow[krow];
       AV = vrow[krow];
+      AP = pprow[krow];
     } else {
       A.x = A.y = A.z = A.s = A.alt = A.pad = 0.f;
       A.lo = A.hi = 0.f;
       AV.u = AV.v = AV.vs = 0.f;
       AV.flags = 1;
+      AP = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     // the item's plane: o = first row of the slice, E / N an orthonormal
     // tangent pair at o (any orthonormal pair is exact-safe; near a pole, or
@@ -808,7 +882,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const float kr = 0.5f * A.s * A.s - 0.5f * (re_ * re_ + rn_ * rn_) + kPlaneMargin;
     const f2 K = {kr, kr};
     const f2 HI = {A.hi, A.hi}, LO = {A.lo, A.lo};
-    const float rx = A.x, ry = A.y, rz = A.z, rsig = A.pad;
+    const float rx = AP.x, ry = AP.y, rz = AP.z, rsig = A.pad;  // refine: position at t = 0
     // the row of this lane for the refine (u = NaN: never refine)
     rv[lane] = make_float4(AV.flags ? qnan : AV.u, AV.v, AV.vs, A.alt);
     const unsigned rowmask = va ? 0xffu : 0u;
@@ -884,7 +958,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         sen[pb + 2] = cn;
         slh[pb] = nx.lo;
         slh[pb + 2] = nx.hi;
-        sx[lane] = make_float4(nx.x, nx.y, nx.z, nx.pad);
+        sx[lane] = make_float4(np.x, np.y, np.z, nx.pad);
         sv[lane] = make_float4(nv.flags ? qnan : nv.u, nv.v, nv.vs, nx.alt);
         sci[lane] = (unsigned)jn;
         colmask = __ballot(jn >= 0);
@@ -892,7 +966,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       gm = drop_batch(gm);
       if (gm) {  // prefetch the next batch while this one is swept
         jn = batch_col(gm);
-        load_col(jn, nx, nv);
+        load_col(jn, nx, nv, np);
       }
       // sweep only the chunks holding valid slots
       const int nchunk = colmask ? (64 - __builtin_clzll(colmask) + 7) >> 3 : 0;
@@ -1298,13 +1372,13 @@ __global__ __launch_bounds__(256) void k_zero(int nrows, int full, int keep, uns
 static inline unsigned blocks_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 // spatial sort of cnt positions starting at original index base -> perm
-static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const double *lon,
-                         DevBuf &key, DevBuf &idx, DevBuf &key2, DevBuf &perm) {
+static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const double *lon, const double *trk,
+                         const double *gs, double f, DevBuf &key, DevBuf &idx, DevBuf &key2, DevBuf &perm) {
   if (!ensure(c, key, (size_t)cnt * 4, "keys") || !ensure(c, idx, (size_t)cnt * 4, "key idx") ||
       !ensure(c, key2, (size_t)cnt * 4, "sorted keys") || !ensure(c, perm, (size_t)cnt * 4, "perm"))
     return -1;
-  hipLaunchKernelGGL(k_keys, dim3(blocks_for(cnt, 256)), dim3(256), 0, c->stream, cnt, base, lat, lon,
-                     (unsigned *)key.p, (unsigned *)idx.p);
+  hipLaunchKernelGGL(k_keys, dim3(blocks_for(cnt, 256)), dim3(256), 0, c->stream, cnt, base, lat, lon, trk, gs,
+                     f, (unsigned *)key.p, (unsigned *)idx.p);
   BSA_HIP(c, hipGetLastError());
   size_t tmp = 0;
   BSA_HIP(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (unsigned *)key.p, (unsigned *)key2.p,
@@ -1368,6 +1442,12 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const bool shared = !distinct && rb == 0 && re == n;
   const bool reuse = c->reuse_on && shared && !noprune && !kwik && n > 0;
   if (!reuse) c->reuse_valid = false;
+  // stage 1 at the look-ahead midpoints: its bound is derived
+  // for the great-circle geometry and fixed reaches, so not with KWIK nor with
+  // the reuse budgets (whose drift checks assume t = 0 points); the
+  // BSA_STAGE1_T0 environment variable selects t = 0 for A/B measurements
+  static const bool t0_env = getenv("BSA_STAGE1_T0") && atoi(getenv("BSA_STAGE1_T0")) != 0;
+  const int mid = (!reuse && !kwik && !(flags & BSA_FLAG_STAGE1_T0) && !t0_env) ? 1 : 0;
   hipEvent_t *ev = nullptr;
   if (next_events(c, &ev)) return -1;
   BSA_HIP(c, hipEventRecord(ev[0], c->stream));
@@ -1402,8 +1482,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // kResortEvery calls on the same shape: aircraft move ~km between calls,
   // tiles span ~100 km (with a reusable list: 64 calls, and every re-sort
   // rebuilds the list).
+  const double kf = mid ? 0.5 * (tla > 0.0 ? tla : 0.0) / 6371000.0 : 0.0;  // k_keys midpoint factor
   const bool resort = !c->perm_valid || c->perm_n != n || c->perm_rb != rb || c->perm_re != re ||
-                      c->perm_shared != shared || c->perm_distinct != distinct ||
+                      c->perm_shared != shared || c->perm_distinct != distinct || c->perm_f != kf ||
                       (flags & BSA_FLAG_RESORT) || c->perm_age >= (reuse ? kResortEveryReuse : kResortEvery);
   // ---- candidate-list reuse: the list of the last build stays valid for
   // this perm / parameters / buffers unless an aircraft overran its budget
@@ -1443,10 +1524,14 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const unsigned *build = reuse ? (const unsigned *)c->reuse_ctl.p : nullptr;
   if (zero(reuse, reuse ? (unsigned *)c->reuse_ctl.p : nullptr, rvalid ? 0 : 1)) return -1;
   if (resort) {
-    if (spatial_order(c, (int)n, 0, intr.lat, intr.lon, c->key_c, c->idx_c, c->key_c2, c->perm_c)) return -1;
-    if (!shared &&
-        spatial_order(c, (int)nrows, (int)rb, own.lat, own.lon, c->key_r, c->idx_r, c->key_r2, c->perm_r))
+    // columns: intruder position, own velocity; rows: own position, intruder velocity
+    if (spatial_order(c, (int)n, 0, intr.lat, intr.lon, own.trk, own.gs, kf, c->key_c, c->idx_c, c->key_c2,
+                      c->perm_c))
       return -1;
+    if (!shared && spatial_order(c, (int)nrows, (int)rb, own.lat, own.lon, intr.trk, intr.gs, kf, c->key_r,
+                                 c->idx_r, c->key_r2, c->perm_r))
+      return -1;
+    c->perm_f = kf;
     c->perm_valid = true;
     c->perm_n = n;
     c->perm_rb = rb;
@@ -1471,24 +1556,27 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // row records too; RowRec and ColRec agree field for field up to `vs`)
   if (!ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
       !ensure(c, c->pfcol, n * sizeof(PFRec), "prefilter columns") ||
-      !ensure(c, c->pfvcol, n * sizeof(PFVel), "prefilter column velocities"))
+      !ensure(c, c->pfvcol, n * sizeof(PFVel), "prefilter column velocities") ||
+      !ensure(c, c->pfpcol, n * sizeof(float4), "prefilter column positions"))
     return -1;
   if (!shared && (!ensure(c, c->rowrec, nrows * sizeof(RowRec), "row records") ||
                   !ensure(c, c->pfrow, nrows * sizeof(PFRec), "prefilter rows") ||
-                  !ensure(c, c->pfvrow, nrows * sizeof(PFVel), "prefilter row velocities")))
+                  !ensure(c, c->pfvrow, nrows * sizeof(PFVel), "prefilter row velocities") ||
+                  !ensure(c, c->pfprow, nrows * sizeof(float4), "prefilter row positions")))
     return -1;
   const RowRec *rowrec = shared ? (const RowRec *)c->colrec.p : (const RowRec *)c->rowrec.p;
   const PFRec *pfrow = shared ? (const PFRec *)c->pfcol.p : (const PFRec *)c->pfrow.p;
   const PFVel *pfvrow = shared ? (const PFVel *)c->pfvcol.p : (const PFVel *)c->pfvrow.p;
+  const float4 *pfprow = shared ? (const float4 *)c->pfpcol.p : (const float4 *)c->pfprow.p;
   if (!shared) {
     hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows,
                        perm_r, own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p, (PFRec *)c->pfrow.p,
-                       (PFVel *)c->pfvrow.p);
+                       (PFVel *)c->pfvrow.p, (float4 *)c->pfprow.p, mid);
     BSA_HIP(c, hipGetLastError());
   }
   hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n, perm_c, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
-                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, rz);
+                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz);
   BSA_HIP(c, hipGetLastError());
 
   // ---- K0c/K0d group / tile boxes and the tile-pair work list
@@ -1525,13 +1613,15 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const unsigned pf_grid = (unsigned)std::max<long long>(
       kWorkShards, std::min<long long>(ntp * PF_ITEMS_PER_TILE / PF_WAVES + 1, 256 * PF_BLOCKS_PER_CU));
   if (noprune)
-    hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
-                       (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
+    hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
+                       (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
+                       (const float4 *)c->pfpcol.p, (int)n, gbox_r,
                        (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build);
   else
-    hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow,
-                       (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p, (int)n, gbox_r,
+    hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
+                       (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
+                       (const float4 *)c->pfpcol.p, (int)n, gbox_r,
                        (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build);
   BSA_HIP(c, hipGetLastError());

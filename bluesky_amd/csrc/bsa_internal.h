@@ -57,15 +57,18 @@ static_assert(sizeof(RowRec) == 128, "RowRec must be one cache line");
 static_assert(sizeof(ColRec) == 128, "ColRec must be one cache line");
 
 // fp32 prefilter record (32 B), one per sorted row / column.
-// Stage 1 keeps a pair iff chord < s_i + s_j (tested in a plane, see
-// k_prefilter) and lo_j < hi_i and hi_j > lo_i (<=> |alt_j - alt_i| < h_i + h_j).
+// Stage 1 keeps a pair iff |x_i - x_j| < s_i + s_j (tested in a plane, see
+// k_prefilter) and lo_j < hi_i and hi_j > lo_i (<=> |a_j - a_i| < h_i + h_j).
+// x / a are the position / altitude at t = 0, or (midpoint mode, DESIGN.md
+// 3.2b) at t = tla/2 along the velocity, with the reaches to match.
 struct alignas(16) PFRec {
-  float x, y, z;   // unit vector of the position
+  float x, y, z;   // stage-1 point (unit-sphere units)
   float s;         // horizontal reach, chord units (half of the pair bound); INF = always
-  float lo, hi;    // alt -/+ h, h = vertical reach [m] (half of the pair bound)
-  float alt;       // altitude [m]
+  float lo, hi;    // a -/+ h, h = vertical reach [m] (half of the pair bound)
+  float alt;       // altitude [m] at t = 0 (refine)
   float pad;
 };
+// The refine's position (PFPos, float4 x y z 0): the unit vector at t = 0.
 static_assert(sizeof(PFRec) == 32, "PFRec must be 32 B");
 
 // velocity part, read only by the CPA refine (rows and columns)
@@ -139,13 +142,14 @@ struct Ctx {
   bool has_intruder = false;
   DevBuf own[6];   // lat lon trk gs alt vs
   DevBuf intr[6];
-  DevBuf rowrec, colrec, pfrow, pfcol, pfvrow, pfvcol;
+  DevBuf rowrec, colrec, pfrow, pfcol, pfvrow, pfvcol, pfprow, pfpcol;
   // spatial order: Morton keys and the sorted-position -> original-index maps
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
   DevBuf tbox_r, tbox_c, gbox_r, gbox_c, sbox_c, tilepairs, workq;
   DevBuf rowcnt, rowoff, lslot;  // K2 counting sort
   // reusable spatial order (any permutation gives identical results)
   bool perm_valid = false, perm_shared = false, perm_distinct = false;
+  double perm_f = 0.0;  // midpoint factor the spatial order was computed with (k_keys)
   int64_t perm_n = 0, perm_rb = 0, perm_re = 0, perm_age = 0;
 
   // detect buffers

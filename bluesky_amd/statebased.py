@@ -34,13 +34,14 @@ def _upload(ctx, ownship, intruder):
 
 
 def detect_indices(ownship, intruder, RPZ, HPZ, tlookahead, with_dcpa=False, ctx=None,
-                   row_begin=0, row_end=-1, noprune=False, kwik=False):
+                   row_begin=0, row_end=-1, noprune=False, kwik=False, stage1_t0=False):
     """Index-array form: dict(ci, cj, qdr, dist, tcpa, tinconf[, dcpa], li, lj, inconf, tcpamax).
-    ``kwik=True``: the opt-in flat-earth variant (``bluesky_amd.kwik``)."""
+    ``kwik=True``: the opt-in flat-earth variant (``bluesky_amd.kwik``).
+    ``noprune`` / ``stage1_t0``: test aids selecting other (result-identical) culling."""
     ctx = ctx or _lib.default_context()
     _upload(ctx, ownship, intruder)
     flags = ((_lib.FLAG_WITH_DCPA if with_dcpa else 0) | (_lib.FLAG_NOPRUNE if noprune else 0) |
-             (_lib.FLAG_KWIK if kwik else 0))
+             (_lib.FLAG_KWIK if kwik else 0) | (_lib.FLAG_STAGE1_T0 if stage1_t0 else 0))
     nc, nl = ctx.detect(RPZ, HPZ, tlookahead, flags, row_begin, row_end)
     return ctx.fetch_pairs(nc, nl, with_dcpa)
 

@@ -44,6 +44,9 @@ typedef struct bsa_ctx bsa_ctx;
 #define BSA_FLAG_KWIK      8 /* opt-in flat-earth variant: geo.kwikqdrdist_matrix
                                 (geo.py:347-363) replaces qdrdist_matrix in StateBasedCD.detect, its
                                 metre distance passed on in nm; qdr in [0, 360) */
+#define BSA_FLAG_STAGE1_T0 16 /* test aid: prefilter stage 1 at the t = 0 positions with the full
+                                look-ahead reach instead of the look-ahead midpoints (DESIGN.md
+                                3.2b); results are identical, only the culling differs */
 
 /* ---------------------------------------------------------------- lifecycle */
 

@@ -23,14 +23,28 @@ def test_detect_matches_reference_golden(ctx, path):
 
 @pytest.mark.parametrize('path', CD, ids=[util.case_name(p) for p in CD])
 def test_prefilter_is_exact_safe_on_golden(ctx, path):
-    """Pruned and unpruned (every pair evaluated) runs give identical results."""
+    """Pruned (midpoint and t = 0 stage 1) and unpruned (every pair evaluated)
+    runs give identical results."""
     own, intr, z = util.load_cd(path)
     a = statebased.detect_indices(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']), ctx=ctx)
     b = statebased.detect_indices(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']),
                                   ctx=ctx, noprune=True)
+    c = statebased.detect_indices(own, intr, float(z['rpz']), float(z['hpz']), float(z['tla']),
+                                  ctx=ctx, stage1_t0=True)
     for k in a:
         if a[k] is not None:
             assert np.array_equal(a[k], b[k]), k
+            assert np.array_equal(a[k], c[k]), k
+
+
+def test_midpoint_stage1_stress_sets_vs_oracle(ctx):
+    """Fast high-latitude traffic, long look-ahead, a big zone, own != intruder
+    (tests/test_stage1_bound.py checks the bound itself on the same sets)."""
+    from tests.test_stage1_bound import _stress_sets
+    for name, own, intr, rpz, hpz, tla in _stress_sets():
+        got = statebased.detect_indices(own, intr, rpz, hpz, tla, ctx=ctx)
+        exp = ocd.detect_arrays(own, intr, rpz, hpz, tla)
+        util.assert_detect_equal(got, exp, rpz, tla)
 
 
 def test_tuple_contract(ctx):
