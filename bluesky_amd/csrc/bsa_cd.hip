@@ -1211,8 +1211,8 @@ __global__ __launch_bounds__(256) void k_exact(
 // Per-row counting sort.  rowcnt holds [conflicts per row | 0 | LoS per row | 0]
 // (2 (nrows + 1) words); its exclusive scan rowoff gives each row's segment
 // in the conflict list and (minus P) in the LoS list.  k_scatter drops every
-// pair's key into its row segment (in any order); k_rowsort ranks each row's
-// short segment by column in registers, so the lists come out exactly in
+// pair's key into its row segment (in any order); k_rank ranks every entry
+// among its row segment's columns, so the lists come out exactly in
 // np.where's row-major order (StateBasedCD.py:93-95).  All counts are read on
 // the device (no host round trip inside a detect), and nothing is written
 // when the candidate list overflowed: the caller retries with more room.
@@ -1247,64 +1247,30 @@ __global__ __launch_bounds__(256) void k_scatter(const Counters *__restrict__ cn
   }
 }
 
-constexpr int kRankMax = 16;  // segments up to this length are ranked in registers
-
-// rank the keys of segment [b, e) (one row: the column is the low word) and
-// hand each entry's final index to emit(entry, index)
-template <typename Emit>
-__device__ __forceinline__ void rank_segment(unsigned b, unsigned e, unsigned long long *__restrict__ key,
-                                             unsigned *__restrict__ slot, Emit emit) {
-  const unsigned n = e - b;
-  if (n == 0) return;
-  if (n <= (unsigned)kRankMax) {
-    unsigned col[kRankMax];
-#pragma unroll
-    for (int i = 0; i < kRankMax; ++i) col[i] = (unsigned)i < n ? (unsigned)key[b + i] : 0xffffffffu;
-#pragma unroll
-    for (int i = 0; i < kRankMax; ++i) {
-      if ((unsigned)i < n) {
-        unsigned rank = 0;
-#pragma unroll
-        for (int j = 0; j < kRankMax; ++j) rank += (col[j] < col[i]) ? 1u : 0u;
-        emit(b + (unsigned)i, b + rank);
-      }
-    }
-    return;
-  }
-  // long segment (rare): insertion sort in place, then emit in order
-  for (unsigned x = b + 1; x < e; ++x) {
-    const unsigned long long kv = key[x];
-    const unsigned sv = slot ? slot[x] : 0u;
-    unsigned y = x;
-    while (y > b && (unsigned)key[y - 1] > (unsigned)kv) {
-      key[y] = key[y - 1];
-      if (slot) slot[y] = slot[y - 1];
-      --y;
-    }
-    key[y] = kv;
-    if (slot) slot[y] = sv;
-  }
-  for (unsigned x = b; x < e; ++x) emit(x, x);
-}
-
-// One lane per row.  Block 0 / lane 0 also publishes the detect's totals:
-// cnt->conf / los, the accumulated statistics and the gate words
+// One lane per pair slot of the scattered lists (grid-stride over P + L, the
+// device-side counts): the slot's rank among its row segment's columns (the
+// segment is short: ~1.5 pairs per row at the 100k box; any length works)
+// is its final index, so ci / cj / payload (conflicts) and li / lj (LoS)
+// come out exactly in np.where's row-major order.  Every lane issues its
+// segment loads independently: ~4 dependent memory round trips per detect
+// instead of a per-row chain.  Block 0 / lane 0 also publishes the detect's
+// totals: cnt->conf / los, the accumulated statistics and the gate words
 // (gate[0] = overflow, gate[1] = P) the resident sim step reads.
-__global__ __launch_bounds__(256) void k_rowsort(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
-                                                 const unsigned *__restrict__ rowoff,
-                                                 unsigned long long *__restrict__ skey,
-                                                 unsigned *__restrict__ sslot,
-                                                 const double *__restrict__ cpay,
-                                                 unsigned long long *__restrict__ lkey, int *__restrict__ ci,
-                                                 int *__restrict__ cj, double *__restrict__ out,
-                                                 int *__restrict__ li, int *__restrict__ lj,
-                                                 unsigned long long *__restrict__ stats,
-                                                 unsigned long long *__restrict__ gate,
-                                                 const unsigned *__restrict__ build) {
+__global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
+                                              const unsigned *__restrict__ rowoff,
+                                              const unsigned long long *__restrict__ skey,
+                                              const unsigned *__restrict__ sslot,
+                                              const double *__restrict__ cpay,
+                                              const unsigned long long *__restrict__ lkey, int rb,
+                                              int *__restrict__ ci, int *__restrict__ cj, double *__restrict__ out,
+                                              int *__restrict__ li, int *__restrict__ lj,
+                                              unsigned long long *__restrict__ stats,
+                                              unsigned long long *__restrict__ gate,
+                                              const unsigned *__restrict__ build) {
   const bool ovf = cand_overflow(cnt, cap);
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned P = rowoff[nrows], L = rowoff[2 * nrows + 1] - P;
-  if (r == 0) {
+  const unsigned t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t0 == 0) {
     unsigned long long pre[kCandShards + 1];
     const unsigned long long ncand = cand_prefix(cnt, cap, pre);
     cnt->conf = ovf ? 0 : P;
@@ -1323,21 +1289,32 @@ __global__ __launch_bounds__(256) void k_rowsort(int nrows, Counters *__restrict
       gate[1] = ovf ? 0 : P;
     }
   }
-  if (ovf || r >= nrows) return;
-  rank_segment(rowoff[r], rowoff[r + 1], skey, sslot, [&](unsigned x, unsigned pos) {
-    const unsigned long long kk = skey[x];
-    const unsigned v = sslot[x];
-    ci[pos] = (int)(kk >> 32);
-    cj[pos] = (int)(kk & 0xffffffffull);
+  if (ovf) return;
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned x = t0; x < P + L; x += stride) {
+    const bool conf = x < P;
+    const unsigned long long *keys = conf ? skey : lkey;
+    const unsigned xl = conf ? x : x - P;
+    const unsigned long long kk = keys[xl];
+    const int row = (int)(kk >> 32) - rb;
+    const unsigned col = (unsigned)kk;
+    const unsigned base = conf ? 0u : P;
+    const unsigned b = rowoff[(conf ? 0 : nrows + 1) + row] - base;
+    const unsigned e = rowoff[(conf ? 1 : nrows + 2) + row] - base;
+    unsigned rank = 0;
+    for (unsigned y = b; y < e; ++y) rank += ((unsigned)keys[y] < col) ? 1u : 0u;
+    const unsigned pos = b + rank;
+    if (conf) {
+      const unsigned v = sslot[xl];
+      ci[pos] = (int)(kk >> 32);
+      cj[pos] = (int)col;
 #pragma unroll
-    for (int f = 0; f < 5; ++f) out[(size_t)f * P + pos] = cpay[f * cap + v];
-  });
-  rank_segment(rowoff[nrows + 1 + r] - P, rowoff[nrows + 2 + r] - P, lkey, nullptr,
-               [&](unsigned x, unsigned pos) {
-                 const unsigned long long kk = lkey[x];
-                 li[pos] = (int)(kk >> 32);
-                 lj[pos] = (int)(kk & 0xffffffffull);
-               });
+      for (int f = 0; f < 5; ++f) out[(size_t)f * P + pos] = cpay[f * cap + v];
+    } else {
+      li[pos] = (int)(kk >> 32);
+      lj[pos] = (int)col;
+    }
+  }
 }
 
 // Zero the per-detect state: counters (but `tiles` unless full; with keep,
@@ -1651,10 +1628,11 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
                      (unsigned long long *)c->lkey2.p);
   BSA_HIP(c, hipGetLastError());
-  hipLaunchKernelGGL(k_rowsort, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
-                     (const unsigned *)c->rowoff.p, (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
-                     (const double *)c->cpay.p, (unsigned long long *)c->lkey2.p, (int *)c->out_ci.p,
-                     (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
+  hipLaunchKernelGGL(k_rank, dim3(256 * 4), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
+                     (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey2.p,
+                     (const unsigned *)c->cval2.p, (const double *)c->cpay.p,
+                     (const unsigned long long *)c->lkey2.p, (int)rb, (int *)c->out_ci.p, (int *)c->out_cj.p,
+                     (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
                      (unsigned long long *)c->stats.p, gate, build);
   BSA_HIP(c, hipGetLastError());
   BSA_HIP(c, hipEventRecord(ev[4], c->stream));
