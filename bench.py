@@ -105,6 +105,28 @@ def variants(ctx, t, rank, world, warmup):
     return out
 
 
+def geo_matrix_line(ctx, t, m=8192):
+    """Secondary line: the standalone qdrdist_matrix / kwikqdrdist_matrix
+    producers (bsa_qdrdist) on an m x m same-set matrix of the
+    workload's first m aircraft.  HBM-write-bound: 16 B algorithmic bytes per
+    entry (qdr + dist fp64; the 2 x 8 B point vectors are L2-resident), timed
+    with HIP events around the producing kernel alone (the PCIe copy of the
+    result to the host is not part of it)."""
+    out = {}
+    lat, lon = t.lat[:m], t.lon[:m]
+    for name, kwik in (('qdrdist_matrix', False), ('kwikqdrdist_matrix', True)):
+        ms = []
+        for _ in range(3):
+            ctx.qdrdist(lat, lon, lat, lon, kwik=kwik)
+            ms.append(ctx.geo_last_ms())
+        best = min(ms)
+        gbps = 16.0 * m * m / (best * 1e-3) / 1e9
+        out[name] = dict(m=m, n=m, kernel_ms=best, entries_per_s=m * m / (best * 1e-3),
+                         algorithmic_bytes=16 * m * m, achieved_GBps=gbps, peak_GBps=HBM_PEAK_GBPS,
+                         frac=gbps / HBM_PEAK_GBPS)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -198,6 +220,8 @@ def main():
                propagation=propagation, exact_fp64=exact_fp64)
     if not args.no_variants and not args.reuse:
         out['variants'] = variants(ctx, t, rank, world, args.warmup)
+        if rank == 0:
+            out['variants']['geo_matrix'] = geo_matrix_line(ctx, t)
     if rank == 0 and world == 1 and not args.no_cpu:
         out['cpu_baseline'] = cpu_baseline(t, args.cpu_rows)
         out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']

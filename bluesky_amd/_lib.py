@@ -20,6 +20,8 @@ FLAG_NOPRUNE = 2
 FLAG_RESORT = 4
 FLAG_KWIK = 8
 FLAG_STAGE1_T0 = 16
+GEO_KWIK = 1
+GEO_PAIRWISE = 2
 
 _c_dp = ctypes.POINTER(ctypes.c_double)
 _c_fp = ctypes.POINTER(ctypes.c_float)
@@ -118,6 +120,16 @@ class SimOut(ctypes.Structure):
     _fields_ = [(k, _c_dp) for k in SIM_OUT_FIELDS] + [('active', _c_u8p)]
 
 
+ACDATA_F64 = ('lat', 'lon', 'alt', 'tas', 'cas', 'gs', 'trk', 'vs', 'tcpamax')
+ACDATA_COUNTS = ('nconf_cur', 'nconf_tot', 'nlos_cur', 'nlos_tot')
+
+
+class AcData(ctypes.Structure):
+    """bsa_acdata (include/bsaccel.h)."""
+    _fields_ = ([(k, ctypes.c_int64) for k in ('steps', 'row_begin', 'row_end') + ACDATA_COUNTS] +
+                [(k, _c_dp) for k in ACDATA_F64] + [('inconf', _c_u8p), ('asasn', _c_fp), ('asase', _c_fp)])
+
+
 SIGNATURES.update({
     'bsa_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
     'bsa_comm_init': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
@@ -130,6 +142,11 @@ SIGNATURES.update({
     'bsa_sim_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_asas_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_resopairs': (ctypes.c_int, [_vp, _c_i32p, _c_i32p, ctypes.c_int64, _c_i64p]),
+    'bsa_qdrdist': (ctypes.c_int, [_vp, ctypes.c_int64, _c_dp, _c_dp, ctypes.c_int64, _c_dp, _c_dp,
+                                   ctypes.c_int, _c_dp, _c_dp]),
+    'bsa_geo_last_ms': (ctypes.c_int, [_vp, _c_dp]),
+    'bsa_sim_acdata_request': (ctypes.c_int, [_vp]),
+    'bsa_sim_acdata_poll': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(AcData)]),
 })
 
 UNIQUE_ID_BYTES = 128
@@ -249,6 +266,48 @@ class Context:
             ptr(o['tcpa']), ptr(o['tinconf']), ptr(o['dcpa']), ptr(o['li'], _c_i32p),
             ptr(o['lj'], _c_i32p), ptr(o['inconf'], _c_u8p), ptr(o['tcpamax'])), 'bsa_fetch_pairs')
         return o
+
+    # ---------------------------------------------------------------- ACDATA feed
+    def sim_acdata_request(self):
+        self.check(self.lib.bsa_sim_acdata_request(self.h), 'bsa_sim_acdata_request')
+
+    def sim_acdata_poll(self, wait=True):
+        """The requested snapshot as a dict, or None while it is in flight (wait=False)."""
+        probe = AcData()   # NULL arrays: status and row range only (no stream sync)
+        st = self.lib.bsa_sim_acdata_poll(self.h, int(bool(wait)), ctypes.byref(probe))
+        if st == 1:
+            return None
+        self.check(st, 'bsa_sim_acdata_poll')
+        nr = probe.row_end - probe.row_begin
+        arr = {k: np.empty(nr) for k in ACDATA_F64}
+        arr.update(inconf=np.empty(nr, np.uint8), asasn=np.empty(nr, np.float32),
+                   asase=np.empty(nr, np.float32))
+        o = AcData(**{k: ptr(arr[k]) for k in ACDATA_F64}, inconf=ptr(arr['inconf'], _c_u8p),
+                   asasn=ptr(arr['asasn'], _c_fp), asase=ptr(arr['asase'], _c_fp))
+        self.check(self.lib.bsa_sim_acdata_poll(self.h, 1, ctypes.byref(o)), 'bsa_sim_acdata_poll')
+        arr['inconf'] = arr['inconf'].astype(bool)
+        arr.update({k: getattr(o, k) for k in ('steps', 'row_begin', 'row_end') + ACDATA_COUNTS})
+        return arr
+
+    # ---------------------------------------------------------------- geo matrices
+    def qdrdist(self, lat1, lon1, lat2, lon2, kwik=False, pairwise=False):
+        """bsa_qdrdist: (qdr, dist) as flat float64 arrays of m*n (outer) or m
+        (pairwise) entries, row-major [i, j]."""
+        la1, lo1, la2, lo2 = (f64(x).ravel() for x in (lat1, lon1, lat2, lon2))
+        m, n = len(la1), len(la2)
+        if len(lo1) != m or len(lo2) != n:
+            raise ValueError('lat/lon lengths differ')
+        total = m if pairwise else m * n
+        qdr, dist = np.empty(total), np.empty(total)
+        flags = (GEO_KWIK if kwik else 0) | (GEO_PAIRWISE if pairwise else 0)
+        self.check(self.lib.bsa_qdrdist(self.h, m, ptr(la1), ptr(lo1), n, ptr(la2), ptr(lo2), flags,
+                                        ptr(qdr), ptr(dist)), 'bsa_qdrdist')
+        return qdr, dist
+
+    def geo_last_ms(self):
+        v = ctypes.c_double()
+        self.check(self.lib.bsa_geo_last_ms(self.h, ctypes.byref(v)), 'bsa_geo_last_ms')
+        return v.value
 
     def last_candidates(self):
         v = ctypes.c_int64()

@@ -25,37 +25,14 @@
 // of separation, and K1b evaluates the survivors exactly.
 #include <hipcub/hipcub.hpp>
 
+#include "bsa_geo_math.h"
 #include "bsa_internal.h"
 
 #pragma clang fp contract(off)
 
 namespace bsa {
 
-// ------------------------------------------------------------------ math
-// numpy.maximum / numpy.minimum semantics: NaN propagates, ties keep `a`.
-__device__ __forceinline__ double np_max(double a, double b) {
-  return (a >= b || a != a) ? a : b;
-}
-__device__ __forceinline__ double np_min(double a, double b) {
-  return (a <= b || a != a) ? a : b;
-}
-
-// geo.py:32-54 rwgs84_matrix, elementwise, same op order.
-__device__ __forceinline__ double rwgs84(double latd) {
-  const double a = kWGS84_A, b = kWGS84_B;
-  const double lat = latd * kD2R;
-  const double coslat = cos(lat);
-  const double sinlat = sin(lat);
-  const double an = (a * a) * coslat;
-  const double bn = (b * b) * sinlat;
-  const double ad = a * coslat;
-  const double bd = b * sinlat;
-  const double anan = an * an;
-  const double bnbn = bn * bn;
-  const double adad = ad * ad;
-  const double bdbd = bd * bd;
-  return sqrt((anan + bnbn) / (adad + bdbd));
-}
+// math helpers (np_max / np_min / np_rem / rwgs84) and the qdrdist entries: bsa_geo_math.h
 
 // ------------------------------------------------------------------ K0a keys
 __device__ __forceinline__ unsigned expand10(unsigned v) {
@@ -1051,17 +1028,6 @@ struct PairResult {
   double qdr, dist, tcpa, tin, dcpa;
 };
 
-// numpy.remainder for float64 (npy_divmod semantics)
-__device__ __forceinline__ double np_rem(double a, double b) {
-  double mod = fmod(a, b);
-  if (mod != 0.0) {
-    if ((b < 0) != (mod < 0)) mod += b;
-  } else {
-    mod = copysign(0.0, b);
-  }
-  return mod;
-}
-
 // One (i, j) entry of StateBasedCD.detect + geo.qdrdist_matrix, i != j.
 // KWIK (opt-in variant, BSA_FLAG_KWIK): geo.kwikqdrdist_matrix (geo.py:347-363)
 // replaces qdrdist_matrix, its metre distance handed over in nm (/ nm) so that
@@ -1073,43 +1039,14 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
   PairResult o;
   double qdr, dist_nm;
   if (KWIK) {
-    // [i, j]: dlat = latb[j] - lata[i], cavelat = cos(radians(lata[j] + latb[i]) * 0.5)
-    const double dlat = (c.lat - r.lat) * kD2R;
-    const double dlon = (c.lon - r.lon) * kD2R;
-    const double cavelat = cos(((c.olat + r.ilat) * kD2R) * 0.5);
-    const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
-    const double dist_m = 6371000. * dangle;
-    qdr = np_rem(atan2(dlon * cavelat, dlat) * kR2D, 360.);
+    // geo.kwikqdrdist_matrix [i, j]: cavelat at lata[j] + latb[i] (geo.py:355)
+    double dist_m;
+    kwik_entry(r.lat, r.lon, c.lat, c.lon, c.olat + r.ilat, qdr, dist_m);
     dist_nm = dist_m / kNM;
   } else {
-  // ---- geo.qdrdist_matrix (geo.py:118-160)
-  const double prodla = r.lat * c.lat;
-  double rr;
-  if (prodla < 0) {
-    // different hemisphere (geo.py:126-129)
-    rr = (0.5 * (r.hemA + c.hemA)) / (fabs(r.lat) + (fabs(c.lat) + c.eps));
-  } else {
-    rr = rwgs84(r.lat + c.lat);  // geo.py:122: radius at the SUM of the latitudes
-  }
-  const double diff_lat = c.lat - r.lat;
-  const double diff_lon = c.lon - r.lon;
-  const double sin1 = diff_lat * kD2R;
-  const double sin2 = diff_lon * kD2R;
-  const double sin21 = sin(sin2);
-  const double cos21 = cos(sin2);
-  const double y = sin21 * c.coslat;
-  const double x1 = r.coslat * c.sinlat;
-  const double x2 = r.sinlat * c.coslat;
-  const double x3 = x2 * cos21;
-  const double x = x1 - x3;
-  qdr = atan2(y, x) * kR2D;
-  const double sin10 = fabs(sin(sin1 / 2.));
-  const double sin20 = fabs(sin(sin2 / 2.));
-  const double sin1sin1 = sin10 * sin10;
-  const double sin2sin2 = sin20 * sin20;
-  const double hav = sin1sin1 + (r.coslat * c.coslat) * sin2sin2;
-  const double dist_c = 2. * atan2(sqrt(hav), sqrt(1 - hav));
-  dist_nm = (rr / kNM) * dist_c;
+    // geo.qdrdist_matrix (geo.py:118-160)
+    qdrdist_entry(r.lat, r.lon, r.sinlat, r.coslat, r.hemA, c.lat, c.lon, c.sinlat, c.coslat, c.hemA,
+                  c.eps, qdr, dist_nm);
   }
 
   // ---- StateBasedCD.detect (StateBasedCD.py:22-83), off-diagonal entry

@@ -142,14 +142,18 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
                         &c->gbox_r, &c->gbox_c, &c->sbox_c, &c->workq, &c->rowcnt, &c->rowoff, &c->lslot,
                         &c->cflag, &c->stats,
-                        &c->tilepairs, &c->snap_build, &c->snap_cur, &c->reuse_ctl, &c->reuse_use};
+                        &c->tilepairs, &c->snap_build, &c->snap_cur, &c->reuse_ctl, &c->reuse_use,
+                        &c->geo_in, &c->geo_pts, &c->geo_out};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);
+  bsa::feed_release(c);
   for (int k = 0; k < 6; ++k) {
     bsa::release(c->own[k]);
     bsa::release(c->intr[k]);
   }
   for (hipEvent_t e : c->evpool)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->geo_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;

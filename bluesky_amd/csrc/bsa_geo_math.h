@@ -1,0 +1,112 @@
+// Device restatements of bluesky/tools/geo.py shared by the fused CD kernel
+// (bsa_cd.hip, K1b) and the standalone matrix producers (bsa_geo.hip).
+// Same operation order as the numpy code, compiled with -ffp-contract=off,
+// so every + - * / sqrt rounds like numpy's.
+#pragma once
+#include "bsa_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace bsa {
+
+// numpy.maximum / numpy.minimum semantics: NaN propagates, ties keep `a`.
+__device__ __forceinline__ double np_max(double a, double b) {
+  return (a >= b || a != a) ? a : b;
+}
+__device__ __forceinline__ double np_min(double a, double b) {
+  return (a <= b || a != a) ? a : b;
+}
+
+// numpy.remainder for float64 (npy_divmod semantics), b > 0.  fmod is exact
+// and returns a itself when |a| < b, so that common case skips fmod's loop.
+__device__ __forceinline__ double np_rem(double a, double b) {
+  double mod = (fabs(a) < b) ? a : fmod(a, b);
+  if (mod != 0.0) {
+    if ((b < 0) != (mod < 0)) mod += b;
+  } else {
+    mod = copysign(0.0, b);
+  }
+  return mod;
+}
+
+// geo.py:32-54 rwgs84_matrix, elementwise, same op order.
+__device__ __forceinline__ double rwgs84(double latd) {
+  const double a = kWGS84_A, b = kWGS84_B;
+  const double lat = latd * kD2R;
+  const double coslat = cos(lat);
+  const double sinlat = sin(lat);
+  const double an = (a * a) * coslat;
+  const double bn = (b * b) * sinlat;
+  const double ad = a * coslat;
+  const double bd = b * sinlat;
+  const double anan = an * an;
+  const double bnbn = bn * bn;
+  const double adad = ad * ad;
+  const double bdbd = bd * bd;
+  return sqrt((anan + bnbn) / (adad + bdbd));
+}
+
+// Per-point factors of qdrdist_matrix's broadcasts (geo.py:127,136-140).
+struct GeoPt {
+  double lat, lon, sinlat, coslat;
+  double hemA;  // |lat| * (rwgs84(lat) + a)      geo.py:127
+};
+__device__ __forceinline__ GeoPt geo_pt(double lat, double lon) {
+  GeoPt p;
+  p.lat = lat;
+  p.lon = lon;
+  p.sinlat = sin(lat * kD2R);
+  p.coslat = cos(lat * kD2R);
+  p.hemA = fabs(lat) * (rwgs84(lat) + kWGS84_A);
+  return p;
+}
+
+// One entry [i, j] of geo.qdrdist_matrix (geo.py:117-160): point 1 = row i,
+// point 2 = column j, eps = (lat1[j] == 0.) * 1e-6 (geo.py:128, indexed by
+// the column).  qdr [deg], dist [nm].
+__device__ __forceinline__ void qdrdist_entry(double lat1, double lon1, double sinlat1, double coslat1,
+                                              double hemA1, double lat2, double lon2, double sinlat2,
+                                              double coslat2, double hemA2, double eps, double &qdr,
+                                              double &dist_nm) {
+  const double prodla = lat1 * lat2;
+  double rr;
+  if (prodla < 0) {
+    // different hemisphere (geo.py:125-128)
+    rr = (0.5 * (hemA1 + hemA2)) / (fabs(lat1) + (fabs(lat2) + eps));
+  } else {
+    rr = rwgs84(lat1 + lat2);  // geo.py:121: radius at the SUM of the latitudes
+  }
+  const double sin1 = (lat2 - lat1) * kD2R;
+  const double sin2 = (lon2 - lon1) * kD2R;
+  const double sin21 = sin(sin2);
+  const double cos21 = cos(sin2);
+  const double y = sin21 * coslat2;
+  const double x1 = coslat1 * sinlat2;
+  const double x2 = sinlat1 * coslat2;
+  const double x3 = x2 * cos21;
+  const double x = x1 - x3;
+  qdr = atan2(y, x) * kR2D;
+  const double sin10 = fabs(sin(sin1 / 2.));
+  const double sin20 = fabs(sin(sin2 / 2.));
+  const double sin1sin1 = sin10 * sin10;
+  const double sin2sin2 = sin20 * sin20;
+  const double hav = sin1sin1 + (coslat1 * coslat2) * sin2sin2;
+  const double dist_c = 2. * atan2(sqrt(hav), sqrt(1 - hav));
+  dist_nm = (rr / kNM) * dist_c;
+}
+
+// One entry [i, j] of geo.kwikqdrdist_matrix (geo.py:351-361):
+// dlat = latb[j] - lata[i], dlon = lonb[j] - lona[i], and the caller passes
+// cavelat's latitudes as written, lata[j] + latb[i] (geo.py:355).
+// qdr [deg] in [0, 360), dist [m].
+__device__ __forceinline__ void kwik_entry(double lata_i, double lona_i, double latb_j, double lonb_j,
+                                           double cavesum, double &qdr, double &dist_m) {
+  const double dlat = (latb_j - lata_i) * kD2R;
+  const double dlon = (lonb_j - lona_i) * kD2R;
+  const double cavelat = cos((cavesum * kD2R) * 0.5);
+  const double dangle = sqrt(dlat * dlat + (dlon * dlon) * (cavelat * cavelat));
+  dist_m = 6371000. * dangle;
+  qdr = np_rem(atan2(dlon * cavelat, dlat) * kR2D, 360.);
+}
+
+}  // namespace bsa

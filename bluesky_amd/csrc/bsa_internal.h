@@ -218,6 +218,20 @@ struct Ctx {
   DevBuf bk_stats, bk_tmp;
   unsigned long long bk_cap = 0;  // resopairs capacity (pairs)
   bool bk_ready = false;
+
+  // standalone geo matrices (bsa_geo.hip)
+  DevBuf geo_in, geo_pts, geo_out;
+  hipEvent_t geo_ev[2] = {nullptr, nullptr};
+  double geo_ms = 0.0;
+
+  // ACDATA feed of the resident sim (bsa_feed.hip): traf.cas of the last step,
+  // device staging, pinned host mirror, completion event
+  DevBuf s_cas, feed_dev;
+  void *feed_host = nullptr;
+  size_t feed_host_bytes = 0;
+  hipEvent_t feed_ev = nullptr;
+  bool feed_pending = false;
+  int64_t feed_steps = 0, feed_rb = 0, feed_re = 0;
 };
 
 // device pointers for the MVP kernel (full-N traffic arrays, per-row outputs)
@@ -265,8 +279,9 @@ int fail(Ctx *c, const char *fmt, ...);
                          __FILE__, __LINE__);                                         \
   } while (0)
 
-// sim / comm teardown (bsa_sim.hip)
+// sim / comm teardown (bsa_sim.hip); ACDATA feed teardown (bsa_feed.hip)
 void sim_release(Ctx *c);
+void feed_release(Ctx *c);
 
 // detect entry points (bsa_cd.hip): detect = enqueue + finish (+ retries)
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,

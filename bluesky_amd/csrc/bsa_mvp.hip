@@ -9,29 +9,17 @@
 // lane per pair); k_mvp_row then folds each ownship's segment in order, which
 // reproduces the reference's summation order exactly (no tree reduction),
 // and runs the per-aircraft finalize (MVP.py:67-143).
+#include "bsa_geo_math.h"  // np_max / np_min / np_rem
 #include "bsa_internal.h"
 
 #pragma clang fp contract(off)
 
 namespace bsa {
 
-__device__ __forceinline__ double np_max2(double a, double b) { return (a >= b || a != a) ? a : b; }
-__device__ __forceinline__ double np_min2(double a, double b) { return (a <= b || a != a) ? a : b; }
 // numpy.sign for float64
 __device__ __forceinline__ double np_sign(double x) {
   return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : (x == 0.0 ? 0.0 : x));
 }
-// numpy.remainder(a, b) for float64 (npy_divmod semantics)
-__device__ __forceinline__ double np_rem(double a, double b) {
-  double mod = fmod(a, b);
-  if (mod != 0.0) {
-    if ((b < 0) != (mod < 0)) mod += b;
-  } else {
-    mod = copysign(0.0, b);
-  }
-  return mod;
-}
-
 // segment start of each row: first k with ci[k] >= rb + r  (ci sorted);
 // seg[nrows] = P.  Used when the pairs came from the host (bsa_set_pairs);
 // a device detect hands its K2 row offsets over directly.
@@ -215,8 +203,8 @@ __global__ __launch_bounds__(256) void k_mvp_row(int rb, bsa_mvp_params p, MvpIn
     newgs = sqrt(newv0 * newv0 + newv1 * newv1);
     newvs = newv2;
   }
-  const double tas = np_max2(p.vmin, np_min2(p.vmax, newgs));
-  const double vsc = np_max2(p.vsmin, np_min2(p.vsmax, newvs));
+  const double tas = np_max(p.vmin, np_min(p.vmax, newgs));
+  const double vsc = np_max(p.vsmin, np_min(p.vsmax, newvs));
   in.o_trk[r] = newtrack;
   in.o_tas[r] = tas;
   in.o_vs[r] = vsc;

@@ -36,6 +36,7 @@ namespace bsa {
 
 struct SimDev {
   double *lat, *lon, *trk, *gs, *alt, *vs, *tas, *hdg, *gse, *gsn;
+  double *cas;                     // traf.cas (traffic.py:434), kept for the ACDATA feed
   const double *aptrk, *aptas, *apalt, *apvs, *bank, *eps, *accel;
   const double *atrk, *atas, *avs, *aalt;
   const uint8_t *active;
@@ -93,6 +94,7 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   d.trk[k] = o.trk;
   d.gse[k] = o.gseast;
   d.gsn[k] = o.gsnorth;
+  d.cas[k] = o.cas;
 }
 
 // field list of one all-gather: fp64 arrays (full n) + optionally one uint8 array
@@ -134,6 +136,7 @@ static SimDev sim_dev(Ctx *c) {
   d.hdg = (double *)c->s_hdg.p;
   d.gse = (double *)c->s_gse.p;
   d.gsn = (double *)c->s_gsn.p;
+  d.cas = (double *)c->s_cas.p;
   d.aptrk = (const double *)c->s_aptrk.p;
   d.aptas = (const double *)c->s_aptas.p;
   d.apalt = (const double *)c->s_apalt.p;
@@ -206,7 +209,7 @@ void sim_release(Ctx *c) {
   DevBuf *all[] = {&c->red, &c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
-                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl};
+                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl, &c->s_cas};
   for (auto *b : all) release(*b);
   bk_release(c);
   if (c->comm) {
@@ -337,8 +340,10 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   // ASAS arrays: asas.trk/tas start at traf.trk/tas (asas.py:405-409), vs 0, inactive
   if (!bsa::ensure(c, c->s_atrk, N8, "asas trk") || !bsa::ensure(c, c->s_atas, N8, "asas tas") ||
       !bsa::ensure(c, c->s_avs, N8, "asas vs") || !bsa::ensure(c, c->s_ase, (size_t)n * 4, "asase") ||
-      !bsa::ensure(c, c->s_asn, (size_t)n * 4, "asasn") || !bsa::ensure(c, c->s_active, n, "active"))
+      !bsa::ensure(c, c->s_asn, (size_t)n * 4, "asasn") || !bsa::ensure(c, c->s_active, n, "active") ||
+      !bsa::ensure(c, c->s_cas, N8, "cas"))
     return -1;
+  BSA_HIP(c, hipMemsetAsync(c->s_cas.p, 0, N8, c->stream));  // traf.cas: 0 until the first step
   BSA_HIP(c, hipMemcpyAsync(c->s_atrk.p, s->trk, N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemcpyAsync(c->s_atas.p, s->tas, N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemsetAsync(c->s_avs.p, 0, N8, c->stream));
@@ -357,6 +362,10 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   c->sim_re = std::min<int64_t>(n, c->sim_rb + c->sim_rpr);
   c->sim_steps = c->sim_cd_calls = c->sim_last_conf = c->sim_last_los = 0;
   c->sim_gathered = true;
+  if (c->feed_pending) {  // a snapshot of the previous sim is dropped
+    BSA_HIP(c, hipEventSynchronize(c->feed_ev));
+    c->feed_pending = false;
+  }
   c->sim_ready = true;
   return 0;
 }

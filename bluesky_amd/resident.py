@@ -84,3 +84,14 @@ class ResidentSim:
 
     def resopairs(self):
         return self.ctx.sim_resopairs()
+
+    def acdata_request(self):
+        """Enqueue an ACDATA snapshot of this rank's rows behind the queued steps
+        (screenio.py:194-239; no host synchronisation)."""
+        self.ctx.sim_acdata_request()
+
+    def acdata(self, wait=True):
+        """The requested snapshot: dict of per-row arrays (lat lon alt tas cas gs
+        trk vs tcpamax inconf asasn asase) plus steps, row_begin/row_end and the
+        four pair counts; None while in flight when ``wait`` is False."""
+        return self.ctx.sim_acdata_poll(wait)

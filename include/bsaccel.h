@@ -212,6 +212,32 @@ typedef struct bsa_kin_io {
 int bsa_kinematics(bsa_ctx *ctx, int64_t n, double simdt, int winddim,
                    double windnorth, double windeast, bsa_kin_io *io);
 
+/* ---------------------------------------------------------------- geo matrices
+ * Standalone materialised producers of
+ *   geo.qdrdist_matrix(lat1, lon1, lat2, lon2)      bluesky/tools/geo.py:110-162
+ *   geo.kwikqdrdist_matrix(lata, lona, latb, lonb)  bluesky/tools/geo.py:347-363 (BSA_GEO_KWIK)
+ * as called outside the CD (traffic/metric.py:596,711,1188 with 1 x m / 1 x n
+ * np.matrix operands; traffic/asas/SSD.py:169 with 1-D arrays, i.e.
+ * element-wise pairs).  qdr [deg] (KWIK: [0, 360)), dist [nm] (KWIK: metres,
+ * as the reference returns them).
+ *   outer  (default): out[i*n + j] for i < m, j < n.  qdrdist needs m == n or
+ *          m == 1 (its `(lat1 == 0.)*1e-6` term is added to the n-vector
+ *          lat2, geo.py:128); KWIK needs m == n (its cavelat is indexed
+ *          [j, i], geo.py:355).  Other shapes make the reference broadcast to
+ *          a different result shape and are rejected (BSA_EINVAL).
+ *   BSA_GEO_PAIRWISE: out[k] for k < m, m == n (1-D operands: every product
+ *          of the reference is element-wise).
+ * Host arrays are borrowed (float64); qdr / dist are caller-allocated
+ * (m*n or m doubles); either may be NULL.  The outputs go through HBM and back
+ * over PCIe; bsa_geo_last_ms reports the device time of the producing kernel
+ * alone (HIP events on the context stream). */
+#define BSA_GEO_KWIK     1
+#define BSA_GEO_PAIRWISE 2
+int bsa_qdrdist(bsa_ctx *ctx, int64_t m, const double *lat1, const double *lon1,
+                int64_t n, const double *lat2, const double *lon2, int flags,
+                double *qdr, double *dist);
+int bsa_geo_last_ms(bsa_ctx *ctx, double *ms);
+
 /* ---------------------------------------------------------------- multi-GPU
  * One process per GPU, one context per process.  Rank r owns the contiguous
  * ownship rows [r*ceil(n/R), min(n, (r+1)*ceil(n/R))) of the resident sim
@@ -283,6 +309,30 @@ int bsa_sim_asas_stats(bsa_ctx *ctx, int64_t *out6);
 /* This rank's resopairs (idx1 ascending, then idx2), at most cap pairs;
  * *count = total (call again with a larger buffer when *count > cap). */
 int bsa_sim_resopairs(bsa_ctx *ctx, int32_t *idx1, int32_t *idx2, int64_t cap, int64_t *count);
+
+/* ACDATA feed: the per-aircraft fields
+ * ScreenIO.send_aircraft_data streams at 5 Hz
+ * (bluesky/simulation/qtgl/screenio.py:194-239) for this rank's rows, served
+ * from HBM without stalling the sim.  _request enqueues a snapshot behind the
+ * steps already queued (one pack kernel + one copy into a pinned host mirror;
+ * no host synchronisation); _poll returns 1 while it is still in flight (wait
+ * = 0) or waits for it (wait = 1), then copies it into the caller's arrays
+ * (row_end - row_begin entries each; any pointer may be NULL) and returns 0.
+ * inconf / tcpamax are asas.inconf / asas.tcpamax of the last CD call (0
+ * before the first), cas is traf.cas after the last step (0 before the first),
+ * asasn / asase as asas holds them.  nconf_cur / nlos_cur = len(confpairs_unique) /
+ * len(lospairs_unique), nconf_tot / nlos_tot = len(confpairs_all) /
+ * len(lospairs_all) (screenio.py:207-210); -1 unless resume_nav = 1 on one
+ * rank.  A new request first waits for the previous snapshot. */
+typedef struct bsa_acdata {
+  int64_t steps, row_begin, row_end;  /* set by _poll */
+  int64_t nconf_cur, nconf_tot, nlos_cur, nlos_tot;
+  double *lat, *lon, *alt, *tas, *cas, *gs, *trk, *vs, *tcpamax;
+  uint8_t *inconf;
+  float *asasn, *asase;
+} bsa_acdata;
+int bsa_sim_acdata_request(bsa_ctx *ctx);
+int bsa_sim_acdata_poll(bsa_ctx *ctx, int wait, bsa_acdata *out);
 
 #ifdef __cplusplus
 }

@@ -129,3 +129,27 @@ def test_oracle_kinematics_matches_reference(path):
         ok, msg = util.close(np.asarray(o[k], dtype=np.float64),
                              np.asarray(z['out_' + k], dtype=np.float64), 1.0, rtol=1e-12)
         assert ok, '%s: %s' % (k, msg)
+
+
+GEO = util.golden('geo_*.npz')
+
+
+@pytest.mark.parametrize('path', GEO, ids=[util.case_name(p) for p in GEO])
+def test_oracle_geo_matches_reference(path):
+    """Standalone geo.qdrdist_matrix / kwikqdrdist_matrix (geo.py:110-162,
+    347-363), outer (row vectors) and pairwise (1-D) operands."""
+    from oracle import geo as ogeo
+    z = np.load(path)
+    fn, mode = str(z['fn']), str(z['mode'])
+    f = {('qdrdist', 'outer'): ogeo.qdrdist_outer, ('qdrdist', 'pairwise'): ogeo.qdrdist_pairwise,
+         ('kwik', 'outer'): ogeo.kwik_outer, ('kwik', 'pairwise'): ogeo.kwik_pairwise}[fn, mode]
+    qdr, dist = f(z['lat1'], z['lon1'], z['lat2'], z['lon2'])
+    for k, got in (('qdr', qdr), ('dist', dist)):
+        exp = z[k].ravel()
+        ok, msg = util.close(np.asarray(got).ravel(), exp, 0.0, rtol=1e-12)
+        assert ok, '%s: %s' % (k, msg)
+
+
+def test_geo_fixtures_present():
+    kinds = {(str(np.load(p)['fn']), str(np.load(p)['mode'])) for p in GEO}
+    assert kinds == {('qdrdist', 'outer'), ('qdrdist', 'pairwise'), ('kwik', 'outer'), ('kwik', 'pairwise')}

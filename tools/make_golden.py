@@ -13,6 +13,9 @@ and outputs as small ``.npz`` files under ``tests/golden/``:
 * ``asas_<case>.npz``  -- ``ASAS.update``'s bookkeeping + ``ResumeNav``
                          (asas.py:409-504) over a few CD calls, run by the
                          reference's own ``ASAS.update`` on a stand-in ``bs.traf``
+* ``geo_<case>.npz``   -- standalone ``geo.qdrdist_matrix`` / ``geo.kwikqdrdist_matrix``
+                         (geo.py:110-162, 347-363) with row-vector (outer) and 1-D
+                         (pairwise) operands, incl. the result types / shapes
 * ``cdkwik_<case>.npz`` -- the opt-in KWIK variant: ``StateBasedCD.detect`` with
                          ``geo.qdrdist_matrix`` swapped for ``geo.kwikqdrdist_matrix``
                          (geo.py:347-363), its metre distance handed over / nm
@@ -413,6 +416,55 @@ def run_asas(name, traf, ncalls=4, dt=20.0):
     print('asas_%-16s N=%5d calls=%d final resopairs=%d' % (name, n, ncalls, len(me.resopairs)))
 
 
+def geo_cases():
+    """(name, kind, lat1, lon1, lat2, lon2); kind = qdrdist|kwik x outer|pairwise."""
+    c = []
+    e = edge_traffic()
+    c.append(('edge_outer', 'qdrdist', 'outer', e.lat, e.lon, e.lat, e.lon))
+    own = synth.box(160, 120.0, seed=41, lat0=0.0, lon0=30.0)
+    intr = synth.box(160, 120.0, seed=42, lat0=0.0, lon0=30.0)
+    own.lat[::13] = 0.0
+    intr.lat[4::19] = 0.0
+    c.append(('equator160_outer', 'qdrdist', 'outer', own.lat, own.lon, intr.lat, intr.lon))
+    g = synth.global_traffic(200, seed=43)
+    c.append(('global200_outer', 'qdrdist', 'outer', g.lat, g.lon, g.lat, g.lon))
+    c.append(('row1_outer', 'qdrdist', 'outer', np.array([-0.5]), np.array([30.2]), own.lat, own.lon))
+    c.append(('row1_zero_outer', 'qdrdist', 'outer', np.array([0.0]), np.array([30.2]), intr.lat, intr.lon))
+    rng = np.random.default_rng(44)
+    g2 = synth.global_traffic(3000, seed=45)
+    i1, i2 = rng.integers(0, 3000, 2000), rng.integers(0, 3000, 2000)
+    la1, la2 = g2.lat[i1].copy(), g2.lat[i2].copy()
+    la1[::11] = 0.0
+    la2[5::17] = 0.0
+    c.append(('global2000_pairwise', 'qdrdist', 'pairwise', la1, g2.lon[i1], la2, g2.lon[i2]))
+    c.append(('edge_pairwise', 'qdrdist', 'pairwise', e.lat, e.lon, e.lat[::-1].copy(), e.lon[::-1].copy()))
+    c.append(('edge_kwik_outer', 'kwik', 'outer', e.lat, e.lon, e.lat, e.lon))
+    c.append(('equator160_kwik_outer', 'kwik', 'outer', own.lat, own.lon, intr.lat, intr.lon))
+    c.append(('global2000_kwik_pairwise', 'kwik', 'pairwise', la1, g2.lon[i1], la2, g2.lon[i2]))
+    return c
+
+
+def run_geo(name, fn, mode, lat1, lon1, lat2, lon2):
+    """Reference geo function on np.matrix row vectors (outer, as metric.py
+    calls it) or 1-D arrays (pairwise, as SSD.py calls it)."""
+    from oracle import geo as ogeo
+    ref = refgeo.qdrdist_matrix if fn == 'qdrdist' else refgeo.kwikqdrdist_matrix
+    if mode == 'outer':
+        args = [np.mat(x) for x in (lat1, lon1, lat2, lon2)]
+        o = (ogeo.qdrdist_outer if fn == 'qdrdist' else ogeo.kwik_outer)(lat1, lon1, lat2, lon2)
+    else:
+        args = [np.asarray(x) for x in (lat1, lon1, lat2, lon2)]
+        o = (ogeo.qdrdist_pairwise if fn == 'qdrdist' else ogeo.kwik_pairwise)(lat1, lon1, lat2, lon2)
+    qdr, dist = ref(*args)
+    for k, v, ov in (('qdr', qdr, o[0]), ('dist', dist, o[1])):
+        assert np.array_equal(np.asarray(v).ravel(), np.asarray(ov).ravel()), \
+            'oracle != reference geo %s/%s' % (name, k)
+    np.savez_compressed(os.path.join(OUT, 'geo_%s.npz' % name), fn=np.array(fn), mode=np.array(mode),
+                        lat1=lat1, lon1=lon1, lat2=lat2, lon2=lon2, qdr=np.asarray(qdr), dist=np.asarray(dist),
+                        shape=np.array(np.shape(qdr)), is_matrix=np.array(isinstance(qdr, np.matrix)))
+    print('geo_%-24s %s %s shape=%s matrix=%s' % (name, fn, mode, np.shape(qdr), isinstance(qdr, np.matrix)))
+
+
 KWIK_CASES = ('box500', 'equator1500', 'antimeridian800', 'polar400', 'edge', 'own_ne_int300')
 
 
@@ -422,6 +474,10 @@ def main():
     if '--kwik-only' in sys.argv:
         for name in KWIK_CASES:
             run_kwik(name, *cds[name])
+        return
+    if '--geo-only' in sys.argv:
+        for case in geo_cases():
+            run_geo(*case)
         return
     if '--asas-only' in sys.argv:
         run_asas('box500', cds['box500'][0])
@@ -438,6 +494,8 @@ def main():
     run_kin('nowind2000', 2000, 31, 0.05)
     run_kin('nowind_dt1', 500, 32, 1.0)
     run_kin('wind1000', 1000, 33, 0.05, wind=(270.0, 25.0 * kts))
+    for case in geo_cases():
+        run_geo(*case)
 
 
 if __name__ == '__main__':
