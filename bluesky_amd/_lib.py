@@ -146,6 +146,7 @@ SIGNATURES.update({
                                    ctypes.c_int, _c_dp, _c_dp]),
     'bsa_geo_last_ms': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_sim_acdata_request': (ctypes.c_int, [_vp]),
+    'bsa_set_windfield': (ctypes.c_int, [_vp, ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp]),
     'bsa_sim_acdata_poll': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(AcData)]),
 })
 
@@ -266,6 +267,18 @@ class Context:
             ptr(o['tcpa']), ptr(o['tinconf']), ptr(o['dcpa']), ptr(o['li'], _c_i32p),
             ptr(o['lj'], _c_i32p), ptr(o['inconf'], _c_u8p), ptr(o['tcpamax'])), 'bsa_fetch_pairs')
         return o
+
+    # ---------------------------------------------------------------- wind field
+    def set_windfield(self, lat=None, lon=None, vnorth=None, veast=None):
+        """2-D wind field for winddim 2 (bsa_set_windfield); no arguments clears it."""
+        if lat is None:
+            self.check(self.lib.bsa_set_windfield(self.h, 0, None, None, None, None), 'bsa_set_windfield')
+            return
+        arrs = [f64(x).ravel() for x in (lat, lon, vnorth, veast)]
+        if len({len(a) for a in arrs}) != 1:
+            raise ValueError('wind field arrays differ in length')
+        self.check(self.lib.bsa_set_windfield(self.h, len(arrs[0]), *[ptr(a) for a in arrs]),
+                   'bsa_set_windfield')
 
     # ---------------------------------------------------------------- ACDATA feed
     def sim_acdata_request(self):

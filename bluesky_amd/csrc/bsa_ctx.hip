@@ -143,7 +143,7 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->gbox_r, &c->gbox_c, &c->sbox_c, &c->workq, &c->rowcnt, &c->rowoff, &c->lslot,
                         &c->cflag, &c->stats,
                         &c->tilepairs, &c->snap_build, &c->snap_cur, &c->reuse_ctl, &c->reuse_use,
-                        &c->geo_in, &c->geo_pts, &c->geo_out};
+                        &c->geo_in, &c->geo_pts, &c->geo_out, &c->wfield};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);
   bsa::feed_release(c);

@@ -219,6 +219,10 @@ struct Ctx {
   unsigned long long bk_cap = 0;  // resopairs capacity (pairs)
   bool bk_ready = false;
 
+  // 2-D wind field (bsa_set_windfield): lat lon vnorth veast of wf_nvec points
+  DevBuf wfield;
+  int64_t wf_nvec = 0;
+
   // standalone geo matrices (bsa_geo.hip)
   DevBuf geo_in, geo_pts, geo_out;
   hipEvent_t geo_ev[2] = {nullptr, nullptr};
@@ -254,6 +258,8 @@ struct KinDev {
   uint8_t *swhdgsel, *swaltsel;
 };
 int kin_device(Ctx *c, int64_t n, double simdt, int winddim, double vn, double ve, const KinDev &d);
+struct WindField;
+WindField wind_field(const Ctx *c);  // device view of the context's 2-D field (bsa_kin.hip)
 
 // ASAS bookkeeping of one CD call (bsa_asas.hip): bk_count before the gate
 // all-reduce and MVP (may raise the gate's bit 1 on resopairs overflow),

@@ -9,9 +9,13 @@
 namespace bsa {
 
 __global__ __launch_bounds__(256) void k_kinematics(int n, double simdt, int winddim, double wn,
-                                                    double we, KinDev d) {
+                                                    double we, WindField wf, KinDev d) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
+  if (winddim == 2) {  // traffic.py:463: getdata at the pre-step position
+    kin::windfield_2d(wf, d.lat[k], d.lon[k], wn, we);
+    winddim = 1;
+  }
   kin::In s;
   s.tas = d.tas[k];
   s.hdg = d.hdg[k];
@@ -47,16 +51,49 @@ __global__ __launch_bounds__(256) void k_kinematics(int n, double simdt, int win
   if (d.swaltsel) d.swaltsel[k] = o.swaltsel;
 }
 
+WindField wind_field(const Ctx *c) {
+  WindField w;
+  const double *p = (const double *)c->wfield.p;
+  w.nvec = (int)c->wf_nvec;
+  w.lat = p;
+  w.lon = p ? p + c->wf_nvec : nullptr;
+  w.vn = p ? p + 2 * c->wf_nvec : nullptr;
+  w.ve = p ? p + 3 * c->wf_nvec : nullptr;
+  return w;
+}
+
 int kin_device(Ctx *c, int64_t n, double simdt, int winddim, double vn, double ve, const KinDev &d) {
   if (n <= 0) return 0;
-  if (winddim != 0 && winddim != 1) return fail(c, "winddim %d not supported (0 or 1)", winddim);
+  if (winddim < 0 || winddim > 2) return fail(c, "winddim %d not supported (0, 1 or 2)", winddim);
+  if (winddim == 2 && c->wf_nvec < 1) return fail(c, "winddim 2 needs a wind field (bsa_set_windfield)");
   hipLaunchKernelGGL(k_kinematics, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, (int)n,
-                     simdt, winddim, vn, ve, d);
+                     simdt, winddim, vn, ve, wind_field(c), d);
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
 
 }  // namespace bsa
+
+extern "C" int bsa_set_windfield(bsa_ctx *cc, int64_t nvec, const double *lat, const double *lon,
+                                 const double *vnorth, const double *veast) {
+  bsa::Ctx *c = (bsa::Ctx *)cc;
+  if (!c) return -1;
+  if (nvec < 0 || nvec > (1 << 20)) return bsa::fail(c, "bad wind field size %lld", (long long)nvec);
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (nvec == 0) {
+    c->wf_nvec = 0;
+    return 0;
+  }
+  if (!lat || !lon || !vnorth || !veast) return bsa::fail(c, "bsa_set_windfield: NULL array");
+  if (!bsa::ensure(c, c->wfield, (size_t)nvec * 32, "wind field")) return -1;
+  const double *src[4] = {lat, lon, vnorth, veast};
+  for (int k = 0; k < 4; ++k)
+    BSA_HIP(c, hipMemcpyAsync((double *)c->wfield.p + k * nvec, src[k], (size_t)nvec * 8, hipMemcpyHostToDevice,
+                              c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  c->wf_nvec = nvec;
+  return 0;
+}
 
 extern "C" int bsa_kinematics(bsa_ctx *cc, int64_t n, double simdt, int winddim, double windnorth,
                               double windeast, bsa_kin_io *io) {

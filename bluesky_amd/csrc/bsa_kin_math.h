@@ -2,7 +2,8 @@
 // kernel (bsa_kin.hip) and the GPU-resident sim step (bsa_sim.hip).
 //
 // Traffic.UpdateAirSpeed    bluesky/traffic/traffic.py:425-454
-// Traffic.UpdateGroundSpeed bluesky/traffic/traffic.py:456-476 (winddim 0/1)
+// Traffic.UpdateGroundSpeed bluesky/traffic/traffic.py:456-476 (winddim 0/1/2)
+// Windfield.getdata, 2-D    bluesky/traffic/windfield.py:158-179 (winddim 2)
 // Traffic.UpdatePosition    bluesky/traffic/traffic.py:478-483
 // aero.vatmos / vtas2cas / vtas2mach  bluesky/tools/aero.py:62-147
 // Every expression keeps numpy's evaluation order (compile with
@@ -11,7 +12,41 @@
 #include "bsa_internal.h"
 
 namespace bsa {
+
+// 2-D wind field (winddim 2): nvec definition points with their wind
+// (Windfield.lat / lon / vnorth[0, :] / veast[0, :]), device pointers.
+struct WindField {
+  const double *lat, *lon, *vn, *ve;
+  int nvec;
+};
+
 namespace kin {
+
+// Windfield.getdata for a 2-D field at one position (windfield.py:158-179):
+// inverse-distance-squared weights in a flat frame of 1-degree units,
+// normalised by their sum.  The reference's sums are BLAS dot products; here
+// they run in point order (same terms, summation order may differ by ulps).
+__device__ __forceinline__ void windfield_2d(const WindField &w, double lat, double lon, double &vn,
+                                             double &ve) {
+  const double eps = 1e-20;
+  double sum = 0.0;
+  for (int k = 0; k < w.nvec; ++k) {
+    const double cavelat = cos((0.5 * (lat + w.lat[k])) * kD2R);
+    const double dy = lat - w.lat[k];
+    const double dx = cavelat * (lon - w.lon[k]);
+    sum += 1. / (eps + dx * dx + dy * dy);
+  }
+  vn = 0.0;
+  ve = 0.0;
+  for (int k = 0; k < w.nvec; ++k) {
+    const double cavelat = cos((0.5 * (lat + w.lat[k])) * kD2R);
+    const double dy = lat - w.lat[k];
+    const double dx = cavelat * (lon - w.lon[k]);
+    const double horfact = (1. / (eps + dx * dx + dy * dy)) / sum;
+    vn += w.vn[k] * horfact;
+    ve += w.ve[k] * horfact;
+  }
+}
 
 constexpr double kG0 = 9.80665;        // aero.py:18
 constexpr double kRgas = 287.05287;    // aero.py:19

@@ -44,14 +44,18 @@ struct SimDev {
   unsigned long long *steps_done;  // steps completed in the batch
 };
 
-// Pilot.APorASAS (pilot.py:28-63; winddim 0 or constant wind) +
+// Pilot.APorASAS (pilot.py:28-63; no wind, constant wind or a 2-D field) +
 // UpdateAirSpeed/GroundSpeed/Position, rows [rb, re)
 __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, int winddim, double vwn,
-                                                       double vwe, SimDev d) {
+                                                       double vwe, WindField wf, SimDev d) {
   if (*d.sticky) return;
   const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
   if (k >= re) return;
+  if (winddim == 2) {  // pilot.py:32 and traffic.py:463 read the field at the same pre-step position
+    kin::windfield_2d(wf, d.lat[k], d.lon[k], vwn, vwe);
+    winddim = 1;
+  }
   const bool act = d.active[k] != 0;
   const double ptrk = act ? d.atrk[k] : d.aptrk[k];   // pilot.py:41
   kin::In s;
@@ -355,6 +359,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   BSA_HIP(c, hipMemsetAsync(c->sim_ctl.p, 0, 64, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   if (p->resume_nav != 0 && p->resume_nav != 1) return bsa::fail(c, "resume_nav must be 0 or 1");
+  if (p->winddim < 0 || p->winddim > 2) return bsa::fail(c, "winddim must be 0, 1 or 2");
   c->simp = *p;
   c->bk_ready = false;  // empty resopairs / previous pair sets
   c->sim_rpr = (n + c->nranks - 1) / c->nranks;
@@ -374,6 +379,8 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
   Ctx *c = (Ctx *)cc;
   if (!c) return -1;
   if (!c->sim_ready) return bsa::fail(c, "bsa_sim_step before bsa_sim_init");
+  if (c->simp.winddim == 2 && c->wf_nvec < 1)
+    return bsa::fail(c, "winddim 2 needs a wind field (bsa_set_windfield)");
   if (nsteps < 0) return bsa::fail(c, "negative step count");
   BSA_HIP(c, hipSetDevice(c->device));
   const int64_t rb = c->sim_rb, re = c->sim_re;
@@ -388,7 +395,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
       const int64_t nb = std::max<int64_t>(1, (re - rb + 255) / 256);
       hipLaunchKernelGGL(bsa::k_sim_pilot_kin, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb, (int)re,
                          c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
-                         bsa::sim_dev(c));
+                         bsa::wind_field(c), bsa::sim_dev(c));
       BSA_HIP(c, hipGetLastError());
       c->sim_gathered = c->nranks == 1;
       c->sim_steps++;

@@ -42,9 +42,10 @@ def initial_state(traf):
 
 def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, reso=True, mar=1.05,
            swresohoriz=True, swresospd=False, swresohdg=False, swresovert=False, swprio=False,
-           priocode='FF1', wind=None, resume_nav=False):
+           priocode='FF1', wind=None, resume_nav=False, windfield=False):
     """bsa_sim_params; ASAS defaults of asas.py:81-112 with asas_mar from data/default.cfg.
-    ``wind=(vnorth, veast)`` [m/s]: constant wind (winddim 1).  ``resume_nav``: ASAS.update's
+    ``wind=(vnorth, veast)`` [m/s]: constant wind (winddim 1); ``windfield=True``: the
+    2-D field handed to ``ResidentSim(windfield=...)`` (winddim 2).  ``resume_nav``: ASAS.update's
     resopairs bookkeeping and ResumeNav's asas.active (asas.py:409-504) instead of
     ``active = inconf``."""
     mvp = _lib.MvpParams(Rm=rpz * mar, dhm=hpz * mar, dtlookahead=tla, vmin=200.0 * NM / 3600.,
@@ -54,7 +55,8 @@ def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, res
                          priocode=_lib.PRIO_CODES.get(priocode, 0), swnoreso=0, swresooff=0)
     wn, we = (0.0, 0.0) if wind is None else (float(wind[0]), float(wind[1]))
     return _lib.SimParams(simdt=simdt, rpz=rpz, hpz=hpz, tla=tla, cd_every=int(cd_every),
-                          reso=int(bool(reso)), mvp=mvp, winddim=0 if wind is None else 1,
+                          reso=int(bool(reso)), mvp=mvp,
+                          winddim=2 if windfield else (0 if wind is None else 1),
                           resume_nav=int(bool(resume_nav)),
                           windnorth=wn, windeast=we)
 
@@ -62,11 +64,16 @@ def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, res
 class ResidentSim:
     """Device-resident traffic; ``rank``/``world`` > 1 shards the rows over GPUs."""
 
-    def __init__(self, state, p, ctx=None, rank=0, world=1):
+    def __init__(self, state, p, ctx=None, rank=0, world=1, windfield=None):
+        """``windfield``: dict(lat, lon, vnorth, veast) of the 2-D field's points
+        (Windfield.lat / lon / vnorth[0, :] / veast[0, :]) for ``winddim`` 2."""
         self.ctx = ctx or _lib.default_context()
         self.rank, self.world = rank, world
         if world > 1:
             dist.init_comm(self.ctx, rank, world)
+        if windfield is not None:
+            self.ctx.set_windfield(windfield['lat'], windfield['lon'], windfield['vnorth'],
+                                   windfield['veast'])
         self.ctx.sim_init(state, p)
         self.params = p
 

@@ -196,7 +196,8 @@ int bsa_mvp(bsa_ctx *ctx, const bsa_mvp_params *p,
  * Traffic.UpdateAirSpeed + UpdateGroundSpeed + UpdatePosition
  * (bluesky/traffic/traffic.py:425-483) for n aircraft, one fused kernel.
  * winddim 0 = no wind, 1 = constant wind (windnorth/windeast m/s,
- * windfield.py:150-152).  Host arrays of length n; state arrays are updated
+ * windfield.py:150-152), 2 = the context's 2-D wind field (bsa_set_windfield;
+ * windnorth/windeast ignored).  Host arrays of length n; state arrays are updated
  * in place; output pointers may be NULL. */
 typedef struct bsa_kin_io {
   /* inputs */
@@ -211,6 +212,18 @@ typedef struct bsa_kin_io {
 
 int bsa_kinematics(bsa_ctx *ctx, int64_t n, double simdt, int winddim,
                    double windnorth, double windeast, bsa_kin_io *io);
+
+/* 2-D wind field for winddim 2 (bsa_kinematics and the resident sim):
+ * Windfield.getdata's inverse-distance-squared interpolation
+ * (bluesky/traffic/windfield.py:158-179) over nvec definition points at
+ * lat/lon [deg] with wind vnorth/veast [m/s] (Windfield.vnorth[0, :] /
+ * veast[0, :], as WindSim.addpoint stores them).  Evaluated per aircraft at
+ * its pre-step position, for both Pilot.APorASAS (pilot.py:31-35) and
+ * UpdateGroundSpeed (traffic.py:463).  Altitude profiles (winddim 3) are not
+ * supported: the reference's 3-D branch raises for arrays (windfield.py:177).
+ * nvec = 0 clears the field.  Host arrays are copied. */
+int bsa_set_windfield(bsa_ctx *ctx, int64_t nvec, const double *lat, const double *lon,
+                      const double *vnorth, const double *veast);
 
 /* ---------------------------------------------------------------- geo matrices
  * Standalone materialised producers of
@@ -269,8 +282,9 @@ typedef struct bsa_sim_params {
   int32_t cd_every; /* >= 1: CD + MVP every k steps (1 = DTNOLOOK=simdt, 20 = asas_dt/simdt) */
   int32_t reso;     /* 1: MVP resolution + asas.active = inconf; 0: CD only (RESO OFF) */
   bsa_mvp_params mvp;
-  int32_t winddim;  /* 0 = no wind, 1 = constant wind (windfield.py:150-152): the wind branches
-                       of Pilot.APorASAS (pilot.py:31-36,51-61) and UpdateGroundSpeed */
+  int32_t winddim;  /* 0 = no wind, 1 = constant wind (windfield.py:150-152), 2 = 2-D field
+                       (bsa_set_windfield): the wind branches of Pilot.APorASAS
+                       (pilot.py:31-36,51-61) and UpdateGroundSpeed */
   int32_t resume_nav; /* 1: ASAS.update bookkeeping on the device: resopairs, ResumeNav's
                          asas.active (asas.py:409-471) and the unique / cumulative pair
                          counts (asas.py:490-502); 0: asas.active = inconf */

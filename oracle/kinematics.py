@@ -84,8 +84,34 @@ def update_airspeed(s, simdt):
     return o
 
 
+def windfield_2d(lat, lon, wlat, wlon, wvnorth, wveast):
+    """Windfield.getdata for a 2-D field (winddim 2, windfield.py:158-179):
+    inverse-distance-squared weights in a flat frame of 1-degree units.
+    wlat/wlon: the nvec definition points, wvnorth/wveast their wind [m/s]
+    (Windfield.vnorth[0, :] / veast[0, :]).  Same numpy expressions (incl. the
+    two matrix products) as the reference, so it is bitwise equal there."""
+    eps = 1e-20
+    npos = len(lat)
+    nvec = len(wlat)
+    lat = np.array(lat).reshape((1, npos))
+    lon = np.array(lon).reshape((1, npos))
+    wl = np.array([np.asarray(wlat, dtype=np.float64)]).transpose()
+    wo = np.array([np.asarray(wlon, dtype=np.float64)]).transpose()
+    cavelat = np.cos(np.radians(0.5 * (lat + wl)))
+    dy = lat - wl
+    dx = cavelat * (lon - wo)
+    invd2 = 1. / (eps + dx * dx + dy * dy)
+    sumsid2 = np.ones((1, nvec)).dot(invd2)
+    totals = np.repeat(sumsid2, nvec, axis=0)
+    horfact = invd2 / totals
+    vnorth = np.asarray(wvnorth, dtype=np.float64).dot(horfact)
+    veast = np.asarray(wveast, dtype=np.float64).dot(horfact)
+    return vnorth, veast
+
+
 def update_groundspeed(tas, hdg, alt, winddim=0, windnorth=0.0, windeast=0.0):
-    """traffic.py:456-476 (winddim 0 or 1)."""
+    """traffic.py:456-476; windnorth/windeast: scalars (winddim 1) or
+    per-aircraft arrays from windfield_2d (winddim 2)."""
     o = {}
     if winddim == 0:
         o['gsnorth'] = tas * np.cos(np.radians(hdg))

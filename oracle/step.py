@@ -6,7 +6,8 @@ Order of Traffic.update (bluesky/traffic/traffic.py:383-409) restricted to
 the hot path: asas.update (asas.py:473-504: detect, then MVP.resolve only if
 confpairs is non-empty) every ``cd_every`` steps with ``asas.active =
 inconf``; Pilot.APorASAS (pilot.py:28-63) without wind or with a constant
-wind (``p['wind'] = (vnorth, veast)``, windfield.py:150-152); UpdateAirSpeed /
+wind (``p['wind'] = (vnorth, veast)``, windfield.py:150-152) or a 2-D field
+(``p['windfield']``, windfield.py:158-179); UpdateAirSpeed /
 UpdateGroundSpeed / UpdatePosition (traffic.py:425-483).  With a
 ``Bookkeeping`` (oracle/asas.py) the CD step instead runs ASAS.update's
 resopairs bookkeeping and ResumeNav (asas.py:409-504) and takes asas.active
@@ -47,8 +48,13 @@ def sim_step(st, p, do_cd, bk=None):
             st['active'] = bk.active.copy()
     act = st['active']
     wind = p.get('wind')
+    field = p.get('windfield')
+    if field is not None:                                     # winddim 2 (windfield.py:158-179)
+        vwn, vwe = okin.windfield_2d(st['lat'], st['lon'], field['lat'], field['lon'],
+                                     field['vnorth'], field['veast'])
+        wind = (vwn, vwe)
     if wind is not None:                                      # pilot.py:31-35
-        vwn, vwe = np.full(n, wind[0]), np.full(n, wind[1])
+        vwn, vwe = np.ones(n) * wind[0], np.ones(n) * wind[1]
         asastasnorth = st['asas_tas'] * np.cos(np.radians(st['asas_trk'])) - vwn
         asastaseast = st['asas_tas'] * np.sin(np.radians(st['asas_trk'])) - vwe
         asastas = np.sqrt(asastasnorth**2 + asastaseast**2)

@@ -75,8 +75,13 @@ def test_kinematics_matches_reference_golden(ctx, path):
     state = {k: np.ascontiguousarray(z[k], dtype=np.float64).copy()
              for k in ('tas', 'hdg', 'alt', 'vs', 'lat', 'lon')}
     inputs = {k: z[k] for k in ('ptas', 'phdg', 'palt', 'pvs', 'bank', 'eps', 'accel')}
-    o = ctx.kinematics(float(z['dt']), state, inputs, int(z['winddim']), float(z['windnorth']),
-                       float(z['windeast']))
+    wd = int(z['winddim'])
+    if wd == 2:   # 2-D wind field (bsa_set_windfield), the reference's getdata pinned by the fixture
+        ctx.set_windfield(z['wlat'], z['wlon'], z['wvnorth'], z['wveast'])
+        o = ctx.kinematics(float(z['dt']), state, inputs, 2, 0.0, 0.0)
+        ctx.set_windfield()
+    else:
+        o = ctx.kinematics(float(z['dt']), state, inputs, wd, float(z['windnorth']), float(z['windeast']))
     o.update(state)
     o['M'] = o.pop('mach')
     scales = dict(ax=1.0, delspd=100.0, tas=300.0, cas=300.0, M=1.0, hdg=360.0, az=1.0, vs=20.0,

@@ -187,3 +187,32 @@ def test_resident_resume_nav_overflow_retry_is_exact(ctx):
     assert np.array_equal(got_reso[0], exp_reso[0]) and np.array_equal(got_reso[1], exp_reso[1])
     assert sim.stats()['steps'] == 6
     c2.close()
+
+
+def test_resident_windfield_matches_oracle(ctx):
+    """winddim 2: the 2-D wind field (windfield.py:158-179) read per aircraft by
+    Pilot.APorASAS and UpdateGroundSpeed inside the resident step."""
+    from oracle import kinematics as okin
+    t = synth.box(1200, 60.0, seed=37)
+    init = resident.initial_state(t)
+    field = dict(lat=np.array([52.0, 52.6, 51.5, 52.3]), lon=np.array([4.0, 3.2, 4.9, 5.1]),
+                 vnorth=np.array([-12.0, 3.5, 20.0, -1.0]), veast=np.array([5.0, -15.0, 2.0, 30.0]))
+    p = resident.params(cd_every=1, windfield=True)
+    sim = resident.ResidentSim(init, p, ctx=ctx, windfield=field)
+    op = oracle_params(p)
+    op['windfield'] = field
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(t.ntraf), active=np.zeros(t.ntraf, bool))
+    for k in range(3):
+        exp = ostep.sim_step(prev, op, do_cd=True)
+        sim.step(1)
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        prev = got
+    vn, _ = okin.windfield_2d(prev['lat'], prev['lon'], field['lat'], field['lon'], field['vnorth'],
+                              field['veast'])
+    assert np.ptp(vn) > 1.0      # the field actually varies over the traffic
+    ctx.set_windfield()
+    with pytest.raises(Exception, match='wind field'):
+        sim.step(1)

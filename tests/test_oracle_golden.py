@@ -123,7 +123,12 @@ def test_oracle_kinematics_matches_reference(path):
     z = dict(np.load(path, allow_pickle=False))
     s = {k: z[k] for k in ('lat', 'lon', 'alt', 'tas', 'hdg', 'vs', 'ptas', 'phdg', 'palt', 'pvs',
                            'bank', 'eps', 'accel')}
-    o = okin.step(s, float(z['dt']), int(z['winddim']), float(z['windnorth']), float(z['windeast']))
+    if int(z['winddim']) == 2:   # 2-D field (windfield.py:158-179) at the pre-step positions
+        vn, ve = okin.windfield_2d(z['lat'], z['lon'], z['wlat'], z['wlon'], z['wvnorth'], z['wveast'])
+        assert util.close(vn, z['windnorth'], 1.0, rtol=1e-12)[0] and util.close(ve, z['windeast'], 1.0, rtol=1e-12)[0]
+        o = okin.step(s, float(z['dt']), 1, vn, ve)
+    else:
+        o = okin.step(s, float(z['dt']), int(z['winddim']), float(z['windnorth']), float(z['windeast']))
     for k in ('ax', 'delspd', 'tas', 'cas', 'M', 'hdg', 'swhdgsel', 'swaltsel', 'az', 'vs',
               'gsnorth', 'gseast', 'gs', 'trk', 'alt', 'lat', 'lon', 'coslat'):
         ok, msg = util.close(np.asarray(o[k], dtype=np.float64),

@@ -332,7 +332,15 @@ def run_kin(name, n, seed, dt, wind=None):
     acc = s['accel'].copy()
     fake.perf = types.SimpleNamespace(acceleration=lambda: acc)
     fake.wind = WindSim()
-    if wind is not None:
+    field = None
+    if isinstance(wind, list):          # 2-D field: several points (winddim 2)
+        for (wlat, wlon, wdir, wspd) in wind:
+            fake.wind.addpoint(wlat, wlon, wdir, wspd)
+        assert fake.wind.winddim == 2
+        field = dict(wlat=np.array(fake.wind.lat, dtype=np.float64),
+                     wlon=np.array(fake.wind.lon, dtype=np.float64),
+                     wvnorth=np.array(fake.wind.vnorth[0, :]), wveast=np.array(fake.wind.veast[0, :]))
+    elif wind is not None:
         fake.wind.addpoint(52.0, 4.0, wind[0], wind[1])
     RefTraffic.UpdateAirSpeed(fake, dt, 0.0)
     RefTraffic.UpdateGroundSpeed(fake, dt)
@@ -341,13 +349,21 @@ def run_kin(name, n, seed, dt, wind=None):
             'gsnorth', 'gseast', 'gs', 'trk', 'alt', 'lat', 'lon', 'coslat')
     ref = {k: np.asarray(getattr(fake, k)) for k in keys}
     vn = ve = 0.0
-    if wind is not None:
+    if field is not None:
+        # the reference's getdata at the pre-step positions (traffic.py:463) vs the oracle's
+        vn, ve = fake.wind.getdata(s['lat'].copy(), s['lon'].copy(), s['alt'].copy())
+        ovn, ove = okin.windfield_2d(s['lat'], s['lon'], field['wlat'], field['wlon'],
+                                     field['wvnorth'], field['wveast'])
+        assert np.array_equal(ovn, vn) and np.array_equal(ove, ve), 'oracle != reference windfield'
+    elif wind is not None:
         vn_, ve_ = fake.wind.getdata(np.array([0.0]), np.array([0.0]), np.array([0.0]))
         vn, ve = float(vn_[0]), float(ve_[0])
     o = okin.step(s, dt, winddim=0 if wind is None else 1, windnorth=vn, windeast=ve)
     for k in keys:
         assert np.array_equal(o[k], ref[k], equal_nan=True), 'oracle != reference kin %s/%s' % (name, k)
-    out = dict(dt=dt, winddim=0 if wind is None else 1, windnorth=vn, windeast=ve, **s)
+    out = dict(dt=dt, winddim=0 if wind is None else (2 if field else 1), windnorth=vn, windeast=ve, **s)
+    if field is not None:
+        out.update(field)
     out.update({'out_' + k: v for k, v in ref.items()})
     np.savez_compressed(os.path.join(OUT, 'kin_%s.npz' % name), **out)
     print('kin_%-17s N=%5d dt=%g wind=%s' % (name, n, dt, wind))
@@ -465,6 +481,12 @@ def run_geo(name, fn, mode, lat1, lon1, lat2, lon2):
     print('geo_%-24s %s %s shape=%s matrix=%s' % (name, fn, mode, np.shape(qdr), isinstance(qdr, np.matrix)))
 
 
+# a 2-D wind field (winddim 2) of 5 points around the kin_state box (52N 4E, 300 NM)
+WIND_FIELD = [(52.0, 4.0, 270.0, 25.0 * kts), (54.0, 1.0, 300.0, 40.0 * kts),
+              (50.5, 7.5, 200.0, 15.0 * kts), (53.5, 8.0, 10.0, 60.0 * kts),
+              (50.0, 0.5, 135.0, 5.0 * kts)]
+
+
 KWIK_CASES = ('box500', 'equator1500', 'antimeridian800', 'polar400', 'edge', 'own_ne_int300')
 
 
@@ -474,6 +496,9 @@ def main():
     if '--kwik-only' in sys.argv:
         for name in KWIK_CASES:
             run_kwik(name, *cds[name])
+        return
+    if '--windfield-only' in sys.argv:
+        run_kin('windfield1500', 1500, 34, 0.05, wind=WIND_FIELD)
         return
     if '--geo-only' in sys.argv:
         for case in geo_cases():
@@ -494,6 +519,7 @@ def main():
     run_kin('nowind2000', 2000, 31, 0.05)
     run_kin('nowind_dt1', 500, 32, 1.0)
     run_kin('wind1000', 1000, 33, 0.05, wind=(270.0, 25.0 * kts))
+    run_kin('windfield1500', 1500, 34, 0.05, wind=WIND_FIELD)
     for case in geo_cases():
         run_geo(*case)
 
