@@ -7,8 +7,11 @@ kernel.  BlueSky has no plugin API for kinematics, so
 ``install(traf)`` rebinds the three methods on the instance: the fused step
 runs in ``UpdateAirSpeed`` and the other two become no-ops.
 
-Supports winddim 0 (no wind) and 1 (constant wind); a 2-D/3-D wind field
-raises (next step).
+Supports winddim 0 (no wind), 1 (constant wind) and 2 (2-D field: the
+inverse-distance-squared interpolation of windfield.py:158-179, per aircraft
+on the device, bsa_set_windfield).  winddim 3 (altitude profiles) raises
+ValueError, as the reference's own getdata does for array positions
+(windfield.py:177 compares an ndarray with None in a boolean context).
 """
 import types
 
@@ -27,9 +30,12 @@ def step(traf, simdt, ctx=None):
     if winddim == 1:
         vn = float(traf.wind.vnorth[0, 0])   # windfield.py:150-152
         ve = float(traf.wind.veast[0, 0])
-    elif winddim > 1:
-        raise NotImplementedError('winddim %d (wind field interpolation) is not on the GPU path yet'
-                                  % winddim)
+    elif winddim == 2:
+        w = traf.wind                         # Windfield.lat / lon / vnorth[0, :] / veast[0, :]
+        ctx.set_windfield(w.lat, w.lon, np.asarray(w.vnorth)[0, :], np.asarray(w.veast)[0, :])
+    elif winddim > 2:
+        raise ValueError('winddim %d: the reference\'s 3-D wind interpolation fails for array '
+                         'positions (windfield.py:177)' % winddim)
     state = {k: np.array(getattr(traf, k), dtype=np.float64, copy=True)
              for k in ('tas', 'hdg', 'alt', 'vs', 'lat', 'lon')}
     inputs = dict(ptas=traf.pilot.tas, phdg=traf.pilot.hdg, palt=traf.pilot.alt, pvs=traf.pilot.vs,

@@ -16,6 +16,12 @@
  *   bsa_kinematics
  *       bluesky/traffic/traffic.py:425-483           UpdateAirSpeed / UpdateGroundSpeed / UpdatePosition
  *       bluesky/tools/aero.py:62-147                 vatmos / vtas2cas / vtas2mach (inlined)
+ *   bsa_set_windfield (winddim 2)
+ *       bluesky/traffic/windfield.py:158-179         Windfield.getdata, 2-D field
+ *   bsa_qdrdist
+ *       bluesky/tools/geo.py:110-162,347-363         qdrdist_matrix / kwikqdrdist_matrix, materialised
+ *   bsa_sim_acdata_*
+ *       bluesky/simulation/qtgl/screenio.py:194-239  send_aircraft_data (ACDATA stream fields)
  *   bsa_sim_*     GPU-resident chain of the above, no reference equivalent
  *   bsa_comm_*    RCCL row-sharded multi-GPU mode, no reference equivalent
  *
