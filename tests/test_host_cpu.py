@@ -50,10 +50,34 @@ def test_resident_initial_state_matches_traffic_create():
     assert np.array_equal(s['tas'], t.gs) and np.array_equal(s['hdg'], t.trk)
 
 
-def test_kinematics_rejects_wind_fields():
-    traf = types.SimpleNamespace(wind=types.SimpleNamespace(winddim=2))
-    with pytest.raises((NotImplementedError, _lib.AccelUnavailable)):
+def test_kinematics_rejects_3d_wind_fields():
+    """winddim 3 fails like the reference's getdata for array positions (windfield.py:177)."""
+    traf = types.SimpleNamespace(wind=types.SimpleNamespace(winddim=3))
+    with pytest.raises(ValueError, match='windfield.py:177'):
         kinematics.step(traf, 0.05, ctx=types.SimpleNamespace())
+
+
+def test_kinematics_uploads_2d_wind_field():
+    """winddim 2 hands Windfield.lat / lon / vnorth[0, :] / veast[0, :] to the library."""
+    got = {}
+
+    class FakeCtx:
+        def set_windfield(self, lat, lon, vn, ve):
+            got.update(lat=lat, lon=lon, vn=vn, ve=ve)
+
+        def kinematics(self, *a, **k):
+            raise _lib.AccelUnavailable('stop here')
+
+    w = types.SimpleNamespace(winddim=2, lat=np.array([1.0, 2.0]), lon=np.array([3.0, 4.0]),
+                              vnorth=np.array([[5.0, 6.0], [0.0, 0.0]]), veast=np.array([[7.0, 8.0], [0.0, 0.0]]))
+    traf = types.SimpleNamespace(wind=w)
+    for k in ('tas', 'hdg', 'alt', 'vs', 'lat', 'lon', 'bank', 'eps'):
+        setattr(traf, k, np.zeros(2))
+    traf.pilot = types.SimpleNamespace(tas=np.zeros(2), hdg=np.zeros(2), alt=np.zeros(2), vs=np.zeros(2))
+    traf.perf = types.SimpleNamespace(acceleration=lambda: np.zeros(2))
+    with pytest.raises(_lib.AccelUnavailable):
+        kinematics.step(traf, 0.05, ctx=FakeCtx())
+    assert np.array_equal(got['vn'], [5.0, 6.0]) and np.array_equal(got['ve'], [7.0, 8.0])
 
 
 def test_workloads():
