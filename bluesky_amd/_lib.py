@@ -147,6 +147,7 @@ SIGNATURES.update({
     'bsa_geo_last_ms': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_sim_acdata_request': (ctypes.c_int, [_vp]),
     'bsa_set_windfield': (ctypes.c_int, [_vp, ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp]),
+    'bsa_sim_set_limits': (ctypes.c_int, [_vp] + [_c_dp] * 6),
     'bsa_sim_acdata_poll': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(AcData)]),
 })
 
@@ -267,6 +268,17 @@ class Context:
             ptr(o['tcpa']), ptr(o['tinconf']), ptr(o['dcpa']), ptr(o['li'], _c_i32p),
             ptr(o['lj'], _c_i32p), ptr(o['inconf'], _c_u8p), ptr(o['tcpamax'])), 'bsa_fetch_pairs')
         return o
+
+    ENVELOPE_FIELDS = ('hmax', 'vmin', 'vmax', 'vsmin', 'vsmax', 'axmax')
+
+    def sim_set_limits(self, env=None):
+        """OpenAP envelope for Pilot.applylimits in the resident step (bsa_sim_set_limits);
+        ``env`` = dict of the six per-aircraft arrays, None switches the limits off."""
+        if env is None:
+            self.check(self.lib.bsa_sim_set_limits(self.h, *([None] * 6)), 'bsa_sim_set_limits')
+            return
+        arrs = [f64(env[k]).ravel() for k in self.ENVELOPE_FIELDS]
+        self.check(self.lib.bsa_sim_set_limits(self.h, *[ptr(a) for a in arrs]), 'bsa_sim_set_limits')
 
     # ---------------------------------------------------------------- wind field
     def set_windfield(self, lat=None, lon=None, vnorth=None, veast=None):

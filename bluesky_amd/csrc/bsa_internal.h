@@ -231,6 +231,9 @@ struct Ctx {
   // ACDATA feed of the resident sim (bsa_feed.hip): traf.cas of the last step,
   // device staging, pinned host mirror, completion event
   DevBuf s_cas, feed_dev;
+  // OpenAP flight envelope of the resident sim (bsa_sim_set_limits) + traf.ax
+  DevBuf s_env, s_ax;
+  bool sim_limits = false;
   void *feed_host = nullptr;
   size_t feed_host_bytes = 0;
   hipEvent_t feed_ev = nullptr;

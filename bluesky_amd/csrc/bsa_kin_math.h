@@ -73,6 +73,53 @@ __device__ __forceinline__ double nprem(double a, double b) {
   return mod;
 }
 
+// vatmos (aero.py:62-74): pressure and density at altitude h [m]
+__device__ __forceinline__ void vatmos(double h, double &p, double &rho, double &T) {
+  T = npmax(288.15 - 0.0065 * h, kTstrat);
+  const double rhotrop = 1.225 * pow(T / 288.15, 4.256848030018761);
+  const double dhstrat = npmax(0., h - 11000.);
+  rho = rhotrop * exp(-dhstrat / 6341.552161);
+  p = rho * kRgas * T;
+}
+
+// aero.py:139-147 vtas2cas, aero.py:128-136 vcas2tas
+__device__ __forceinline__ double vtas2cas(double tas, double h) {
+  double p, rho, T;
+  vatmos(h, p, rho, T);
+  const double qdyn = p * (pow(1. + rho * tas * tas / (7. * p), 3.5) - 1.);
+  const double cas = sqrt(7. * kP0 / kRho0 * (pow(qdyn / kP0 + 1., 2. / 7.) - 1.));
+  return tas < 0 ? -1 * cas : cas;
+}
+__device__ __forceinline__ double vcas2tas(double cas, double h) {
+  double p, rho, T;
+  vatmos(h, p, rho, T);
+  const double qdyn = kP0 * (pow(1. + kRho0 * cas * cas / (7. * kP0), 3.5) - 1.);
+  const double tas = sqrt(7. * p / rho * (pow(1. + qdyn / p, 2. / 7.) - 1.));
+  return cas < 0 ? -1 * tas : tas;
+}
+
+// per-aircraft OpenAP flight envelope (perfoap.py:185-209; vmin / vmax are CAS)
+struct Envelope {
+  double hmax, vmin, vmax, vsmin, vsmax, axmax;
+};
+
+// OpenAP.limits as Pilot.applylimits applies it (pilot.py:65-68) to the
+// pilot's tas / vs / alt; ax = traf.ax of the previous step.
+__device__ __forceinline__ void openap_limits(const Envelope &e, double ax, double &tas, double &vs,
+                                              double &h) {
+  const double allow_h = h > e.hmax ? e.hmax : h;
+  const double intent_v_cas = vtas2cas(tas, allow_h);
+  double allow_v_cas = intent_v_cas < e.vmin ? e.vmin : intent_v_cas;
+  allow_v_cas = intent_v_cas > e.vmax ? e.vmax : allow_v_cas;
+  const double allow_v_tas = vcas2tas(allow_v_cas, allow_h);
+  const double vs_max_with_acc = (1 - ax / e.axmax) * e.vsmax;
+  double allow_vs = vs > e.vsmax ? vs_max_with_acc : vs;
+  allow_vs = vs < e.vsmin ? e.vsmin : allow_vs;
+  tas = allow_v_tas;
+  vs = allow_vs;
+  h = allow_h;
+}
+
 struct In {
   double tas, hdg, alt, vs, lat, lon;       // state before the step
   double ptas, phdg, palt, pvs;             // pilot targets
@@ -93,11 +140,8 @@ __device__ __forceinline__ Out step(const In &s, double simdt, int winddim, doub
   o.delspd = delta_spd;
   const double tas = s.tas + o.ax * simdt;
   // vatmos(alt) (aero.py:62-74), shared by vtas2cas and vtas2mach
-  const double T = npmax(288.15 - 0.0065 * s.alt, kTstrat);
-  const double rhotrop = 1.225 * pow(T / 288.15, 4.256848030018761);
-  const double dhstrat = npmax(0., s.alt - 11000.);
-  const double rho = rhotrop * exp(-dhstrat / 6341.552161);
-  const double p = rho * kRgas * T;
+  double p, rho, T;
+  vatmos(s.alt, p, rho, T);
   const double qdyn = p * (pow(1. + rho * tas * tas / (7. * p), 3.5) - 1.);
   double cas = sqrt(7. * kP0 / kRho0 * (pow(qdyn / kP0 + 1., 2. / 7.) - 1.));
   o.cas = tas < 0 ? -1 * cas : cas;

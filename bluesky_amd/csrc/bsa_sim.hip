@@ -37,6 +37,9 @@ namespace bsa {
 struct SimDev {
   double *lat, *lon, *trk, *gs, *alt, *vs, *tas, *hdg, *gse, *gsn;
   double *cas;                     // traf.cas (traffic.py:434), kept for the ACDATA feed
+  double *ax;                      // traf.ax (traffic.py:431), read by the OpenAP limits next step
+  const double *env;               // OpenAP envelope, 6 x n (hmax vmin vmax vsmin vsmax axmax) or NULL
+  int n;
   const double *aptrk, *aptas, *apalt, *apvs, *bank, *eps, *accel;
   const double *atrk, *atas, *avs, *aalt;
   const uint8_t *active;
@@ -78,6 +81,11 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   } else {
     s.phdg = kin::nprem(ptrk, 360.);                  // pilot.py:63
   }
+  if (d.env) {  // Pilot.applylimits (pilot.py:65-68, OpenAP), traffic.py:404
+    const kin::Envelope e{d.env[k], d.env[d.n + k], d.env[2 * d.n + k], d.env[3 * d.n + k],
+                          d.env[4 * d.n + k], d.env[5 * d.n + k]};
+    kin::openap_limits(e, d.ax[k], s.ptas, s.pvs, s.palt);
+  }
   s.tas = d.tas[k];
   s.hdg = d.hdg[k];
   s.alt = d.alt[k];
@@ -99,6 +107,7 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   d.gse[k] = o.gseast;
   d.gsn[k] = o.gsnorth;
   d.cas[k] = o.cas;
+  d.ax[k] = o.ax;
 }
 
 // field list of one all-gather: fp64 arrays (full n) + optionally one uint8 array
@@ -141,6 +150,9 @@ static SimDev sim_dev(Ctx *c) {
   d.gse = (double *)c->s_gse.p;
   d.gsn = (double *)c->s_gsn.p;
   d.cas = (double *)c->s_cas.p;
+  d.ax = (double *)c->s_ax.p;
+  d.env = c->sim_limits ? (const double *)c->s_env.p : nullptr;
+  d.n = (int)c->n;
   d.aptrk = (const double *)c->s_aptrk.p;
   d.aptas = (const double *)c->s_aptas.p;
   d.apalt = (const double *)c->s_apalt.p;
@@ -213,7 +225,7 @@ void sim_release(Ctx *c) {
   DevBuf *all[] = {&c->red, &c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
-                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl, &c->s_cas};
+                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl, &c->s_cas, &c->s_ax, &c->s_env};
   for (auto *b : all) release(*b);
   bk_release(c);
   if (c->comm) {
@@ -345,8 +357,10 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   if (!bsa::ensure(c, c->s_atrk, N8, "asas trk") || !bsa::ensure(c, c->s_atas, N8, "asas tas") ||
       !bsa::ensure(c, c->s_avs, N8, "asas vs") || !bsa::ensure(c, c->s_ase, (size_t)n * 4, "asase") ||
       !bsa::ensure(c, c->s_asn, (size_t)n * 4, "asasn") || !bsa::ensure(c, c->s_active, n, "active") ||
-      !bsa::ensure(c, c->s_cas, N8, "cas"))
+      !bsa::ensure(c, c->s_cas, N8, "cas") || !bsa::ensure(c, c->s_ax, N8, "ax"))
     return -1;
+  BSA_HIP(c, hipMemsetAsync(c->s_ax.p, 0, N8, c->stream));   // traf.ax: 0 at create
+  c->sim_limits = false;
   BSA_HIP(c, hipMemsetAsync(c->s_cas.p, 0, N8, c->stream));  // traf.cas: 0 until the first step
   BSA_HIP(c, hipMemcpyAsync(c->s_atrk.p, s->trk, N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemcpyAsync(c->s_atas.p, s->tas, N8, hipMemcpyHostToDevice, c->stream));
@@ -427,6 +441,28 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     c->cand_cap = std::max(2 * c->cand_cap,
                            (unsigned long long)bsa::kCandShards * (worst + worst / 4 + 1024));
   }
+  return 0;
+}
+
+int bsa_sim_set_limits(bsa_ctx *cc, const double *hmax, const double *vmin, const double *vmax,
+                       const double *vsmin, const double *vsmax, const double *axmax) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_set_limits before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (!hmax) {
+    c->sim_limits = false;
+    return 0;
+  }
+  const double *src[6] = {hmax, vmin, vmax, vsmin, vsmax, axmax};
+  for (auto q : src)
+    if (!q) return bsa::fail(c, "bsa_sim_set_limits: NULL envelope array");
+  const size_t N8 = (size_t)c->n * 8;
+  if (!bsa::ensure(c, c->s_env, 6 * N8, "OpenAP envelope")) return -1;
+  for (int k = 0; k < 6; ++k)
+    BSA_HIP(c, hipMemcpyAsync((char *)c->s_env.p + k * N8, src[k], N8, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  c->sim_limits = true;
   return 0;
 }
 

@@ -64,9 +64,11 @@ def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, res
 class ResidentSim:
     """Device-resident traffic; ``rank``/``world`` > 1 shards the rows over GPUs."""
 
-    def __init__(self, state, p, ctx=None, rank=0, world=1, windfield=None):
+    def __init__(self, state, p, ctx=None, rank=0, world=1, windfield=None, limits=None):
         """``windfield``: dict(lat, lon, vnorth, veast) of the 2-D field's points
-        (Windfield.lat / lon / vnorth[0, :] / veast[0, :]) for ``winddim`` 2."""
+        (Windfield.lat / lon / vnorth[0, :] / veast[0, :]) for ``winddim`` 2.
+        ``limits``: per-aircraft OpenAP envelope dict(hmax, vmin, vmax, vsmin,
+        vsmax, axmax) for Pilot.applylimits (pilot.py:65-68), or None."""
         self.ctx = ctx or _lib.default_context()
         self.rank, self.world = rank, world
         if world > 1:
@@ -75,6 +77,8 @@ class ResidentSim:
             self.ctx.set_windfield(windfield['lat'], windfield['lon'], windfield['vnorth'],
                                    windfield['veast'])
         self.ctx.sim_init(state, p)
+        if limits is not None:
+            self.ctx.sim_set_limits(limits)
         self.params = p
 
     def step(self, nsteps=1):

@@ -20,6 +20,8 @@
  *       bluesky/traffic/windfield.py:158-179         Windfield.getdata, 2-D field
  *   bsa_qdrdist
  *       bluesky/tools/geo.py:110-162,347-363         qdrdist_matrix / kwikqdrdist_matrix, materialised
+ *   bsa_sim_set_limits
+ *       bluesky/traffic/pilot.py:65-68 + performance/openap/perfoap.py:185-209  applylimits (OpenAP)
  *   bsa_sim_acdata_*
  *       bluesky/simulation/qtgl/screenio.py:194-239  send_aircraft_data (ACDATA stream fields)
  *   bsa_sim_*     GPU-resident chain of the above, no reference equivalent
@@ -313,6 +315,17 @@ typedef struct bsa_sim_out {
 int bsa_sim_init(bsa_ctx *ctx, int64_t n, const bsa_sim_state *s, const bsa_sim_params *p);
 /* Advance nsteps; collective when a communicator is set. */
 int bsa_sim_step(bsa_ctx *ctx, int nsteps);
+/* Pilot.applylimits with the OpenAP model (pilot.py:65-68 ->
+ * performance/openap/perfoap.py:185-209) inside the step, between
+ * Pilot.APorASAS and UpdateAirSpeed (traffic.py:397-407): the pilot's tas /
+ * vs / alt are clipped to a per-aircraft envelope (full-n host arrays, copied:
+ * hmax [m], vmin / vmax [m/s CAS], vsmin / vsmax [m/s], axmax [m/s^2]), the
+ * vertical-speed cap scaled by (1 - ax/axmax) with ax = traf.ax of the
+ * previous step (0 after bsa_sim_init).  The envelope is a frozen input
+ * (OpenAP's per-phase table update, perfoap.py:115-183, is not modelled);
+ * hmax == NULL switches the limits off (the default after bsa_sim_init). */
+int bsa_sim_set_limits(bsa_ctx *ctx, const double *hmax, const double *vmin, const double *vmax,
+                       const double *vsmin, const double *vsmax, const double *axmax);
 /* Full-n host copies of the state (collective: gathers all ranks' rows).
  * Any pointer may be NULL. */
 int bsa_sim_read(bsa_ctx *ctx, bsa_sim_out *o);

@@ -84,6 +84,30 @@ def update_airspeed(s, simdt):
     return o
 
 
+def vcas2tas(cas, h):
+    """aero.py:128-136."""
+    p, rho, T = vatmos(h)
+    qdyn = p0 * ((1. + rho0 * cas * cas / (7. * p0)) ** 3.5 - 1.)
+    tas = np.sqrt(7. * p / rho * ((1. + qdyn / p) ** (2. / 7.) - 1.))
+    return np.where(cas < 0, -1 * tas, tas)
+
+
+def openap_limits(intent_v_tas, intent_vs, intent_h, ax, env):
+    """OpenAP.limits (performance/openap/perfoap.py:185-209), applied by
+    Pilot.applylimits (pilot.py:65-68) to the pilot's tas / vs / alt.
+    env: per-aircraft envelope dict(hmax, vmin, vmax, vsmin, vsmax, axmax)
+    (vmin / vmax are CAS); ax: traf.ax of the previous step."""
+    allow_h = np.where(intent_h > env['hmax'], env['hmax'], intent_h)
+    intent_v_cas = vtas2cas(intent_v_tas, allow_h)
+    allow_v_cas = np.where(intent_v_cas < env['vmin'], env['vmin'], intent_v_cas)
+    allow_v_cas = np.where(intent_v_cas > env['vmax'], env['vmax'], allow_v_cas)
+    allow_v_tas = vcas2tas(allow_v_cas, allow_h)
+    vs_max_with_acc = (1 - ax / env['axmax']) * env['vsmax']
+    allow_vs = np.where(intent_vs > env['vsmax'], vs_max_with_acc, intent_vs)
+    allow_vs = np.where(intent_vs < env['vsmin'], env['vsmin'], allow_vs)
+    return allow_v_tas, allow_vs, allow_h
+
+
 def windfield_2d(lat, lon, wlat, wlon, wvnorth, wveast):
     """Windfield.getdata for a 2-D field (winddim 2, windfield.py:158-179):
     inverse-distance-squared weights in a flat frame of 1-degree units.

@@ -73,6 +73,9 @@ def sim_step(st, p, do_cd, bk=None):
         phdg = (ptrk + np.degrees(steer)) % 360.
     else:
         phdg = ptrk % 360.
+    env = p.get('limits')
+    if env is not None:                                       # pilot.py:65-68 (OpenAP)
+        ptas, pvs, palt = okin.openap_limits(ptas, pvs, palt, st.get('ax', np.zeros(n)), env)
     s = dict(tas=st['tas'], hdg=st['hdg'], alt=st['alt'], vs=st['vs'], lat=st['lat'], lon=st['lon'],
              ptas=ptas, phdg=phdg, palt=palt, pvs=pvs, bank=st['bank'], eps=st['eps'],
              accel=st['accel'])
@@ -80,7 +83,7 @@ def sim_step(st, p, do_cd, bk=None):
         o = okin.step(s, p['simdt'], winddim=1, windnorth=wind[0], windeast=wind[1])
     else:
         o = okin.step(s, p['simdt'])
-    for k in ('tas', 'hdg', 'alt', 'vs', 'lat', 'lon', 'gs', 'trk', 'gseast', 'gsnorth'):
+    for k in ('tas', 'hdg', 'alt', 'vs', 'lat', 'lon', 'gs', 'trk', 'gseast', 'gsnorth', 'ax'):
         st[k] = np.asarray(o[k], dtype=np.float64)
     assert len(st['lat']) == n
     return st

@@ -216,3 +216,40 @@ def test_resident_windfield_matches_oracle(ctx):
     ctx.set_windfield()
     with pytest.raises(Exception, match='wind field'):
         sim.step(1)
+
+
+def test_resident_openap_limits_match_oracle(ctx):
+    """Pilot.applylimits with an OpenAP envelope (pilot.py:65-68, perfoap.py:185-209)
+    between APorASAS and UpdateAirSpeed; the envelope clips most aircraft."""
+    t = synth.box(1500, 60.0, seed=41)
+    init = resident.initial_state(t)
+    rng = np.random.default_rng(41)
+    n = t.ntraf
+    init['ap_vs'] = rng.choice([0.0, 5.0, 25.0], n)
+    init['ap_tas'] = init['tas'] * rng.choice([0.6, 1.0, 1.3], n)
+    init['ap_alt'] = init['alt'] + rng.choice([0.0, 3000.0, -3000.0], n)
+    env = dict(hmax=np.full(n, 11500.0), vmin=rng.uniform(70., 90., n), vmax=rng.uniform(140., 160., n),
+               vsmin=np.full(n, -15.0), vsmax=rng.uniform(8., 12., n), axmax=np.full(n, 2.0))
+    p = resident.params(cd_every=2)
+    sim = resident.ResidentSim(init, p, ctx=ctx, limits=env)
+    op = oracle_params(p)
+    op['limits'] = env
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(n), active=np.zeros(n, bool), ax=np.zeros(n))
+    for k in range(4):
+        exp = ostep.sim_step(prev, op, do_cd=(k % 2 == 0))
+        sim.step(1)
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        got['ax'] = exp['ax']      # traf.ax is device-internal; the oracle's is carried over
+        prev = got
+    # the envelope binds: without it the oracle's first step already differs
+    free = dict(op)
+    free.pop('limits')
+    s0 = dict(init)
+    s0.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(), asas_vs=np.zeros(n),
+              active=np.zeros(n, bool), ax=np.zeros(n))
+    a, b = ostep.sim_step(s0, op, do_cd=True), ostep.sim_step(s0, free, do_cd=True)
+    assert np.mean(a['tas'] != b['tas']) > 0.1 and np.any(a['vs'] != b['vs'])
+    ctx.sim_set_limits(None)

@@ -158,3 +158,17 @@ def test_oracle_geo_matches_reference(path):
 def test_geo_fixtures_present():
     kinds = {(str(np.load(p)['fn']), str(np.load(p)['mode'])) for p in GEO}
     assert kinds == {('qdrdist', 'outer'), ('qdrdist', 'pairwise'), ('kwik', 'outer'), ('kwik', 'pairwise')}
+
+
+LIMITS = util.golden('limits_*.npz')
+
+
+@pytest.mark.parametrize('path', LIMITS, ids=[util.case_name(p) for p in LIMITS])
+def test_oracle_openap_limits_matches_reference(path):
+    """OpenAP.limits (perfoap.py:185-209) as Pilot.applylimits applies it."""
+    z = np.load(path)
+    env = {k: z[k] for k in ('hmax', 'vmin', 'vmax', 'vsmin', 'vsmax', 'axmax')}
+    t, v, h = okin.openap_limits(z['tas'], z['vs'], z['h'], z['ax'], env)
+    for k, got in (('tas', t), ('vs', v), ('alt', h)):
+        ok, msg = util.close(got, z['out_' + k], 1.0, rtol=1e-12)
+        assert ok, '%s: %s' % (k, msg)

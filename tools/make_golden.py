@@ -369,6 +369,34 @@ def run_kin(name, n, seed, dt, wind=None):
     print('kin_%-17s N=%5d dt=%g wind=%s' % (name, n, dt, wind))
 
 
+def run_limits(name, n, seed):
+    """OpenAP.limits (perfoap.py:185-209) on a per-aircraft envelope: the
+    reference's own method on an OpenAP instance made without __init__ (its
+    tables are not needed: limits only reads the six envelope arrays)."""
+    from bluesky.traffic.performance.openap.perfoap import OpenAP
+    rng = np.random.default_rng(seed)
+    env = dict(hmax=rng.uniform(9000., 13000., n), vmin=rng.uniform(50., 80., n),
+               vmax=rng.uniform(150., 180., n), vsmin=-rng.uniform(10., 25., n),
+               vsmax=rng.uniform(8., 20., n), axmax=rng.uniform(1.0, 3.0, n))
+    tas = rng.uniform(20., 320., n)
+    vs = rng.uniform(-30., 30., n)
+    h = rng.uniform(0., 14000., n)
+    ax = rng.choice([0.0, 0.5, -0.5, 2.0], n)
+    tas[:3] = [0.0, -5.0, 1e-3]
+    h[3:6] = [env['hmax'][3], 0.0, 11000.]
+    vs[6:8] = [env['vsmax'][6], env['vsmin'][7]]
+    perf = OpenAP.__new__(OpenAP)
+    for k, v in env.items():
+        object.__setattr__(perf, k, v)
+    rt, rv, rh = OpenAP.limits(perf, tas.copy(), vs.copy(), h.copy(), ax.copy())
+    ot, ov, oh = okin.openap_limits(tas, vs, h, ax, env)
+    for a, b, k in ((rt, ot, 'tas'), (rv, ov, 'vs'), (rh, oh, 'alt')):
+        assert np.array_equal(a, b, equal_nan=True), 'oracle != reference limits %s' % k
+    np.savez_compressed(os.path.join(OUT, 'limits_%s.npz' % name), tas=tas, vs=vs, h=h, ax=ax,
+                        out_tas=rt, out_vs=rv, out_alt=rh, **env)
+    print('limits_%-14s N=%5d' % (name, n))
+
+
 def run_asas(name, traf, ncalls=4, dt=20.0):
     """Reference ASAS.update (asas.py:473-504) incl. ResumeNav on a stand-in
     bs.traf; state advanced along straight tracks between CD calls."""
@@ -497,6 +525,9 @@ def main():
         for name in KWIK_CASES:
             run_kwik(name, *cds[name])
         return
+    if '--limits-only' in sys.argv:
+        run_limits('openap2000', 2000, 71)
+        return
     if '--windfield-only' in sys.argv:
         run_kin('windfield1500', 1500, 34, 0.05, wind=WIND_FIELD)
         return
@@ -520,6 +551,7 @@ def main():
     run_kin('nowind_dt1', 500, 32, 1.0)
     run_kin('wind1000', 1000, 33, 0.05, wind=(270.0, 25.0 * kts))
     run_kin('windfield1500', 1500, 34, 0.05, wind=WIND_FIELD)
+    run_limits('openap2000', 2000, 71)
     for case in geo_cases():
         run_geo(*case)
 
