@@ -8,6 +8,7 @@
 // has completed (or waits for it).  No collective: each rank serves its own
 // rows [row_begin, row_end), concatenated in rank order by the caller.
 #include "bsa_internal.h"
+#include "bsa_kin_math.h"
 
 namespace bsa {
 
@@ -17,7 +18,8 @@ constexpr int kFeedF64 = 9;  // lat lon alt tas cas gs trk vs tcpamax
 static size_t feed_bytes(int64_t nr) { return 64 + (size_t)nr * (kFeedF64 * 8 + 2 * 4 + 1); }
 
 struct FeedSrc {
-  const double *f[kFeedF64 - 1];        // lat lon alt tas cas gs trk vs (full n, row k)
+  const double *f[kFeedF64 - 1];        // lat lon alt tas [altprev] gs trk vs (full n, row k)
+  int stepped;                          // a step ran: slot 4 holds the pre-step altitude
   const double *tcpamax;                // last CD call's rows (row k - rb), may be NULL
   const float *asasn, *asase;           // full n
   const uint8_t *inconf;                // last CD call's rows, may be NULL
@@ -33,6 +35,9 @@ __global__ __launch_bounds__(256) void k_feed_pack(int64_t rb, int64_t nr, FeedS
   const int64_t k = rb + r;
 #pragma unroll
   for (int f = 0; f < kFeedF64 - 1; ++f) f64[f * nr + r] = s.f[f][k];
+  // traf.cas = vtas2cas(tas, alt) in UpdateAirSpeed, i.e. with the step's new
+  // tas and its pre-step altitude (traffic.py:434, before UpdatePosition)
+  f64[4 * nr + r] = s.stepped ? kin::vtas2cas(s.f[3][k], s.f[4][k]) : 0.0;
   f64[(kFeedF64 - 1) * nr + r] = s.tcpamax ? s.tcpamax[r] : 0.0;
   float *f32 = (float *)(f64 + kFeedF64 * nr);
   f32[r] = s.asasn[k];
@@ -49,7 +54,6 @@ void feed_release(Ctx *c) {
   c->feed_host_bytes = 0;
   c->feed_pending = false;
   release(c->feed_dev);
-  release(c->s_cas);
 }
 
 static int feed_request(Ctx *c) {
@@ -70,8 +74,9 @@ static int feed_request(Ctx *c) {
   const bool have_cd = c->sim_cd_calls > 0 && c->inconf.p && c->last_rb == rb && c->last_re == c->sim_re;
   FeedSrc s;
   const void *src[kFeedF64 - 1] = {c->own[0].p, c->own[1].p, c->own[4].p, c->s_tas.p,
-                                   c->s_cas.p, c->own[3].p, c->own[2].p, c->own[5].p};
+                                   c->s_altprev.p, c->own[3].p, c->own[2].p, c->own[5].p};
   for (int f = 0; f < kFeedF64 - 1; ++f) s.f[f] = (const double *)src[f];
+  s.stepped = c->sim_steps > 0;
   s.tcpamax = have_cd ? (const double *)c->tcpamax.p : nullptr;
   s.inconf = have_cd ? (const uint8_t *)c->inconf.p : nullptr;
   s.asasn = (const float *)c->s_asn.p;

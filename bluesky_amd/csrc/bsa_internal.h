@@ -228,9 +228,9 @@ struct Ctx {
   hipEvent_t geo_ev[2] = {nullptr, nullptr};
   double geo_ms = 0.0;
 
-  // ACDATA feed of the resident sim (bsa_feed.hip): traf.cas of the last step,
-  // device staging, pinned host mirror, completion event
-  DevBuf s_cas, feed_dev;
+  // ACDATA feed of the resident sim (bsa_feed.hip): pre-step altitude of the
+  // last step (for traf.cas), device staging, pinned host mirror, completion event
+  DevBuf s_altprev, feed_dev;
   // OpenAP flight envelope of the resident sim (bsa_sim_set_limits) + traf.ax
   DevBuf s_env, s_ax;
   bool sim_limits = false;

@@ -36,7 +36,8 @@ namespace bsa {
 
 struct SimDev {
   double *lat, *lon, *trk, *gs, *alt, *vs, *tas, *hdg, *gse, *gsn;
-  double *cas;                     // traf.cas (traffic.py:434), kept for the ACDATA feed
+  double *altprev;                 // pre-step altitude: the ACDATA feed derives traf.cas =
+                                   // vtas2cas(tas, altprev) (traffic.py:434) off the step
   double *ax;                      // traf.ax (traffic.py:431), read by the OpenAP limits next step
   const double *env;               // OpenAP envelope, 6 x n (hmax vmin vmax vsmin vsmax axmax) or NULL
   int n;
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   d.trk[k] = o.trk;
   d.gse[k] = o.gseast;
   d.gsn[k] = o.gsnorth;
-  d.cas[k] = o.cas;
+  d.altprev[k] = s.alt;
   d.ax[k] = o.ax;
 }
 
@@ -149,7 +150,7 @@ static SimDev sim_dev(Ctx *c) {
   d.hdg = (double *)c->s_hdg.p;
   d.gse = (double *)c->s_gse.p;
   d.gsn = (double *)c->s_gsn.p;
-  d.cas = (double *)c->s_cas.p;
+  d.altprev = (double *)c->s_altprev.p;
   d.ax = (double *)c->s_ax.p;
   d.env = c->sim_limits ? (const double *)c->s_env.p : nullptr;
   d.n = (int)c->n;
@@ -225,7 +226,7 @@ void sim_release(Ctx *c) {
   DevBuf *all[] = {&c->red, &c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
-                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl, &c->s_cas, &c->s_ax, &c->s_env};
+                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env};
   for (auto *b : all) release(*b);
   bk_release(c);
   if (c->comm) {
@@ -357,11 +358,10 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   if (!bsa::ensure(c, c->s_atrk, N8, "asas trk") || !bsa::ensure(c, c->s_atas, N8, "asas tas") ||
       !bsa::ensure(c, c->s_avs, N8, "asas vs") || !bsa::ensure(c, c->s_ase, (size_t)n * 4, "asase") ||
       !bsa::ensure(c, c->s_asn, (size_t)n * 4, "asasn") || !bsa::ensure(c, c->s_active, n, "active") ||
-      !bsa::ensure(c, c->s_cas, N8, "cas") || !bsa::ensure(c, c->s_ax, N8, "ax"))
+      !bsa::ensure(c, c->s_altprev, N8, "pre-step altitude") || !bsa::ensure(c, c->s_ax, N8, "ax"))
     return -1;
   BSA_HIP(c, hipMemsetAsync(c->s_ax.p, 0, N8, c->stream));   // traf.ax: 0 at create
   c->sim_limits = false;
-  BSA_HIP(c, hipMemsetAsync(c->s_cas.p, 0, N8, c->stream));  // traf.cas: 0 until the first step
   BSA_HIP(c, hipMemcpyAsync(c->s_atrk.p, s->trk, N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemcpyAsync(c->s_atas.p, s->tas, N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemsetAsync(c->s_avs.p, 0, N8, c->stream));
