@@ -36,6 +36,7 @@ PF_FLOPS_PER_PAIR = 9        # prefilter stage-1 fp32 flops per tested pair (DES
 KIN_BYTES_PER_AC = 234       # K4 algorithmic HBM bytes per aircraft-step
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E (spec)
 PMC_JSON = os.path.join(REPO, 'profiles', 'pmc_latest.json')
+TIMING_SAMPLE = 4            # detects per HIP-event-timed detect (bsa_set_timing_sample)
 
 
 def pmc_figures():
@@ -147,6 +148,9 @@ def main():
     if world != args.gpus:
         world = max(world, 1)
     ctx = _lib.Context(local)
+    # HIP-event stage timing of one detect in TIMING_SAMPLE, inside the timed
+    # region (each event record leaves a ~5 us gap before the next kernel)
+    ctx.set_timing_sample(TIMING_SAMPLE)
     if args.reuse:
         ctx.set_candidate_reuse(True, args.reuse[0], args.reuse[1])
     t = synth.workload(args.workload, n=args.n, seed=7)
@@ -212,7 +216,8 @@ def main():
                       if args.reuse else None),
                roofline=roof,
                kernels_ms_rank0=dict(k0_prep=tm['prep'], prefilter=tm['prefilter'], exact=tm['exact'],
-                                     k2_sort=tm['sort'], detect_total=tm['total']),
+                                     k2_sort=tm['sort'], detect_total=tm['total'],
+                                     timed_detects='1 in %d' % TIMING_SAMPLE),
                prefilter_pair_tests_rank0=tested,
                tile_pairs_rank0=ts['tiles'] / max(ts['detects'], 1),
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),

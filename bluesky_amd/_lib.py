@@ -62,6 +62,7 @@ SIGNATURES = {
     'bsa_timing_reset': (ctypes.c_int, [_vp]),
     'bsa_set_candidate_capacity': (ctypes.c_int, [_vp, ctypes.c_int64]),
     'bsa_timing_summary': (ctypes.c_int, [_vp, _c_dp, _c_i64p]),
+    'bsa_set_timing_sample': (ctypes.c_int, [_vp, ctypes.c_int]),
 }
 
 PRIO_CODES = {'FF1': 1, 'FF2': 2, 'FF3': 3, 'LAY1': 4, 'LAY2': 5}
@@ -370,6 +371,10 @@ class Context:
         t = np.zeros(5)
         self.check(self.lib.bsa_last_timings(self.h, ptr(t)), 'bsa_last_timings')
         return dict(prep=t[0], prefilter=t[1], exact=t[2], sort=t[3], total=t[4])
+
+    def set_timing_sample(self, every):
+        """Time one detect in ``every`` (bsa_set_timing_sample; 0 = none)."""
+        self.check(self.lib.bsa_set_timing_sample(self.h, int(every)), 'bsa_set_timing_sample')
 
     def timing_reset(self):
         """Forget recorded detect timings / statistics (bsa_timing_reset)."""

@@ -1313,7 +1313,10 @@ static int next_events(Ctx *c, hipEvent_t **ev) {
   if ((int)c->evpool.size() < 5 * (k + 1)) {
     const size_t old = c->evpool.size();
     c->evpool.resize(5 * (size_t)(k + 1), nullptr);
-    for (size_t q = old; q < c->evpool.size(); ++q) BSA_HIP(c, hipEventCreate(&c->evpool[q]));
+    // timing-only events: no system-scope fence at record (a fenced record left a
+    // ~6 us bubble before the next kernel, 5 per detect; only elapsed times are read)
+    for (size_t q = old; q < c->evpool.size(); ++q)
+      BSA_HIP(c, hipEventCreateWithFlags(&c->evpool[q], hipEventDisableSystemFence));
   }
   *ev = &c->evpool[5 * (size_t)k];
   c->ev_last = k;
@@ -1362,9 +1365,16 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // BSA_STAGE1_T0 environment variable selects t = 0 for A/B measurements
   static const bool t0_env = getenv("BSA_STAGE1_T0") && atoi(getenv("BSA_STAGE1_T0")) != 0;
   const int mid = (!reuse && !kwik && !(flags & BSA_FLAG_STAGE1_T0) && !t0_env) ? 1 : 0;
+  // stage events of this detect: only one detect in ev_every is timed (each
+  // record costs a ~5 us bubble before the next kernel, bsa_set_timing_sample)
   hipEvent_t *ev = nullptr;
-  if (next_events(c, &ev)) return -1;
-  BSA_HIP(c, hipEventRecord(ev[0], c->stream));
+  const bool timed = c->ev_every > 0 && (c->ev_count++ % c->ev_every) == 0;
+  if (timed && next_events(c, &ev)) return -1;
+  auto mark = [&](int e) -> int {
+    if (timed) BSA_HIP(c, hipEventRecord(ev[e], c->stream));
+    return 0;
+  };
+  if (mark(0)) return -1;
   Counters *dcnt = (Counters *)c->counters.p;
   // K0z: zero the per-detect state (launched once the reuse decision is known)
   auto zero = [&](bool keep, unsigned *rctl, int rforce) -> int {
@@ -1379,8 +1389,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (n == 0 || nrows == 0) {
     if (zero(false, nullptr, 0)) return -1;
     if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
-    for (int e = 1; e < 5; ++e) BSA_HIP(c, hipEventRecord(ev[e], c->stream));
-    c->ev_valid = true;
+    for (int e = 1; e < 5; ++e)
+      if (mark(e)) return -1;
+    c->ev_valid = c->ev_valid || timed;
     c->empty_detect = true;
     return 0;
   }
@@ -1517,7 +1528,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + 255) / 256)), dim3(256), 0, c->stream, nrt, nct,
                      tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p, &dcnt->tiles, build);
   BSA_HIP(c, hipGetLastError());
-  BSA_HIP(c, hipEventRecord(ev[1], c->stream));
+  if (mark(1)) return -1;
 
   const float T = (float)(tla > 0.0 ? tla : 0.0);
   const float lim = (float)((rpz + kEABS + (reuse ? 2.0 * c->reuse_sh : 0.0)) / (1.0 - kE1));
@@ -1539,7 +1550,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build);
   BSA_HIP(c, hipGetLastError());
-  BSA_HIP(c, hipEventRecord(ev[2], c->stream));
+  if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count, one
   // resident round (4 workgroups per CU at its register budget)
   hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
@@ -1549,7 +1560,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      (unsigned *)c->rowcnt.p, kwik, reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
                      (const Snap *)c->snap_cur.p, (Snap *)c->snap_build.p, (int)n);
   BSA_HIP(c, hipGetLastError());
-  BSA_HIP(c, hipEventRecord(ev[3], c->stream));
+  if (mark(3)) return -1;
   // ---- K2: row offsets, scatter into row segments, per-row rank + gather
   const int nscan = (int)(2 * (nrows + 1));
   size_t scan_tmp = 0;
@@ -1572,8 +1583,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
                      (unsigned long long *)c->stats.p, gate, build);
   BSA_HIP(c, hipGetLastError());
-  BSA_HIP(c, hipEventRecord(ev[4], c->stream));
-  c->ev_valid = true;
+  if (mark(4)) return -1;
+  c->ev_valid = c->ev_valid || timed;
   return 0;
 }
 

@@ -330,10 +330,19 @@ int bsa_timing_reset(bsa_ctx *c) {
   BSA_HIP(c, hipSetDevice(c->device));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   c->ev_sets = 0;
+  c->ev_count = 0;
   c->ev_valid = false;
   if (!bsa::ensure(c, c->stats, 8 * 8, "detect statistics")) return -1;
   BSA_HIP(c, hipMemsetAsync(c->stats.p, 0, 8 * 8, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int bsa_set_timing_sample(bsa_ctx *c, int every) {
+  if (!c) return -1;
+  if (every < 0) return bsa::fail(c, "timing sample interval must be >= 0");
+  c->ev_every = every;
+  c->ev_count = 0;
   return 0;
 }
 

@@ -125,7 +125,7 @@ static int geo_run(Ctx *c, int64_t m, const double *lat1, const double *lon1, in
   BSA_HIP(c, hipMemcpyAsync(d_lat2, lat2, n * 8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemcpyAsync(d_lon2, lon2, n * 8, hipMemcpyHostToDevice, c->stream));
   for (int k = 0; k < 2; ++k)
-    if (!c->geo_ev[k]) BSA_HIP(c, hipEventCreate(&c->geo_ev[k]));
+    if (!c->geo_ev[k]) BSA_HIP(c, hipEventCreateWithFlags(&c->geo_ev[k], hipEventDisableSystemFence));
   GeoPt *p1 = nullptr, *p2 = nullptr;
   if (!pairwise && !kwik) {
     if (!ensure(c, c->geo_pts, (size_t)(m + n) * sizeof(GeoPt), "geo points")) return -1;

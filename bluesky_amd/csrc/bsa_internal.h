@@ -187,6 +187,8 @@ struct Ctx {
   // detect timing: one set of 5 events per detect since the last reset
   std::vector<hipEvent_t> evpool;
   int ev_sets = 0, ev_last = 0;
+  int ev_every = 1;       // time one detect in ev_every (0 = none), bsa_set_timing_sample
+  int64_t ev_count = 0;   // detects since the last bsa_timing_reset
   bool ev_valid = false;
   bool empty_detect = false;
   DevBuf stats;  // accumulated per-detect statistics {groups, candidates, tiles, detects, list builds}

@@ -161,6 +161,12 @@ int bsa_last_timings(bsa_ctx *ctx, double *ms5);
  * blocks swept, candidates, surviving tile pairs, detects}. */
 int bsa_timing_reset(bsa_ctx *ctx);
 int bsa_timing_summary(bsa_ctx *ctx, double *ms5, int64_t *stats4);
+/* Record the stage events of one detect in `every` (default 1 = all; 0 =
+ * none; counted from the last bsa_timing_reset, whose first detect is timed).
+ * Each event record costs a ~5 us gap before the next kernel, so the bench
+ * samples; bsa_last_timings then reports the last timed detect and
+ * bsa_timing_summary averages the timed ones. */
+int bsa_set_timing_sample(bsa_ctx *ctx, int every);
 
 /* ---------------------------------------------------------------- MVP
  * MVP.resolve (bluesky/traffic/asas/MVP.py:14-143) on the device-resident
