@@ -85,3 +85,43 @@ def test_workloads():
     assert t.ntraf == 2000 and len(t.id) == 2000
     g = synth.global_traffic(5000, seed=1)
     assert np.all(np.abs(g.lat) <= 70.5)
+
+
+class _GeoCtx:
+    """Records what bluesky_amd.geo hands to Context.qdrdist (no GPU needed)."""
+
+    def __init__(self):
+        self.calls = []
+
+    def qdrdist(self, lat1, lon1, lat2, lon2, kwik=False, pairwise=False):
+        la1, la2 = np.ravel(lat1), np.ravel(lat2)
+        self.calls.append((len(la1), len(la2), kwik, pairwise))
+        total = len(la1) if pairwise else len(la1) * len(la2)
+        return np.arange(total, dtype=np.float64), -np.arange(total, dtype=np.float64)
+
+
+def test_geo_operand_forms_and_result_types():
+    """bluesky_amd.geo mirrors geo.py's result types for the two operand forms
+    its callers use (metric.py row vectors, SSD.py 1-D arrays)."""
+    from bluesky_amd import geo
+    ctx = _GeoCtx()
+    a, b = np.linspace(0, 1, 3), np.linspace(0, 1, 4)
+    q, d = geo.qdrdist_matrix(np.asmatrix(a), np.asmatrix(a), np.asmatrix(b), np.asmatrix(b), ctx=ctx)
+    assert isinstance(q, np.matrix) and q.shape == (3, 4) and q[1, 0] == 4.0
+    q, d = geo.qdrdist_matrix(a, a, a, a, ctx=ctx)
+    assert isinstance(q, np.matrix) and q.shape == (1, 3)
+    q, d = geo.kwikqdrdist_matrix(a, a, a, a, ctx=ctx)
+    assert not isinstance(q, np.matrix) and q.shape == (3,)
+    q, d = geo.kwikqdrdist_matrix(a[None, :], a[None, :], a[None, :], a[None, :], ctx=ctx)
+    assert not isinstance(q, np.matrix) and q.shape == (3, 3)
+    q, d = geo.kwikqdrdist_matrix(np.asmatrix(a), np.asmatrix(a), np.asmatrix(a), np.asmatrix(a), ctx=ctx)
+    assert isinstance(q, np.matrix)
+    # a length-1 1-D operand broadcasts (numpy semantics), made explicit for the C ABI
+    geo.qdrdist_matrix(a[:1], a[:1], b, b, ctx=ctx)
+    assert ctx.calls[-1] == (4, 4, False, True)
+    with pytest.raises(ValueError):
+        geo.qdrdist_matrix(a, a, b, b, ctx=ctx)          # 3 vs 4 do not broadcast
+    with pytest.raises(ValueError):
+        geo.qdrdist_matrix(np.asmatrix(a), a, a, a, ctx=ctx)
+    with pytest.raises(ValueError):
+        geo.qdrdist_matrix(np.ones((2, 3)), np.ones((2, 3)), np.ones((2, 3)), np.ones((2, 3)), ctx=ctx)
