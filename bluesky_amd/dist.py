@@ -72,12 +72,13 @@ def cleanup_rendezvous(rank):
 def init_comm(ctx, rank, world):
     """Create the RCCL communicator of this rank's context (collective)."""
     from . import _lib
-    if world == 1:
-        return
+    if world == 1 or getattr(ctx, 'comm_rank_world', None) == (rank, world):
+        return                        # one communicator per context, reused by later sims
     uid = rendezvous_unique_id(rank, world, _lib.comm_unique_id)
     ctx.comm_init(world, rank, uid)
     ctx.allreduce_max([0.0])          # everyone has joined
     cleanup_rendezvous(rank)
+    ctx.comm_rank_world = (rank, world)
 
 
 def merge_rank_pairs(parts):
