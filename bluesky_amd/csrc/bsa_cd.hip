@@ -258,13 +258,25 @@ struct ReuseParams {
 };
 constexpr double kRefineChord = 0.03;  // the refine keeps (without refining) pairs with a longer chord
 
+__device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__restrict__ P, TileBox *gb,
+                                           TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
+                                           TileBox *__restrict__ tbox);
+
+// K0c fused into K0b (no candidate-list reuse): the workgroup's kTile records
+// are one tile, so the boxes are reduced right after the records are written.
+struct FusedBoxes {
+  TileBox *sbox, *gbox, *tbox;  // gbox == nullptr: not fused (k_boxes runs)
+};
+
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
-__global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__restrict__ perm,
-                                                   SoA6 own, SoA6 intr, int distinct, int shared,
-                                                   double rpz, double hpz, double tla,
-                                                   ColRec *__restrict__ C, PFRec *__restrict__ PC,
-                                                   PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
-                                                   ReuseParams rz) {
+// Workgroup = kTile lanes (one tile of sorted records).
+__global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__restrict__ perm,
+                                                     SoA6 own, SoA6 intr, int distinct, int shared,
+                                                     double rpz, double hpz, double tla,
+                                                     ColRec *__restrict__ C, PFRec *__restrict__ PC,
+                                                     PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
+                                                     ReuseParams rz, FusedBoxes fb) {
+  __shared__ TileBox fgb[kTile / 64];
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
@@ -363,6 +375,8 @@ __global__ __launch_bounds__(256) void k_prep_cols(int cnt, const unsigned *__re
       rz.use[2 * wv + 1] = use_v;
     }
   }
+  // K0c (fused): this thread wrote PC[k] above, every thread reaches the barrier
+  if (fb.gbox) tile_boxes(cnt, blockIdx.x, PC, fgb, fb.sbox, fb.gbox, fb.tbox);
 }
 
 // ------------------------------------------------------------------ K0c tile boxes
@@ -407,24 +421,18 @@ __device__ __forceinline__ bool list_word(int k) {
   return k == kCand || k == kTiles || k == kGroups || k >= kStamp;
 }
 
-// one workgroup per tile, one wave per group (lane = record): 16-record
-// sub-group boxes to sbox (nullable), group boxes to gbox, their union to tbox
 __device__ __forceinline__ float xmin(float v, int o) { return fminf(v, __shfl_xor(v, o)); }
 __device__ __forceinline__ float xmax(float v, int o) { return fmaxf(v, __shfl_xor(v, o)); }
 
-__global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restrict__ P,
-                                                 TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
-                                                 TileBox *__restrict__ tbox, const unsigned *__restrict__ build,
-                                                 Counters *__restrict__ reset) {
-  __shared__ TileBox gb[kGroupsPerTile];
-  if (build && !build[0]) return;  // reused candidate list: no sweep this detect
-  if (reset && blockIdx.x == 0) {  // reuse build: start from an empty candidate list
-    constexpr int kWords = (int)(sizeof(Counters) / 8);
-    for (int k = threadIdx.x; k < kWords; k += blockDim.x)
-      if (list_word(k)) reinterpret_cast<unsigned long long *>(reset)[k] = 0;
-  }
+// Boxes of one kTile-record tile (workgroup = kTile lanes, one wave per
+// kGroup-record group, lane = record): kSub-record sub-group boxes to sbox
+// (nullable), group boxes to gbox, their union to tbox[tile].  Shared by
+// k_boxes and the fused K0b+K0c path of k_prep_cols.
+__device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__restrict__ P, TileBox *gb,
+                                           TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
+                                           TileBox *__restrict__ tbox) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int g = blockIdx.x * kGroupsPerTile + w;
+  const int g = tile * kGroupsPerTile + w;
   const int k = g * kGroup + lane;
   const int ngroups = (cnt + kGroup - 1) / kGroup;
   float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -487,8 +495,22 @@ __global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restric
   if (threadIdx.x == 0) {
     TileBox u = gb[0];
     for (int q = 1; q < kGroupsPerTile; ++q) u = box_union(u, gb[q]);
-    tbox[blockIdx.x] = u;
+    tbox[tile] = u;
   }
+}
+
+__global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restrict__ P,
+                                                 TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
+                                                 TileBox *__restrict__ tbox, const unsigned *__restrict__ build,
+                                                 Counters *__restrict__ reset) {
+  __shared__ TileBox gb[kGroupsPerTile];
+  if (build && !build[0]) return;  // reused candidate list: no sweep this detect
+  if (reset && blockIdx.x == 0) {  // reuse build: start from an empty candidate list
+    constexpr int kWords = (int)(sizeof(Counters) / 8);
+    for (int k = threadIdx.x; k < kWords; k += blockDim.x)
+      if (list_word(k)) reinterpret_cast<unsigned long long *>(reset)[k] = 0;
+  }
+  tile_boxes(cnt, blockIdx.x, P, gb, sbox, gbox, tbox);
 }
 
 // ------------------------------------------------------------------ K0d tile pairs
@@ -1510,12 +1532,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (PFVel *)c->pfvrow.p, (float4 *)c->pfprow.p, mid);
     BSA_HIP(c, hipGetLastError());
   }
-  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, (int)n, perm_c, own,
-                     intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
-                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz);
-  BSA_HIP(c, hipGetLastError());
-
-  // ---- K0c/K0d group / tile boxes and the tile-pair work list
+  // K0c for the columns is fused into K0b unless the candidate list is reused
+  // (then the boxes wait for the build decision every K0b lane contributes to)
   const int nrt = (int)((nrows + kTile - 1) / kTile), nct = (int)((n + kTile - 1) / kTile);
   const long long ntp = (long long)nrt * nct;
   const int ngr = (int)((nrows + kGroup - 1) / kGroup), ngc = (int)((n + kGroup - 1) / kGroup);
@@ -1525,6 +1543,14 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
       !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
     return -1;
+  FusedBoxes fb{nullptr, nullptr, nullptr};
+  if (!reuse) fb = FusedBoxes{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p};
+  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, kTile)), dim3(kTile), 0, c->stream, (int)n, perm_c, own,
+                     intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
+                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb);
+  BSA_HIP(c, hipGetLastError());
+
+  // ---- K0c/K0d group / tile boxes (rows; columns when reused) and the tile-pair work list
   if (!shared && (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
                   !ensure(c, c->gbox_r, ngr * sizeof(TileBox), "row group boxes")))
     return -1;
@@ -1533,9 +1559,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (!shared)
     hipLaunchKernelGGL(k_boxes, dim3(nrt), dim3(kTile), 0, c->stream, (int)nrows, pfrow, (TileBox *)nullptr,
                        (TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p, build, (Counters *)nullptr);
-  hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
-                     (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build,
-                     reuse ? dcnt : (Counters *)nullptr);
+  if (reuse)
+    hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
+                       (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + kTPThreads - 1) / kTPThreads)), dim3(kTPThreads), 0,
                      c->stream, nrt, nct,
                      tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p, &dcnt->tiles, build);
