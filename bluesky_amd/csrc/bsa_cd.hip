@@ -258,6 +258,35 @@ struct ReuseParams {
 };
 constexpr double kRefineChord = 0.03;  // the refine keeps (without refining) pairs with a longer chord
 
+constexpr int kWorkShards = 8;   // one dequeue counter per XCD group
+constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
+
+// Per-detect state to zero (k_zero, or fused into k_prep_cols: cnt != nullptr)
+struct ZeroArgs {
+  int nrows, full, keep;
+  Counters *cnt;
+  unsigned long long *work;
+  unsigned char *inconf;
+  unsigned long long *tcpamax;
+  unsigned *rowcnt;
+};
+__device__ __forceinline__ bool list_word(int k);
+__device__ __forceinline__ void zero_state(const ZeroArgs &z, int t, int nt) {
+  constexpr int kWords = (int)(sizeof(Counters) / 8);
+  constexpr int kTilesWord = (int)(offsetof(Counters, tiles) / 8);
+  const int m = max(max(2 * (z.nrows + 1), kWorkShards * kWorkStride), kWords);
+  for (int k = t; k < m; k += nt) {
+    if (k < kWords && (z.full || k != kTilesWord) && !(z.keep && list_word(k)))
+      reinterpret_cast<unsigned long long *>(z.cnt)[k] = 0;
+    if (k < kWorkShards * kWorkStride) z.work[k] = 0;
+    if (k < z.nrows) {
+      z.inconf[k] = 0;
+      z.tcpamax[k] = 0;
+    }
+    if (k < 2 * (z.nrows + 1)) z.rowcnt[k] = 0;
+  }
+}
+
 __device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__restrict__ P, TileBox *gb,
                                            TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
                                            TileBox *__restrict__ tbox);
@@ -275,9 +304,10 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
                                                      double rpz, double hpz, double tla,
                                                      ColRec *__restrict__ C, PFRec *__restrict__ PC,
                                                      PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
-                                                     ReuseParams rz, FusedBoxes fb) {
+                                                     ReuseParams rz, FusedBoxes fb, ZeroArgs zs) {
   __shared__ TileBox fgb[kTile / 64];
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (zs.cnt) zero_state(zs, k, gridDim.x * blockDim.x);  // K0z (fused): nothing here reads that state
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
   if (k < cnt) {
@@ -669,8 +699,6 @@ constexpr int PF_WROWS = 64;   // rows per wave (one per lane)
 constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 constexpr int PF_BLOCKS_PER_CU = 5;  // LDS-limited (~7.8 KB per wave) and BSA_PF_WAVES_PER_EU
 constexpr int kSubsPerTile = kTile / kSub;
-constexpr int kWorkShards = 8;   // one dequeue counter per XCD group
-constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
 static_assert(kSubsPerTile == 64, "one sub-group box per lane");
 constexpr int kSubsPerBatch = 64 / kSub;  // sub-groups per 64-column batch
 static_assert(PF_Q1 >= 64 * 8, "one 8-column chunk of survivors fits the stage-1 queue");
@@ -1289,30 +1317,20 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
 
 // Zero the per-detect state: counters (but `tiles` unless full; with keep,
 // nothing of the candidate list: its counts, tiles and groups), the dequeue
-// shards and the per-row outputs / counts.  Grid-stride, one word per lane.
+// shards and the per-row outputs / counts.  Grid-stride, one word per lane
+// (zero_state, shared with the fused K0z+K0b path of k_prep_cols).
 __global__ __launch_bounds__(256) void k_zero(int nrows, int full, int keep, unsigned *__restrict__ rctl,
                                               int rforce, Counters *__restrict__ cnt,
                                               unsigned long long *__restrict__ work,
                                               unsigned char *__restrict__ inconf,
                                               unsigned long long *__restrict__ tcpamax,
                                               unsigned *__restrict__ rowcnt) {
-  constexpr int kWords = (int)(sizeof(Counters) / 8);
-  constexpr int kTilesWord = (int)(offsetof(Counters, tiles) / 8);
-  const int m = max(max(2 * (nrows + 1), kWorkShards * kWorkStride), kWords);
   if (rctl && blockIdx.x == 0 && threadIdx.x == 0) {  // reuse: build this detect? (force: age 0)
     rctl[0] = rforce ? 1u : 0u;
     if (rforce) rctl[1] = 0u;
   }
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
-    if (k < kWords && (full || k != kTilesWord) && !(keep && list_word(k)))
-      reinterpret_cast<unsigned long long *>(cnt)[k] = 0;
-    if (k < kWorkShards * kWorkStride) work[k] = 0;
-    if (k < nrows) {
-      inconf[k] = 0;
-      tcpamax[k] = 0;
-    }
-    if (k < 2 * (nrows + 1)) rowcnt[k] = 0;
-  }
+  zero_state(ZeroArgs{nrows, full, keep, cnt, work, inconf, tcpamax, rowcnt},
+             blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
 }
 
 // ------------------------------------------------------------------ host side
@@ -1480,7 +1498,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     c->reuse_candp = c->cand.p;
   }
   const unsigned *build = reuse ? (const unsigned *)c->reuse_ctl.p : nullptr;
-  if (zero(reuse, reuse ? (unsigned *)c->reuse_ctl.p : nullptr, rvalid ? 0 : 1)) return -1;
+  // K0z runs inside K0b (k_prep_cols) unless the list is reused (its build flag is set here)
+  if (reuse && zero(true, (unsigned *)c->reuse_ctl.p, rvalid ? 0 : 1)) return -1;
   if (resort) {
     // columns: intruder position, own velocity; rows: own position, intruder velocity
     if (spatial_order(c, (int)n, 0, intr.lat, intr.lon, own.trk, own.gs, kf, c->key_c, c->idx_c, c->key_c2,
@@ -1544,10 +1563,15 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
     return -1;
   FusedBoxes fb{nullptr, nullptr, nullptr};
-  if (!reuse) fb = FusedBoxes{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p};
+  ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (!reuse) {
+    fb = FusedBoxes{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p};
+    zs = ZeroArgs{(int)nrows, 1, 0, dcnt, (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
+                  (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p};
+  }
   hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, kTile)), dim3(kTile), 0, c->stream, (int)n, perm_c, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
-                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb);
+                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs);
   BSA_HIP(c, hipGetLastError());
 
   // ---- K0c/K0d group / tile boxes (rows; columns when reused) and the tile-pair work list
