@@ -27,6 +27,7 @@
 
 #include "bsa_geo_math.h"
 #include "bsa_internal.h"
+#include "bsa_mvp_math.h"
 
 #pragma clang fp contract(off)
 
@@ -1245,6 +1246,14 @@ __global__ __launch_bounds__(256) void k_scatter(const Counters *__restrict__ cn
   }
 }
 
+// MVP's per-pair vectors written by k_rank in the resident step (pdv == NULL: off)
+struct MvpFuse {
+  bsa_mvp_params p;
+  MvpPairIn in;
+  double4 *pdv;
+  uint8_t *pfl;
+};
+
 // One lane per pair slot of the scattered lists (grid-stride over P + L, the
 // device-side counts): the slot's rank among its row segment's columns (the
 // segment is short: ~1.5 pairs per row at the 100k box; any length works)
@@ -1264,7 +1273,7 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
                                               int *__restrict__ li, int *__restrict__ lj,
                                               unsigned long long *__restrict__ stats,
                                               unsigned long long *__restrict__ gate,
-                                              const unsigned *__restrict__ build) {
+                                              const unsigned *__restrict__ build, MvpFuse mf) {
   const bool ovf = cand_overflow(cnt, cap);
   const unsigned P = rowoff[nrows], L = rowoff[2 * nrows + 1] - P;
   const unsigned t0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1306,8 +1315,19 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
       const unsigned v = sslot[xl];
       ci[pos] = (int)(kk >> 32);
       cj[pos] = (int)col;
+      double pay[5];
 #pragma unroll
-      for (int f = 0; f < 5; ++f) out[(size_t)f * P + pos] = cpay[f * cap + v];
+      for (int f = 0; f < 5; ++f) {
+        pay[f] = cpay[f * cap + v];
+        out[(size_t)f * P + pos] = pay[f];
+      }
+      if (mf.pdv) {  // resident step: MVP's per-pair vector (MVP.py:33-56) for k_mvp_row
+        double4 dv;
+        uint8_t fl;
+        mvp_pair(mf.p, mf.in, (int)(kk >> 32), (int)col, pay[0], pay[1], pay[2], pay[3], dv, fl);
+        mf.pdv[pos] = dv;
+        mf.pfl[pos] = fl;
+      }
     } else {
       li[pos] = (int)(kk >> 32);
       lj[pos] = (int)col;
@@ -1379,6 +1399,7 @@ static int next_events(Ctx *c, hipEvent_t **ev) {
 // gate (device, nullable): receives {overflow, P} for the resident sim step.
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
                    unsigned long long *gate) {
+  c->fuse_done = false;  // set again only if K2 below evaluates MVP's per-pair vectors
   const int64_t n = c->n;
   if (re <= 0) re = n;
   if (rb < 0 || rb > re || re > n)
@@ -1638,12 +1659,24 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
                      (unsigned long long *)c->lkey2.p);
   BSA_HIP(c, hipGetLastError());
+  MvpFuse mf{};
+  c->fuse_done = false;
+  if (c->fuse_mvp) {
+    if (!ensure(c, c->mvp_pdv, std::max<unsigned long long>(cap, 1) * sizeof(double4), "mvp pair dv") ||
+        !ensure(c, c->mvp_pfl, std::max<unsigned long long>(cap, 1), "mvp pair flags"))
+      return -1;
+    mf.p = *c->fuse_mvp;
+    mf.in = MvpPairIn{c->fuse_gse, c->fuse_gsn, c->fuse_vs, c->fuse_alt, nullptr};
+    mf.pdv = (double4 *)c->mvp_pdv.p;
+    mf.pfl = (uint8_t *)c->mvp_pfl.p;
+    c->fuse_done = true;
+  }
   hipLaunchKernelGGL(k_rank, dim3(256 * 4), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
                      (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey2.p,
                      (const unsigned *)c->cval2.p, (const double *)c->cpay.p,
                      (const unsigned long long *)c->lkey2.p, (int)rb, (int *)c->out_ci.p, (int *)c->out_cj.p,
                      (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
-                     (unsigned long long *)c->stats.p, gate, build);
+                     (unsigned long long *)c->stats.p, gate, build, mf);
   BSA_HIP(c, hipGetLastError());
   if (mark(4)) return -1;
   c->ev_valid = c->ev_valid || timed;

@@ -225,6 +225,12 @@ struct Ctx {
   DevBuf wfield;
   int64_t wf_nvec = 0;
 
+  // resident step: per-pair MVP vectors evaluated inside K2 (k_rank) when set
+  // (sim_cd sets it around detect_enqueue; full-N device arrays)
+  const bsa_mvp_params *fuse_mvp = nullptr;
+  const double *fuse_gse = nullptr, *fuse_gsn = nullptr, *fuse_vs = nullptr, *fuse_alt = nullptr;
+  bool fuse_done = false;  // the last detect_enqueue produced the per-pair vectors
+
   // standalone geo matrices (bsa_geo.hip)
   DevBuf geo_in, geo_pts, geo_out;
   hipEvent_t geo_ev[2] = {nullptr, nullptr};
@@ -253,7 +259,7 @@ struct MvpDev {
 };
 int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned *seg,
                const unsigned long long *gate, unsigned *sticky, const uint8_t *inconf, uint8_t *active,
-               bool resolve);
+               bool resolve, bool pairs_done = false);
 
 // device pointers for the fused kinematics kernel
 struct KinDev {

@@ -11,6 +11,7 @@
 // and runs the per-aircraft finalize (MVP.py:67-143).
 #include "bsa_geo_math.h"  // np_max / np_min / np_rem
 #include "bsa_internal.h"
+#include "bsa_mvp_math.h"
 
 #pragma clang fp contract(off)
 
@@ -73,66 +74,13 @@ __global__ __launch_bounds__(256) void k_mvp_pair(int rb, bsa_mvp_params p, MvpI
   const unsigned P = in.seg[in.nrows];
   const unsigned stride = gridDim.x * blockDim.x;
   for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < P; k += stride) {
-    const int id1 = in.ci[k], id2 = in.cj[k];
-    const double gse1 = in.gseast[id1], gsn1 = in.gsnorth[id1], vs1 = in.vs[id1], alt1 = in.alt[id1];
-    const double dist = in.pay[(size_t)1 * P + k], tcpa = in.pay[(size_t)2 * P + k];
-    const double tLOS = in.pay[(size_t)3 * P + k];
-    // ---- MVP.MVP (MVP.py:149-231)
-    const double qdr = in.pay[k] * kD2R;
-    const double drel0 = sin(qdr) * dist;
-    const double drel1 = cos(qdr) * dist;
-    const double drel2 = in.alt[id2] - alt1;
-    const double vrel0 = in.gseast[id2] - gse1;
-    const double vrel1 = in.gsnorth[id2] - gsn1;
-    const double vrel2 = in.vs[id2] - vs1;
-    double dcpa0 = drel0 + vrel0 * tcpa;
-    double dcpa1 = drel1 + vrel1 * tcpa;
-    double dabsH = sqrt(dcpa0 * dcpa0 + dcpa1 * dcpa1);
-    const double iH = p.Rm - dabsH;
-    if (dabsH <= 10.) {
-      dabsH = 10.;
-      dcpa0 = drel1 / dist * dabsH;
-      dcpa1 = -drel0 / dist * dabsH;
-    }
-    double dv1 = (iH * dcpa0) / (fabs(tcpa) * dabsH);
-    double dv2 = (iH * dcpa1) / (fabs(tcpa) * dabsH);
-    if (p.Rm < dist && dabsH < dist) {
-      const double erratum = cos(asin(p.Rm / dist) - asin(dabsH / dist));
-      dv1 = dv1 / erratum;
-      dv2 = dv2 / erratum;
-    }
-    const bool vz = fabs(vrel2) > 0.0;
-    double iV = vz ? p.dhm : p.dhm - fabs(drel2);
-    double tsolV = vz ? fabs(drel2 / vrel2) : tLOS;
-    if (tsolV > p.dtlookahead) {
-      tsolV = tLOS;
-      iV = p.dhm;
-    }
-    double dv3 = vz ? (iV / tsolV) * (-vrel2 / fabs(vrel2)) : (iV / tsolV);
-    // ---- accumulation rule (MVP.py:44-56): subtract? (then) add back?
-    bool sub = true;
-    if (p.swprio) {
-      const double vs2 = in.vs[id2];
-      const bool c1 = fabs(vs1) < 0.1 && fabs(vs2) > 0.1;  // ac1 cruising, ac2 climbing
-      const bool c2 = fabs(vs2) < 0.1 && fabs(vs1) > 0.1;  // ac2 cruising, ac1 climbing
-      switch (p.priocode) {
-        case BSA_PRIO_FF1: dv3 = dv3 / 2.0; break;
-        case BSA_PRIO_FF2: dv3 = dv3 / 2.0; sub = !c1; break;
-        case BSA_PRIO_FF3:
-          if (c1) dv3 = 0.0;
-          else if (c2) { dv3 = 0.0; sub = false; }
-          else dv3 = dv3 / 2.0;
-          break;
-        case BSA_PRIO_LAY1: dv3 = 0.0; sub = !c1; break;
-        case BSA_PRIO_LAY2: dv3 = 0.0; sub = !c2; break;
-        default: sub = false; break;  // unknown code: prioRules changes nothing
-      }
-    } else {
-      dv3 = 0.5 * dv3;
-    }
-    const bool add = p.swnoreso && in.noreso && in.noreso[id2];
-    in.pdv[k] = make_double4(dv1, dv2, dv3, tsolV);
-    in.pfl[k] = (uint8_t)((sub ? 1 : 0) | (add ? 2 : 0));
+    double4 dv;
+    uint8_t fl;
+    mvp_pair(p, MvpPairIn{in.gseast, in.gsnorth, in.vs, in.alt, p.swnoreso ? in.noreso : nullptr}, in.ci[k],
+             in.cj[k], in.pay[k], in.pay[(size_t)1 * P + k], in.pay[(size_t)2 * P + k],
+             in.pay[(size_t)3 * P + k], dv, fl);
+    in.pdv[k] = dv;
+    in.pfl[k] = fl;
   }
 }
 
@@ -228,7 +176,7 @@ __global__ __launch_bounds__(256) void k_mvp_row(int rb, bsa_mvp_params p, MvpIn
 // gate / sticky / inconf / active: resident sim step only.
 int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned *seg,
                const unsigned long long *gate, unsigned *sticky, const uint8_t *inconf, uint8_t *active,
-               bool resolve) {
+               bool resolve, bool pairs_done) {
   const int64_t rb = c->last_rb, re = c->last_re, nrows = re - rb;
   if (nrows <= 0) return 0;
   const unsigned long long pcap = std::max<unsigned long long>(c->cand_cap, (unsigned long long)c->last_conf);
@@ -272,8 +220,10 @@ int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned 
   in.active = active;
   in.nrows = (int)nrows;
   in.resolve = resolve ? 1 : 0;
-  hipLaunchKernelGGL(k_mvp_pair, dim3(256 * 4), dim3(256), 0, c->stream, (int)rb, p, in);
-  BSA_HIP(c, hipGetLastError());
+  if (!pairs_done) {  // else K2 of the same step already wrote pdv / pfl (k_rank)
+    hipLaunchKernelGGL(k_mvp_pair, dim3(256 * 4), dim3(256), 0, c->stream, (int)rb, p, in);
+    BSA_HIP(c, hipGetLastError());
+  }
   hipLaunchKernelGGL(k_mvp_row, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, c->stream, (int)rb, p,
                      in);
   BSA_HIP(c, hipGetLastError());

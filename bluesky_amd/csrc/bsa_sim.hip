@@ -240,7 +240,18 @@ static int sim_cd(Ctx *c) {
   const bsa_sim_params &p = c->simp;
   if (sim_gather(c)) return -1;
   unsigned long long *gate = (unsigned long long *)c->sim_ctl.p;
-  if (detect_enqueue(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, gate)) return -1;
+  // MVP's per-pair vectors are evaluated by K2 as it places each pair (no
+  // NORESO list in the resident step); k_mvp_row folds them after the gate
+  if (p.reso) {
+    c->fuse_mvp = &p.mvp;
+    c->fuse_gse = (const double *)c->s_gse.p;
+    c->fuse_gsn = (const double *)c->s_gsn.p;
+    c->fuse_vs = (const double *)c->own[5].p;
+    c->fuse_alt = (const double *)c->own[4].p;
+  }
+  const int de = detect_enqueue(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, gate);
+  c->fuse_mvp = nullptr;
+  if (de) return -1;
   c->sim_cd_calls++;
   unsigned *sticky = (unsigned *)((char *)c->sim_ctl.p + 16);
   BkDev bk;
@@ -278,7 +289,8 @@ static int sim_cd(Ctx *c) {
   d.o_tsolv = nullptr;
   // K3 (+ gate, + asas.active = inconf unless ResumeNav runs) on the detect's own row offsets
   if (mvp_device(c, p.mvp, d, (const unsigned *)c->rowoff.p, gate, sticky,
-                 p.resume_nav ? nullptr : (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p, p.reso != 0))
+                 p.resume_nav ? nullptr : (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p, p.reso != 0,
+                 c->fuse_done))
     return -1;
   // second half: resopairs rewrite, ResumeNav's asas.active, unique / cumulative counts
   return p.resume_nav ? bk_apply(c, bk) : 0;
