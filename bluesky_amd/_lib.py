@@ -139,6 +139,7 @@ SIGNATURES.update({
     'bsa_sim_init': (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.POINTER(SimState),
                                     ctypes.POINTER(SimParams)]),
     'bsa_sim_step': (ctypes.c_int, [_vp, ctypes.c_int]),
+    'bsa_sim_update': (ctypes.c_int, [_vp, ctypes.POINTER(SimState)]),
     'bsa_sim_read': (ctypes.c_int, [_vp, ctypes.POINTER(SimOut)]),
     'bsa_sim_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_asas_stats': (ctypes.c_int, [_vp, _c_i64p]),
@@ -214,6 +215,10 @@ class Context:
                                    % (device, self.lib.bsa_last_error(None).decode()))
         self.h = h
         self.device = device
+        # bumped by every call that replaces the device-resident state or pairs
+        # (set_state / set_intruder / detect / set_pairs / sim_*): the MVP drop-in
+        # reuses a detect's device pairs only while it is unchanged
+        self.gen = 0
 
     def close(self):
         if getattr(self, 'h', None):
@@ -232,6 +237,7 @@ class Context:
 
     # ---------------------------------------------------------------- state
     def set_state(self, lat, lon, trk, gs, alt, vs):
+        self.gen += 1
         arrs = [f64(x) for x in (lat, lon, trk, gs, alt, vs)]
         n = len(arrs[0])
         if any(len(a) != n for a in arrs):
@@ -240,6 +246,7 @@ class Context:
         self.n = n
 
     def set_intruder(self, lat=None, lon=None, trk=None, gs=None, alt=None, vs=None):
+        self.gen += 1
         if lat is None:
             self.check(self.lib.bsa_set_intruder(self.h, 0, *([None] * 6)), 'bsa_set_intruder')
             return
@@ -249,6 +256,7 @@ class Context:
 
     # ---------------------------------------------------------------- detect
     def detect(self, rpz, hpz, tla, flags=0, row_begin=0, row_end=-1):
+        self.gen += 1
         nc = ctypes.c_int64()
         nl = ctypes.c_int64()
         self.check(self.lib.bsa_detect(self.h, float(rpz), float(hpz), float(tla), int(flags),
@@ -395,6 +403,7 @@ class Context:
     # ---------------------------------------------------------------- MVP
     def set_pairs(self, ci, cj, qdr, dist, tcpa, tlos):
         """bsa_set_pairs: external confpairs (row-major) for bsa_mvp."""
+        self.gen += 1
         ci = np.ascontiguousarray(ci, dtype=np.int32)
         cj = np.ascontiguousarray(cj, dtype=np.int32)
         arrs = [f64(x) for x in (qdr, dist, tcpa, tlos)]
@@ -437,6 +446,7 @@ class Context:
 
     # ---------------------------------------------------------------- resident sim
     def sim_init(self, state, params):
+        self.gen += 1
         n = len(state['lat'])
         keep = {k: f64(state[k]) for k in SIM_STATE_FIELDS}
         for k, a in keep.items():
@@ -447,7 +457,21 @@ class Context:
                    'bsa_sim_init')
         self.n = n
 
+    def sim_update(self, **arrays):
+        """bsa_sim_update: overwrite the given full-n state arrays (SIM_STATE_FIELDS
+        names) of the resident sim, keeping its ASAS bookkeeping."""
+        bad = set(arrays) - set(SIM_STATE_FIELDS)
+        if bad:
+            raise ValueError('unknown sim state fields %s' % sorted(bad))
+        keep = {k: f64(v) for k, v in arrays.items() if v is not None}
+        for k, a in keep.items():
+            if len(a) != self.n:
+                raise ValueError('sim state %s has length %d != %d' % (k, len(a), self.n))
+        st = SimState(**{k: ptr(a) for k, a in keep.items()})
+        self.check(self.lib.bsa_sim_update(self.h, ctypes.byref(st)), 'bsa_sim_update')
+
     def sim_step(self, nsteps=1):
+        self.gen += 1
         self.check(self.lib.bsa_sim_step(self.h, int(nsteps)), 'bsa_sim_step')
 
     def sim_read(self):

@@ -252,6 +252,7 @@ struct Ctx {
 // device pointers for the MVP kernel (full-N traffic arrays, per-row outputs)
 struct MvpDev {
   const double *gseast, *gsnorth, *vs, *alt, *trk, *gs, *selalt, *apvs;
+  const double *aptrk, *aptas, *apalt;  // resident step, CR OFF (DoNothing.py) only; else NULL
   const uint8_t *noreso, *resooff;
   double *asas_alt, *o_trk, *o_tas, *o_vs;
   float *o_asase, *o_asasn;

@@ -44,6 +44,7 @@ struct MvpIn {
   const unsigned *seg;               // row segments, nrows + 1 entries; seg[nrows] = P
   const double *gseast, *gsnorth, *vs, *alt, *trk, *gs;  // full-N traffic arrays
   const double *selalt, *apvs;                           // full-N
+  const double *aptrk, *aptas, *apalt;                   // full-N, resident CR OFF only (else NULL)
   const uint8_t *noreso, *resooff;                       // full-N flags or NULL
   double *asas_alt;                                      // rows [rb, re), in/out
   double *o_trk, *o_tas, *o_vs;                          // rows [rb, re)
@@ -58,7 +59,7 @@ struct MvpIn {
   const uint8_t *inconf;
   uint8_t *active;
   int nrows;
-  int resolve;                                           // 0: only the active copy
+  int resolve;                                           // 0: CR OFF (DoNothing.py), resident step only
 };
 
 __device__ __forceinline__ bool mvp_aborted(const MvpIn &in) {
@@ -86,17 +87,26 @@ __global__ __launch_bounds__(256) void k_mvp_pair(int rb, bsa_mvp_params p, MvpI
 
 // Per row: the dv fold over the row's pairs in confpair order (MVP.py:44-61),
 // then the per-aircraft finalize (MVP.py:67-143).  In the resident sim step
-// this kernel also gates the step (overflow -> sticky abort) and copies
-// asas.active = inconf.
+// this kernel also gates the step (overflow -> sticky abort), copies
+// asas.active = inconf (the stand-in for ResumeNav without resume_nav) and,
+// with CR OFF, runs DoNothing.resolve instead of MVP.
 __global__ __launch_bounds__(256) void k_mvp_row(int rb, bsa_mvp_params p, MvpIn in) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (in.gate) {
     const bool abort = in.sticky[0] != 0 || in.gate[0] != 0;
     if (r == 0 && in.gate[0] != 0) in.sticky[0] = 1u;
-    if (abort || r >= in.nrows || !in.resolve) return;  // RESO off: asas stays inactive
+    if (abort || r >= in.nrows) return;
     if (in.inconf) in.active[rb + r] = in.inconf[r];  // stand-in for ResumeNav unless resume_nav
     // asas.py:486-487: resolve only if confpairs is non-empty (over all ranks)
     if (in.gate[1] == 0) return;
+    if (!in.resolve) {  // CR "OFF" = DoNothing.resolve (DoNothing.py:11-20, asas.py:41,76-77):
+      const int id1 = rb + r;  // the ASAS targets become the autopilot's
+      in.o_trk[r] = in.aptrk[id1];
+      in.o_tas[r] = in.aptas[id1];
+      in.o_vs[r] = in.apvs[id1];
+      in.asas_alt[r] = in.apalt[id1];
+      return;
+    }
   } else if (r >= in.nrows) {
     return;
   }
@@ -203,6 +213,9 @@ int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned 
   in.gs = d.gs;
   in.selalt = d.selalt;
   in.apvs = d.apvs;
+  in.aptrk = d.aptrk;
+  in.aptas = d.aptas;
+  in.apalt = d.apalt;
   in.noreso = d.noreso;
   in.resooff = d.resooff;
   in.asas_alt = d.asas_alt;
@@ -220,7 +233,9 @@ int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned 
   in.active = active;
   in.nrows = (int)nrows;
   in.resolve = resolve ? 1 : 0;
-  if (!pairs_done) {  // else K2 of the same step already wrote pdv / pfl (k_rank)
+  if (!resolve && (!gate || !d.aptrk || !d.aptas || !d.apalt))
+    return fail(c, "CR OFF (DoNothing) needs the resident step's autopilot targets");
+  if (!pairs_done && resolve) {  // else K2 of the same step already wrote pdv / pfl (k_rank)
     hipLaunchKernelGGL(k_mvp_pair, dim3(256 * 4), dim3(256), 0, c->stream, (int)rb, p, in);
     BSA_HIP(c, hipGetLastError());
   }
@@ -277,6 +292,7 @@ extern "C" int bsa_mvp(bsa_ctx *cc, const bsa_mvp_params *p, const double *gseas
   d.gs = (const double *)c->own[3].p;
   d.selalt = d_sel;
   d.apvs = d_apvs;
+  d.aptrk = d.aptas = d.apalt = nullptr;
   d.noreso = noreso ? d_nr : nullptr;
   d.resooff = resooff ? d_ro : nullptr;
   d.asas_alt = d_alt;

@@ -278,6 +278,9 @@ static int sim_cd(Ctx *c) {
   d.gs = (const double *)c->own[3].p;
   d.selalt = (const double *)c->s_selalt.p;
   d.apvs = (const double *)c->s_apvs.p;
+  d.aptrk = (const double *)c->s_aptrk.p;
+  d.aptas = (const double *)c->s_aptas.p;
+  d.apalt = (const double *)c->s_apalt.p;
   d.noreso = nullptr;
   d.resooff = nullptr;
   d.asas_alt = (double *)c->s_aalt.p + rb;
@@ -347,8 +350,13 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   Ctx *c = (Ctx *)cc;
   if (!c) return -1;
   if (!s || !p) return bsa::fail(c, "NULL sim state / params");
+  // every parameter is checked before anything is uploaded; a failed init
+  // leaves no half-initialised sim behind (sim_ready stays false)
+  c->sim_ready = false;
   if (n <= 0 || n > 0x7fffffff) return bsa::fail(c, "bad n");
   if (p->cd_every < 1) return bsa::fail(c, "cd_every must be >= 1");
+  if (p->resume_nav != 0 && p->resume_nav != 1) return bsa::fail(c, "resume_nav must be 0 or 1");
+  if (p->winddim < 0 || p->winddim > 2) return bsa::fail(c, "winddim must be 0, 1 or 2");
   BSA_HIP(c, hipSetDevice(c->device));
   const double *src[] = {s->lat, s->lon, s->alt, s->tas, s->hdg, s->vs, s->gs, s->trk, s->gseast,
                          s->gsnorth, s->ap_trk, s->ap_tas, s->ap_alt, s->ap_vs, s->selalt, s->bank,
@@ -384,8 +392,6 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   if (!bsa::ensure(c, c->sim_ctl, 64, "sim control words")) return -1;
   BSA_HIP(c, hipMemsetAsync(c->sim_ctl.p, 0, 64, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
-  if (p->resume_nav != 0 && p->resume_nav != 1) return bsa::fail(c, "resume_nav must be 0 or 1");
-  if (p->winddim < 0 || p->winddim > 2) return bsa::fail(c, "winddim must be 0, 1 or 2");
   c->simp = *p;
   c->bk_ready = false;  // empty resopairs / previous pair sets
   c->sim_rpr = (n + c->nranks - 1) / c->nranks;
@@ -475,6 +481,38 @@ int bsa_sim_set_limits(bsa_ctx *cc, const double *hmax, const double *vmin, cons
     BSA_HIP(c, hipMemcpyAsync((char *)c->s_env.p + k * N8, src[k], N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   c->sim_limits = true;
+  return 0;
+}
+
+int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!s) return bsa::fail(c, "NULL sim state");
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_update before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  const size_t N8 = (size_t)c->n * 8;
+  struct {
+    const double *src;
+    void *dst;
+  } cp[] = {{s->lat, c->own[0].p},     {s->lon, c->own[1].p},     {s->trk, c->own[2].p},
+            {s->gs, c->own[3].p},      {s->alt, c->own[4].p},     {s->vs, c->own[5].p},
+            {s->tas, c->s_tas.p},      {s->hdg, c->s_hdg.p},      {s->gseast, c->s_gse.p},
+            {s->gsnorth, c->s_gsn.p},  {s->ap_trk, c->s_aptrk.p}, {s->ap_tas, c->s_aptas.p},
+            {s->ap_alt, c->s_apalt.p}, {s->ap_vs, c->s_apvs.p},   {s->selalt, c->s_selalt.p},
+            {s->bank, c->s_bank.p},    {s->eps, c->s_eps.p},      {s->accel, c->s_accel.p},
+            {s->asas_alt, c->s_aalt.p}};
+  // the replicated CD inputs are rewritten on every rank
+  bool any_cd = false;
+  for (int k = 0; k < 19; ++k) {
+    if (!cp[k].src) continue;
+    if (k < 10) any_cd = true;
+    BSA_HIP(c, hipMemcpyAsync(cp[k].dst, cp[k].src, N8, hipMemcpyHostToDevice, c->stream));
+  }
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  if (any_cd) {
+    c->sim_gathered = true;     // every rank passed the same full arrays
+    c->reuse_valid = false;     // a state jump rebuilds any reused candidate list
+  }
   return 0;
 }
 

@@ -49,8 +49,10 @@ def resolve(asas, traf, ctx=None):
     ctx = ctx or _lib.default_context()
     n = traf.ntraf
     last = statebased.last_detect()
+    # the device still holds that detect's pairs only if nothing replaced them since
+    # (another detect, set_pairs or set_state on the same context bumps ctx.gen)
     reuse = (last is not None and last['confpairs'] is asas.confpairs and last['ctx'] is ctx
-             and last['n'] == n)
+             and last['n'] == n and last['gen'] == ctx.gen)
     if not reuse:
         ctx.set_state(traf.lat, traf.lon, traf.trk, traf.gs, traf.alt, traf.vs)
         idx = {k: i for i, k in enumerate(traf.id)}   # MVP.py:34-35 traf.id.index

@@ -84,6 +84,11 @@ class ResidentSim:
     def step(self, nsteps=1):
         self.ctx.sim_step(nsteps)
 
+    def update(self, **arrays):
+        """Overwrite state arrays (host simulator changed the traffic between
+        steps) keeping the ASAS bookkeeping (bsa_sim_update)."""
+        self.ctx.sim_update(**arrays)
+
     def read(self):
         return self.ctx.sim_read()
 

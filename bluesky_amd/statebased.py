@@ -58,7 +58,8 @@ _last = {}
 
 
 def last_detect():
-    """The last drop-in detect's confpairs list, context and n (for MVP reuse)."""
+    """The last drop-in detect's confpairs list, context, n and the context's
+    generation right after it (for MVP reuse)."""
     return _last or None
 
 
@@ -72,7 +73,7 @@ def detect(ownship, intruder, RPZ, HPZ, tlookahead, with_dcpa=False, kwik=False)
     lospairs = pairs_from_indices(ids, o['li'], o['lj'])
     _last.clear()
     if intruder is ownship:
-        _last.update(confpairs=confpairs, ctx=ctx, n=len(ids))
+        _last.update(confpairs=confpairs, ctx=ctx, n=len(ids), gen=ctx.gen)
     inconf = o['inconf'].astype(bool)
     if with_dcpa:
         return (confpairs, lospairs, inconf, o['tcpamax'], o['qdr'], o['dist'], o['dcpa'],

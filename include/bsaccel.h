@@ -294,7 +294,10 @@ int bsa_comm_allreduce_sum(bsa_ctx *ctx, double *values, int count);
 typedef struct bsa_sim_params {
   double simdt, rpz, hpz, tla;
   int32_t cd_every; /* >= 1: CD + MVP every k steps (1 = DTNOLOOK=simdt, 20 = asas_dt/simdt) */
-  int32_t reso;     /* 1: MVP resolution + asas.active = inconf; 0: CD only (RESO OFF) */
+  int32_t reso;     /* 1: RESO MVP (MVP.py:14-143); 0: RESO OFF, the reference's default CR
+                       (asas.py:41,76-77): DoNothing.resolve (DoNothing.py:11-20) copies the
+                       autopilot targets into asas.trk/tas/vs/alt when there are confpairs.
+                       Either way asas.active = inconf, or ResumeNav's with resume_nav = 1 */
   bsa_mvp_params mvp;
   int32_t winddim;  /* 0 = no wind, 1 = constant wind (windfield.py:150-152), 2 = 2-D field
                        (bsa_set_windfield): the wind branches of Pilot.APorASAS
@@ -332,6 +335,14 @@ int bsa_sim_step(bsa_ctx *ctx, int nsteps);
  * hmax == NULL switches the limits off (the default after bsa_sim_init). */
 int bsa_sim_set_limits(bsa_ctx *ctx, const double *hmax, const double *vmin, const double *vmax,
                        const double *vsmin, const double *vsmax, const double *axmax);
+/* Overwrite per-aircraft arrays of the resident sim (full-n host arrays, all
+ * ranks pass the same) while keeping the ASAS bookkeeping (resopairs, the
+ * previous call's pair sets, asas.active / trk / tas / vs) and traf.ax: the
+ * hybrid mode where the host simulator (autopilot, performance model, stack
+ * commands) changes traffic between steps (traffic.py:383-404 runs them
+ * before Traffic.update's kinematics).  NULL pointers leave that array as it
+ * is; asas_alt overwrites the persistent asas.alt. */
+int bsa_sim_update(bsa_ctx *ctx, const bsa_sim_state *s);
 /* Full-n host copies of the state (collective: gathers all ranks' rows).
  * Any pointer may be NULL. */
 int bsa_sim_read(bsa_ctx *ctx, bsa_sim_out *o);

@@ -3,8 +3,9 @@
 TEST INFRASTRUCTURE ONLY (see ``oracle/__init__.py``).
 
 Order of Traffic.update (bluesky/traffic/traffic.py:383-409) restricted to
-the hot path: asas.update (asas.py:473-504: detect, then MVP.resolve only if
-confpairs is non-empty) every ``cd_every`` steps with ``asas.active =
+the hot path: asas.update (asas.py:473-504: detect, then the resolver only
+if confpairs is non-empty -- MVP.resolve, or with ``reso`` off the reference's
+default CR DoNothing.resolve) every ``cd_every`` steps with ``asas.active =
 inconf``; Pilot.APorASAS (pilot.py:28-63) without wind or with a constant
 wind (``p['wind'] = (vnorth, veast)``, windfield.py:150-152) or a 2-D field
 (``p['windfield']``, windfield.py:158-179); UpdateAirSpeed /
@@ -20,27 +21,32 @@ from . import mvp as omvp
 from . import statebased as ocd
 
 
-def sim_step(st, p, do_cd, bk=None):
+def sim_step(st, p, do_cd, bk=None, cd=None):
     """One step on the dict ``st`` (keys of bluesky_amd.resident.initial_state
     plus asas_trk/asas_tas/asas_vs/asas_alt/active).  Returns the new dict.
-    ``bk``: an oracle.asas.Bookkeeping, updated in place on CD steps."""
+    ``bk``: an oracle.asas.Bookkeeping, updated in place on CD steps.
+    ``cd``: detect results (oracle.statebased.detect_arrays layout) to use
+    instead of running the oracle detect -- for sizes where the N^2 oracle
+    detect is out of reach and the pair lists were verified separately."""
     st = {k: np.array(v, copy=True) for k, v in st.items()}
     n = len(st['lat'])
     if do_cd:
         traf = dict(lat=st['lat'], lon=st['lon'], trk=st['trk'], gs=st['gs'], alt=st['alt'],
                     vs=st['vs'])
-        r = ocd.detect_arrays(traf, traf, p['rpz'], p['hpz'], p['tla'])
+        r = cd if cd is not None else ocd.detect_arrays(traf, traf, p['rpz'], p['hpz'], p['tla'])
         st['n_conf'] = len(r['ci'])
-        if p['reso']:
-            if len(r['ci']):
-                o = omvp.resolve_arrays(r['ci'], r['cj'], r['qdr'], r['dist'], r['tcpa'],
-                                        r['tinconf'], st['gseast'], st['gsnorth'], st['vs'],
-                                        st['alt'], st['trk'], st['gs'], st['selalt'], st['ap_vs'],
-                                        st['asas_alt'].copy(), p['mvp'])
-                st['asas_trk'], st['asas_tas'], st['asas_vs'] = o['trk'], o['tas'], o['vs']
-                st['asas_alt'] = o['alt']
-            if bk is None:
-                st['active'] = np.asarray(r['inconf'], dtype=bool)
+        if not p['reso'] and len(r['ci']):     # CR OFF: DoNothing.resolve (DoNothing.py:11-20)
+            st['asas_trk'], st['asas_tas'] = st['ap_trk'].copy(), st['ap_tas'].copy()
+            st['asas_vs'], st['asas_alt'] = st['ap_vs'].copy(), st['ap_alt'].copy()
+        if p['reso'] and len(r['ci']):         # RESO MVP (asas.py:486-487)
+            o = omvp.resolve_arrays(r['ci'], r['cj'], r['qdr'], r['dist'], r['tcpa'],
+                                    r['tinconf'], st['gseast'], st['gsnorth'], st['vs'],
+                                    st['alt'], st['trk'], st['gs'], st['selalt'], st['ap_vs'],
+                                    st['asas_alt'].copy(), p['mvp'])
+            st['asas_trk'], st['asas_tas'], st['asas_vs'] = o['trk'], o['tas'], o['vs']
+            st['asas_alt'] = o['alt']
+        if bk is None:
+            st['active'] = np.asarray(r['inconf'], dtype=bool)
         if bk is not None:
             bk.active = np.asarray(st['active'], dtype=bool).copy()
             bk.update(zip(r['ci'], r['cj']), zip(r['li'], r['lj']), st['lat'], st['lon'],

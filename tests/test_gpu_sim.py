@@ -7,7 +7,7 @@ state arrays within 1e-9 relative, asas.active and conflict counts exact."""
 import numpy as np
 import pytest
 
-from bluesky_amd import resident, synth
+from bluesky_amd import _lib, resident, synth
 from oracle import mvp as omvp
 from oracle import step as ostep
 from tests import util
@@ -19,12 +19,16 @@ SCALES = dict(lat=90.0, lon=180.0, alt=1e4, tas=300.0, hdg=360.0, vs=20.0, gs=30
               asas_alt=1e4)
 
 
+PRIO_NAMES = {v: k for k, v in _lib.PRIO_CODES.items()}
+
+
 def oracle_params(p, reso=True):
     return dict(simdt=p.simdt, rpz=p.rpz, hpz=p.hpz, tla=p.tla, reso=reso,
                 wind=(p.windnorth, p.windeast) if p.winddim else None,
                 mvp=omvp.params_from_settings(p.rpz, p.hpz, p.tla, p.mvp.Rm / p.rpz,
                                               bool(p.mvp.swresohoriz), bool(p.mvp.swresospd),
-                                              bool(p.mvp.swresohdg), bool(p.mvp.swresovert)))
+                                              bool(p.mvp.swresohdg), bool(p.mvp.swresovert),
+                                              bool(p.mvp.swprio), PRIO_NAMES.get(p.mvp.priocode, 'FF1')))
 
 
 def full_state(init, read):
@@ -65,15 +69,50 @@ def test_resident_steps_match_oracle(ctx, cd_every, steps, hv, wind):
     assert sim.stats()['cd_calls'] == (steps + cd_every - 1) // cd_every
 
 
+@pytest.mark.parametrize('prio', ['FF1', 'FF2', 'FF3', 'LAY1', 'LAY2'])
+def test_resident_priority_rules_match_oracle(ctx, prio):
+    """swprio with each priority code (MVP.py:235-300) on the fused path, where
+    K2 evaluates MVP's per-pair vectors (k_rank, bsa_mvp_math.h) as it places
+    each conflict pair; horizontal + vertical resolution so the vertical rules act."""
+    t = synth.box(1500, 60.0, seed=53)
+    init = resident.initial_state(t)
+    rng = np.random.default_rng(53)
+    init['vs'] = rng.choice([0.0, 0.0, 5.0, -7.0], t.ntraf)   # mix of level / climbing / descending
+    p = resident.params(cd_every=1, swresohoriz=False, swprio=True, priocode=prio)
+    sim = resident.ResidentSim(init, p, ctx=ctx)
+    op = oracle_params(p)
+    assert op['mvp']['swprio'] and op['mvp']['priocode'] == prio
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(t.ntraf), active=np.zeros(t.ntraf, bool))
+    for k in range(3):
+        exp = ostep.sim_step(prev, op, do_cd=True)
+        sim.step(1)
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        prev = got
+
+
 def test_resident_cd_only(ctx):
+    """RESO OFF, the reference's default CR (asas.py:76-77): DoNothing.resolve
+    (DoNothing.py:11-20) sets the ASAS targets to the autopilot's, so active
+    aircraft fly their (frozen) autopilot targets; compared with the oracle."""
     t = synth.box(800, 40.0, seed=29)
     init = resident.initial_state(t)
     p = resident.params(reso=False)
     sim = resident.ResidentSim(init, p, ctx=ctx)
-    sim.step(2)
-    got = sim.read()
-    assert not got['active'].any()
-    # with RESO off every aircraft follows its (frozen) autopilot targets
+    op = oracle_params(p, reso=False)
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(t.ntraf), active=np.zeros(t.ntraf, bool))
+    for k in range(2):
+        exp = ostep.sim_step(prev, op, do_cd=True)
+        sim.step(1)
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        prev = got
+    assert got['active'].any()
+    assert np.array_equal(got['asas_vs'][got['active']], init['ap_vs'][got['active']])
     assert np.allclose(got['hdg'], init['hdg'], rtol=0, atol=1e-9)
 
 
@@ -220,7 +259,8 @@ def test_resident_windfield_matches_oracle(ctx):
 
 def test_resident_openap_limits_match_oracle(ctx):
     """Pilot.applylimits with an OpenAP envelope (pilot.py:65-68, perfoap.py:185-209)
-    between APorASAS and UpdateAirSpeed; the envelope clips most aircraft."""
+    between APorASAS and UpdateAirSpeed; the envelope changes the first step's
+    tas of more than 10 % of the aircraft (checked below)."""
     t = synth.box(1500, 60.0, seed=41)
     init = resident.initial_state(t)
     rng = np.random.default_rng(41)

@@ -60,3 +60,33 @@ def assert_detect_equal(got, exp, rpz, tla, rows=None):
     for k, s in scales.items():
         ok, msg = close(got[k], exp[k], s)
         assert ok, '%s: %s' % (k, msg)
+
+
+TRACE_PAIRS = {'ci': 'ci', 'cj': 'ci', 'qdr': 'ci', 'dist': 'ci', 'tcpa': 'ci', 'tLOS': 'ci',
+               'li': 'li', 'lj': 'li', 'reso_i': 'reso_i', 'reso_j': 'reso_i',
+               'reso_in_i': 'reso_in_i', 'reso_in_j': 'reso_in_i'}
+
+
+def load_trace(path):
+    """Full-simulator trace (tools/make_trace.py): (settings dict, list of per-ASAS-call
+    dicts).  Per call: the traffic state the detector read (lat lon trk gs alt vs tas
+    gseast gsnorth selalt apvs), asas.alt / asas.active before the call, the detect
+    outputs (ci cj li lj inconf tcpamax qdr dist tcpa tLOS), asas.trk/tas/vs/alt and
+    asase/asasn after it, resopairs before / after, asas.active after, the four
+    bookkeeping counts and whether MVP ran."""
+    z = dict(np.load(path, allow_pickle=False))
+    n = int(z['ncalls'])
+    settings = {k[4:]: z[k][()] for k in z if k.startswith('set_')}
+    calls = []
+    for c in range(n):
+        rec = {}
+        for k, v in z.items():
+            if k.startswith('set_') or k == 'ncalls' or k.endswith('_off'):
+                continue
+            if k in TRACE_PAIRS:
+                off = z[TRACE_PAIRS[k] + '_off']
+                rec[k] = v[off[c]:off[c + 1]]
+            else:
+                rec[k] = v[c]
+        calls.append(rec)
+    return settings, calls
