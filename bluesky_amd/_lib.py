@@ -131,7 +131,19 @@ class AcData(ctypes.Structure):
                 [(k, _c_dp) for k in ACDATA_F64] + [('inconf', _c_u8p), ('asasn', _c_fp), ('asase', _c_fp)])
 
 
+class PairsOut(ctypes.Structure):
+    """bsa_pairs_out (include/bsaccel.h)."""
+    _fields_ = [('ci', _c_i32p), ('cj', _c_i32p), ('qdr', _c_dp), ('dist', _c_dp), ('tcpa', _c_dp),
+                ('tinconf', _c_dp), ('dcpa', _c_dp), ('li', _c_i32p), ('lj', _c_i32p), ('inconf', _c_u8p),
+                ('tcpamax', _c_dp)]
+
+
 SIGNATURES.update({
+    'bsa_group_create': (_vp, [ctypes.c_int]),
+    'bsa_group_destroy': (None, [_vp]),
+    'bsa_comm_init_group': (ctypes.c_int, [_vp, _vp, ctypes.c_int]),
+    'bsa_gather_counts': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_gather_pairs': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(PairsOut)]),
     'bsa_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
     'bsa_comm_init': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     'bsa_comm_allreduce_max': (ctypes.c_int, [_vp, _c_dp, ctypes.c_int]),
@@ -191,6 +203,24 @@ def comm_unique_id():
     if lib.bsa_comm_unique_id(buf) != 0:
         raise AccelError('bsa_comm_unique_id failed')
     return buf.raw
+
+
+class Group:
+    """In-process group of contexts (bsa_group_*): the ranks of a row-sharded
+    sim in ONE process, one host thread per rank.  Keep it alive until every
+    member context is closed."""
+
+    def __init__(self, nranks):
+        self.lib = load()
+        self.h = self.lib.bsa_group_create(int(nranks))
+        if not self.h:
+            raise AccelError('bsa_group_create(%d) failed' % nranks)
+        self.nranks = nranks
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.bsa_group_destroy(self.h)
+            self.h = None
 
 
 def ptr(a, ctype=_c_dp):
@@ -434,6 +464,32 @@ class Context:
             raise ValueError('unique id must be %d bytes' % UNIQUE_ID_BYTES)
         self.check(self.lib.bsa_comm_init(self.h, int(nranks), int(rank), uid), 'bsa_comm_init')
 
+    def comm_init_group(self, group, rank):
+        """Join an in-process Group as ``rank`` (call from this rank's thread)."""
+        self.check(self.lib.bsa_comm_init_group(self.h, group.h, int(rank)), 'bsa_comm_init_group')
+        self.comm_rank_world = (rank, group.nranks)
+        self.gen += 1
+
+    def gather_pairs(self, root=0, with_dcpa=False):
+        """C2: every rank's last detect gathered to ``root`` in rank order
+        (collective; bsa_gather_counts + bsa_gather_pairs).  Returns the
+        fetch_pairs-style dict on the root, None elsewhere."""
+        tot = np.zeros(3, np.int64)
+        self.check(self.lib.bsa_gather_counts(self.h, ptr(tot, _c_i64p)), 'bsa_gather_counts')
+        P, L, R = (int(x) for x in tot)
+        rank = getattr(self, 'comm_rank_world', (0, 1))[0]
+        if rank != root:
+            self.check(self.lib.bsa_gather_pairs(self.h, int(root), None), 'bsa_gather_pairs')
+            return None
+        o = dict(ci=np.empty(P, np.int32), cj=np.empty(P, np.int32), qdr=np.empty(P), dist=np.empty(P),
+                 tcpa=np.empty(P), tinconf=np.empty(P), dcpa=np.empty(P) if with_dcpa else None,
+                 li=np.empty(L, np.int32), lj=np.empty(L, np.int32), inconf=np.empty(R, np.uint8),
+                 tcpamax=np.empty(R))
+        po = PairsOut(**{k: ptr(v, _c_i32p if v.dtype == np.int32 else (_c_u8p if v.dtype == np.uint8 else _c_dp))
+                         for k, v in o.items() if v is not None})
+        self.check(self.lib.bsa_gather_pairs(self.h, int(root), ctypes.byref(po)), 'bsa_gather_pairs')
+        return o
+
     def allreduce_max(self, values):
         v = np.array(values, dtype=np.float64, copy=True).ravel()
         self.check(self.lib.bsa_comm_allreduce_max(self.h, ptr(v), len(v)), 'bsa_comm_allreduce_max')
@@ -456,6 +512,8 @@ class Context:
         self.check(self.lib.bsa_sim_init(self.h, n, ctypes.byref(st), ctypes.byref(params)),
                    'bsa_sim_init')
         self.n = n
+        st = self.sim_stats()
+        self._rows = (st['row_begin'], st['row_end'])   # fetch_pairs after steps: this rank's rows
 
     def sim_update(self, **arrays):
         """bsa_sim_update: overwrite the given full-n state arrays (SIM_STATE_FIELDS

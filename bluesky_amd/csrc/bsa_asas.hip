@@ -16,13 +16,19 @@
 //   k_bk_write   same merge + test, write the kept pairs and asas.active
 //                (true iff any of the row's pairs is kept; rows without
 //                resopairs keep their value, as in the reference)
-//   k_bk_unique  (one rank) |confpairs_unique|, |lospairs_unique| and the
-//                growth of confpairs_all / lospairs_all (asas.py:494-502):
-//                pair (i, j) is the representative of {i, j} when i < j or
-//                (j, i) is not a pair; it is new when neither (i, j) nor
-//                (j, i) was a pair of the previous call
+//   k_bk_unique  |confpairs_unique|, |lospairs_unique| and the growth of
+//                confpairs_all / lospairs_all (asas.py:494-502): pair (i, j)
+//                is the representative of {i, j} when i < j or (j, i) is not a
+//                pair; it is new when neither (i, j) nor (j, i) was a pair of
+//                the previous call.  One rank: on the K2 CSR.  Several ranks
+//                (k_bk_unique_g): the sets are global, so every rank packs its
+//                pair keys (k_bk_pack, before the gate: a full key buffer
+//                aborts the step like a resopairs overflow), one all-gather
+//                replicates all ranks' blocks -- concatenated in rank order
+//                they are the global row-major lists -- and every rank counts
+//                the global sets itself (identical counts on all ranks)
 //   k_bk_commit  copy the next CSR and this call's pair lists over the
-//                persistent ones
+//                persistent ones (several ranks: the gathered key blocks)
 // Every kernel is a no-op once the step batch is aborted (sticky flag), so a
 // retried step finds the bookkeeping as it was at the step's start.  The
 // reference iterates a Python set in ResumeNav, so an aircraft whose pairs
@@ -210,6 +216,91 @@ __global__ __launch_bounds__(256) void k_bk_commit(BkCommit m, const unsigned lo
   for (unsigned k = t0; k < L; k += stride) m.plcol[k] = m.lcol[k];
 }
 
+
+// ---- several ranks: global pair-key blocks.  Block of rank q (W words):
+// [0] conflict pairs Pc, [1] LoS pairs Pl, then Pc conflict keys and Pl LoS
+// keys, key = i << 32 | j, ascending (rows of rank q, row-major).
+__global__ __launch_bounds__(256) void k_bk_pack(int nrows, const unsigned *rowoff, const int *ci, const int *cj,
+                                                 const int *li, const int *lj, unsigned long long W,
+                                                 unsigned long long *blk, unsigned long long *gate,
+                                                 const unsigned *sticky, unsigned long long *demand) {
+  if (bk_aborted(gate, sticky)) return;
+  // (a rank without rows has no K2 offsets: no pairs)
+  const unsigned long long Pc = nrows ? rowoff[nrows] : 0, Pl = nrows ? rowoff[2 * nrows + 1] - rowoff[nrows + 1] : 0;
+  const unsigned long long need = 2 + Pc + Pl;
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  if (need > W) {
+    if (t == 0) {
+      gate[0] = 2;
+      atomicMax(demand, need);
+    }
+    return;
+  }
+  if (t == 0) {
+    blk[0] = Pc;
+    blk[1] = Pl;
+  }
+  for (unsigned long long x = t; x < Pc; x += stride)
+    blk[2 + x] = (unsigned long long)(unsigned)ci[x] << 32 | (unsigned)cj[x];
+  for (unsigned long long x = t; x < Pl; x += stride)
+    blk[2 + Pc + x] = (unsigned long long)(unsigned)li[x] << 32 | (unsigned)lj[x];
+}
+
+struct KeyBlocks {
+  const unsigned long long *cur, *prev;  // nranks x W words each
+  unsigned long long W;
+  int nranks, rpr;                       // rows per rank: row i lives in block i / rpr
+};
+
+// is (i, j) a pair of the global list (los = 0: conflicts, 1: LoS)?
+__device__ __forceinline__ bool key_has(const unsigned long long *blocks, unsigned long long W, int rpr, int los,
+                                        unsigned i, unsigned j) {
+  const unsigned long long *b = blocks + (size_t)(i / (unsigned)rpr) * W;
+  const unsigned long long Pc = b[0], Pl = b[1];
+  const unsigned long long *k = b + 2 + (los ? Pc : 0);
+  unsigned long long lo = 0, hi = los ? Pl : Pc;
+  const unsigned long long key = (unsigned long long)i << 32 | j;
+  while (lo < hi) {
+    const unsigned long long mid = (lo + hi) >> 1;
+    if (k[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo < (los ? Pl : Pc) && k[lo] == key;
+}
+
+// blockIdx.y = rank block, blockIdx.z = 0 conflicts / 1 LoS
+__global__ __launch_bounds__(256) void k_bk_unique_g(KeyBlocks kb, unsigned long long *st,
+                                                     const unsigned long long *gate, const unsigned *sticky) {
+  if (bk_aborted(gate, sticky)) return;
+  const int los = blockIdx.z;
+  const unsigned long long *b = kb.cur + (size_t)blockIdx.y * kb.W;
+  const unsigned long long P = los ? b[1] : b[0];
+  const unsigned long long *keys = b + 2 + (los ? b[0] : 0);
+  const unsigned lane = threadIdx.x & 63;
+  for (unsigned long long x = blockIdx.x * blockDim.x + threadIdx.x; x - lane < P;
+       x += (unsigned long long)gridDim.x * blockDim.x) {
+    bool rep = false, fresh = false;
+    if (x < P) {
+      const unsigned i = (unsigned)(keys[x] >> 32), j = (unsigned)keys[x];
+      rep = i < j || !key_has(kb.cur, kb.W, kb.rpr, los, j, i);
+      if (rep) fresh = !(key_has(kb.prev, kb.W, kb.rpr, los, i, j) || key_has(kb.prev, kb.W, kb.rpr, los, j, i));
+    }
+    const unsigned long long mr = __ballot(rep), mf = __ballot(fresh);
+    if (lane == 0) {
+      if (mr) atomicAdd(st + 1 + los, (unsigned long long)__popcll(mr));
+      if (mf) atomicAdd(st + 3 + los, (unsigned long long)__popcll(mf));
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bk_copy_keys(unsigned long long words, const unsigned long long *src,
+                                                      unsigned long long *dst, const unsigned long long *gate,
+                                                      const unsigned *sticky) {
+  if (bk_aborted(gate, sticky)) return;
+  for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < words;
+       k += (unsigned long long)gridDim.x * blockDim.x)
+    dst[k] = src[k];
+}
+
 static BkIn bk_in(Ctx *c, const BkDev &d) {
   BkIn in;
   in.rb = (int)c->last_rb;
@@ -239,8 +330,9 @@ static BkIn bk_in(Ctx *c, const BkDev &d) {
 static unsigned long long bk_ncap(Ctx *c) { return c->bk_cap; }
 
 int bk_count(Ctx *c, const BkDev &d) {
-  const int64_t nrows = c->last_re - c->last_rb, n = c->n;
-  if (nrows <= 0) return 0;
+  const int64_t nrows = std::max<int64_t>(c->last_re - c->last_rb, 0), n = c->n;
+  // a rank without rows still takes part in the key all-gather (several ranks)
+  if (nrows == 0 && !comm_multi(c)) return 0;
   if (c->bk_cap == 0) c->bk_cap = std::max<unsigned long long>(c->cand_cap, 1 << 16);
   const unsigned long long ncap = bk_ncap(c);
   const size_t lcap = (size_t)std::max(c->cand_cap, c->los_cap) * 4;
@@ -256,11 +348,32 @@ int bk_count(Ctx *c, const BkDev &d) {
       !ensure_keep(c, c->bk_plcol, lcap, "previous los") ||
       !ensure_keep(c, c->bk_stats, 8 * 8, "bookkeeping stats"))
     return -1;
+  const bool multi = comm_multi(c);
+  if (multi) {  // global unique-pair sets: this rank's key block + all ranks' (this and the previous call)
+    if (c->bk_kw == 0) c->bk_kw = 1 << 16;
+    const size_t blk = (size_t)c->bk_kw * 8, all = blk * c->nranks;
+    if (c->bk_ready && c->bk_kw_alloc && c->bk_kw != c->bk_kw_alloc) {
+      // key blocks regrown after an overflow: re-lay the previous call's blocks out at the new width
+      DevBuf nb;
+      if (!ensure(c, nb, all, "previous gathered pair keys")) return -1;
+      BSA_HIP(c, hipMemsetAsync(nb.p, 0, all, c->stream));
+      BSA_HIP(c, hipMemcpy2DAsync(nb.p, blk, c->bk_kprev.p, (size_t)c->bk_kw_alloc * 8,
+                                  (size_t)c->bk_kw_alloc * 8, c->nranks, hipMemcpyDeviceToDevice, c->stream));
+      BSA_HIP(c, hipStreamSynchronize(c->stream));
+      release(c->bk_kprev);
+      c->bk_kprev = nb;
+    }
+    if (!ensure(c, c->bk_ksend, blk, "pair key block") || !ensure(c, c->bk_kcur, all, "gathered pair keys") ||
+        !ensure_keep(c, c->bk_kprev, all, "previous gathered pair keys"))
+      return -1;
+    c->bk_kw_alloc = c->bk_kw;
+  }
   if (!c->bk_ready) {  // empty sets
     BSA_HIP(c, hipMemsetAsync(c->bk_rptr.p, 0, (size_t)(nrows + 1) * 4, c->stream));
     BSA_HIP(c, hipMemsetAsync(c->bk_pcptr.p, 0, (size_t)(n + 1) * 4, c->stream));
     BSA_HIP(c, hipMemsetAsync(c->bk_plptr.p, 0, (size_t)(n + 1) * 4, c->stream));
     BSA_HIP(c, hipMemsetAsync(c->bk_stats.p, 0, 8 * 8, c->stream));
+    if (multi) BSA_HIP(c, hipMemsetAsync(c->bk_kprev.p, 0, (size_t)c->bk_kw * 8 * c->nranks, c->stream));
     c->bk_ready = true;
   }
   const BkIn in = bk_in(c, d);
@@ -276,15 +389,22 @@ int bk_count(Ctx *c, const BkDev &d) {
   hipLaunchKernelGGL(k_bk_check, dim3(1), dim3(1), 0, c->stream, (int)nrows, (const unsigned *)c->bk_nptr.p,
                      ncap, d.gate, (const unsigned *)d.sticky, d.demand);
   BSA_HIP(c, hipGetLastError());
+  if (multi) {
+    hipLaunchKernelGGL(k_bk_pack, dim3(256), dim3(256), 0, c->stream, (int)nrows, (const unsigned *)c->rowoff.p,
+                       (const int *)c->out_ci.p, (const int *)c->out_cj.p, (const int *)c->out_li.p,
+                       (const int *)c->out_lj.p, (unsigned long long)c->bk_kw,
+                       (unsigned long long *)c->bk_ksend.p, d.gate, (const unsigned *)d.sticky, d.kdemand);
+    BSA_HIP(c, hipGetLastError());
+  }
   return 0;
 }
 
 int bk_apply(Ctx *c, const BkDev &d) {
-  const int64_t nrows = c->last_re - c->last_rb;
-  if (nrows <= 0) return 0;
-  const bool uniq = c->nranks == 1;
+  const int64_t nrows = std::max<int64_t>(c->last_re - c->last_rb, 0);
+  if (nrows == 0 && !comm_multi(c)) return 0;
+  const bool multi = comm_multi(c), uniq = !multi;
   const BkIn in = bk_in(c, d);
-  const unsigned nb = (unsigned)((nrows + 255) / 256);
+  const unsigned nb = (unsigned)std::max<int64_t>((nrows + 255) / 256, 1);  // block 0 resets the per-call counts
   hipLaunchKernelGGL(k_bk_write, dim3(nb), dim3(256), 0, c->stream, in);
   BSA_HIP(c, hipGetLastError());
   hipLaunchKernelGGL(k_bk_lptr, dim3((unsigned)((nrows + 1 + 255) / 256)), dim3(256), 0, c->stream,
@@ -315,6 +435,20 @@ int bk_apply(Ctx *c, const BkDev &d) {
     hipLaunchKernelGGL(k_bk_unique, dim3(256), dim3(256), 0, c->stream, u, (const unsigned long long *)d.gate,
                        (const unsigned *)d.sticky);
     BSA_HIP(c, hipGetLastError());
+  } else {
+    // every rank's key block (stream-ordered after k_bk_pack and the gate)
+    const size_t blk = (size_t)c->bk_kw * 8;
+    if (comm_allgather(c, c->bk_ksend.p, c->bk_kcur.p, blk)) return -1;
+    KeyBlocks kb{(const unsigned long long *)c->bk_kcur.p, (const unsigned long long *)c->bk_kprev.p,
+                 (unsigned long long)c->bk_kw, c->nranks, (int)c->sim_rpr};
+    hipLaunchKernelGGL(k_bk_unique_g, dim3(64, c->nranks, 2), dim3(256), 0, c->stream, kb, st,
+                       (const unsigned long long *)d.gate, (const unsigned *)d.sticky);
+    BSA_HIP(c, hipGetLastError());
+    hipLaunchKernelGGL(k_bk_copy_keys, dim3(256), dim3(256), 0, c->stream,
+                       (unsigned long long)c->bk_kw * c->nranks, (const unsigned long long *)c->bk_kcur.p,
+                       (unsigned long long *)c->bk_kprev.p, (const unsigned long long *)d.gate,
+                       (const unsigned *)d.sticky);
+    BSA_HIP(c, hipGetLastError());
   }
   BkCommit m;
   m.nrows = (int)nrows;
@@ -339,10 +473,12 @@ int bk_apply(Ctx *c, const BkDev &d) {
 
 void bk_release(Ctx *c) {
   DevBuf *all[] = {&c->bk_rptr, &c->bk_rcol, &c->bk_nptr, &c->bk_ncol, &c->bk_cnt, &c->bk_lptr,
-                   &c->bk_pcptr, &c->bk_plptr, &c->bk_pccol, &c->bk_plcol, &c->bk_stats, &c->bk_tmp};
+                   &c->bk_pcptr, &c->bk_plptr, &c->bk_pccol, &c->bk_plcol, &c->bk_stats, &c->bk_tmp,
+                   &c->bk_ksend, &c->bk_kcur, &c->bk_kprev};
   for (auto *b : all) release(*b);
   c->bk_ready = false;
   c->bk_cap = 0;
+  c->bk_kw = c->bk_kw_alloc = 0;
 }
 
 }  // namespace bsa

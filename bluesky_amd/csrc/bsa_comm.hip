@@ -1,0 +1,404 @@
+// Collectives of the row-sharded resident sim, behind one
+// interface with two transports:
+//
+//  * RCCL (ncclComm_t over xGMI): one process per GPU -- the production path
+//    (bsa_comm_init with an id from bsa_comm_unique_id).
+//  * an in-process group (bsa_group_*): several contexts in ONE process, each
+//    driven by its own host thread, exchanging through device-to-device copies
+//    ordered by HIP events and a host barrier.  RCCL rejects two ranks on one
+//    GPU, so this is how the nranks > 1 code paths (k_pack / k_unpack, the gate
+//    all-reduce, the rank-order pair gather, the global unique-pair counts) run
+//    and are checked on a one-GPU box; it also serves a single process that
+//    drives several GPUs from several threads.
+//
+// Every collective is stream-ordered like RCCL's: it is enqueued on the
+// context's stream behind the work that produces its input, and later work on
+// that stream sees its output; only the host-value reductions synchronise.
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <new>
+
+#include "bsa_internal.h"
+
+namespace bsa {
+
+#define BSA_NCCL(c, call)                                                                     \
+  do {                                                                                        \
+    ncclResult_t r_ = (call);                                                                 \
+    if (r_ != ncclSuccess)                                                                    \
+      return ::bsa::fail((c), "%s failed: %s (%s:%d)", #call, ncclGetErrorString(r_), __FILE__, \
+                         __LINE__);                                                           \
+  } while (0)
+
+constexpr int kMaxGroup = 16;
+
+struct Group {
+  int n = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  unsigned long long phase = 0;
+  bool broken = false;
+  Ctx *ctx[kMaxGroup] = {};
+  DevBuf slot[kMaxGroup];                 // each rank's published copy (its own device)
+  hipEvent_t pub[kMaxGroup] = {}, done[kMaxGroup] = {};
+  std::vector<double> host[kMaxGroup];    // host-value exchange
+};
+
+// host barrier of the group; false (and the group marked broken) after 120 s
+// or when another rank gave up, so an error on one rank cannot hang the others
+static bool barrier(Ctx *c) {
+  Group *g = c->group;
+  std::unique_lock<std::mutex> lk(g->m);
+  if (g->broken) return fail(c, "in-process group broken by another rank"), false;
+  const unsigned long long ph = g->phase;
+  if (++g->arrived == g->n) {
+    g->arrived = 0;
+    g->phase++;
+    g->cv.notify_all();
+    return true;
+  }
+  const bool ok = g->cv.wait_for(lk, std::chrono::seconds(120), [&] { return g->phase != ph || g->broken; });
+  if (!ok || g->broken) {
+    g->broken = true;
+    g->cv.notify_all();
+    fail(c, "in-process group barrier timed out or broken (rank %d)", c->rank);
+    return false;
+  }
+  return true;
+}
+
+// rank r publishes `bytes` from device `src` into its slot (after every rank
+// finished reading the previous collective's slots), then waits for all slots
+static int publish(Ctx *c, const void *src, size_t bytes) {
+  Group *g = c->group;
+  const int r = c->rank;
+  for (int q = 0; q < g->n; ++q) BSA_HIP(c, hipStreamWaitEvent(c->stream, g->done[q], 0));
+  if (g->slot[r].bytes < bytes) {
+    for (int q = 0; q < g->n; ++q) BSA_HIP(c, hipEventSynchronize(g->done[q]));
+    if (!ensure(c, g->slot[r], bytes, "group slot")) return -1;
+  }
+  if (bytes) BSA_HIP(c, hipMemcpyAsync(g->slot[r].p, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+  BSA_HIP(c, hipEventRecord(g->pub[r], c->stream));
+  if (!barrier(c)) return -1;
+  for (int q = 0; q < g->n; ++q) BSA_HIP(c, hipStreamWaitEvent(c->stream, g->pub[q], 0));
+  return 0;
+}
+
+static int retire(Ctx *c) {
+  Group *g = c->group;
+  BSA_HIP(c, hipEventRecord(g->done[c->rank], c->stream));
+  return barrier(c) ? 0 : -1;
+}
+
+struct SlotPtrs {
+  const unsigned long long *p[kMaxGroup];
+};
+__global__ void k_max_u64_slots(unsigned long long *out, int count, int nq, SlotPtrs s) {
+  const int k = threadIdx.x;
+  if (k >= count) return;
+  unsigned long long v = 0;
+  for (int q = 0; q < nq; ++q) v = s.p[q][k] > v ? s.p[q][k] : v;
+  out[k] = v;
+}
+
+bool comm_multi(const Ctx *c) { return c->nranks > 1 && (c->comm || c->group); }
+
+int comm_allgather(Ctx *c, const void *send, void *recv, size_t bytes) {
+  if (!comm_multi(c)) {
+    if (bytes && recv != send) BSA_HIP(c, hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+  }
+  if (c->comm) {
+    BSA_NCCL(c, ncclAllGather(send, recv, bytes, ncclUint8, (ncclComm_t)c->comm, c->stream));
+    return 0;
+  }
+  Group *g = c->group;
+  if (publish(c, send, bytes)) return -1;
+  for (int q = 0; q < g->n; ++q)
+    if (bytes)
+      BSA_HIP(c, hipMemcpyAsync((char *)recv + (size_t)q * bytes, g->slot[q].p, bytes, hipMemcpyDeviceToDevice,
+                                c->stream));
+  return retire(c);
+}
+
+int comm_allreduce_max_u64(Ctx *c, unsigned long long *buf, int count) {
+  if (!comm_multi(c) || count <= 0) return 0;
+  if (count > 256) return fail(c, "device max all-reduce of %d words", count);
+  if (c->comm) {
+    BSA_NCCL(c, ncclAllReduce(buf, buf, (size_t)count, ncclUint64, ncclMax, (ncclComm_t)c->comm, c->stream));
+    return 0;
+  }
+  Group *g = c->group;
+  if (publish(c, buf, (size_t)count * 8)) return -1;
+  SlotPtrs s{};
+  for (int q = 0; q < g->n; ++q) s.p[q] = (const unsigned long long *)g->slot[q].p;
+  hipLaunchKernelGGL(k_max_u64_slots, dim3(1), dim3(256), 0, c->stream, buf, count, g->n, s);
+  BSA_HIP(c, hipGetLastError());
+  return retire(c);
+}
+
+int comm_allreduce_host(Ctx *c, double *v, int count, bool max) {
+  if (!comm_multi(c) || count <= 0) return 0;
+  if (c->comm) {
+    if (!ensure(c, c->red, (size_t)count * 8, "reduction scratch")) return -1;
+    BSA_HIP(c, hipMemcpyAsync(c->red.p, v, (size_t)count * 8, hipMemcpyHostToDevice, c->stream));
+    BSA_NCCL(c, ncclAllReduce(c->red.p, c->red.p, (size_t)count, ncclDouble, max ? ncclMax : ncclSum,
+                              (ncclComm_t)c->comm, c->stream));
+    BSA_HIP(c, hipMemcpyAsync(v, c->red.p, (size_t)count * 8, hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    return 0;
+  }
+  Group *g = c->group;
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  g->host[c->rank].assign(v, v + count);
+  if (!barrier(c)) return -1;
+  for (int k = 0; k < count; ++k) {
+    double a = max ? g->host[0][k] : 0.0;
+    for (int q = 0; q < g->n; ++q) {
+      const double x = g->host[q][k];
+      a = max ? (x > a ? x : a) : a + x;
+    }
+    v[k] = a;
+  }
+  return barrier(c) ? 0 : -1;
+}
+
+// rank-order gather of variable-size device blocks to root's device buffer
+// `recv` (root only; block q lands at offset off[q], off[] known to all ranks)
+int comm_gatherv(Ctx *c, int root, const void *send, size_t bytes, void *recv, const size_t *off,
+                 const size_t *len) {
+  if (!comm_multi(c)) {
+    if (bytes && recv != send) BSA_HIP(c, hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+  }
+  if (c->comm) {
+    BSA_NCCL(c, ncclGroupStart());
+    if (c->rank == root) {
+      for (int q = 0; q < c->nranks; ++q) {
+        if (!len[q]) continue;
+        if (q == root)
+          BSA_HIP(c, hipMemcpyAsync((char *)recv + off[q], send, len[q], hipMemcpyDeviceToDevice, c->stream));
+        else
+          BSA_NCCL(c, ncclRecv((char *)recv + off[q], len[q], ncclUint8, q, (ncclComm_t)c->comm, c->stream));
+      }
+    } else if (bytes) {
+      BSA_NCCL(c, ncclSend(send, bytes, ncclUint8, root, (ncclComm_t)c->comm, c->stream));
+    }
+    BSA_NCCL(c, ncclGroupEnd());
+    return 0;
+  }
+  Group *g = c->group;
+  if (publish(c, send, bytes)) return -1;
+  if (c->rank == root)
+    for (int q = 0; q < g->n; ++q)
+      if (len[q])
+        BSA_HIP(c, hipMemcpyAsync((char *)recv + off[q], g->slot[q].p, len[q], hipMemcpyDeviceToDevice, c->stream));
+  return retire(c);
+}
+
+void comm_release(Ctx *c) {
+  if (c->comm) {
+    ncclCommDestroy((ncclComm_t)c->comm);
+    c->comm = nullptr;
+  }
+  if (c->group) {
+    Group *g = c->group;
+    std::lock_guard<std::mutex> lk(g->m);
+    if (g->ctx[c->rank] == c) {
+      (void)hipStreamSynchronize(c->stream);
+      release(g->slot[c->rank]);
+      if (g->pub[c->rank]) (void)hipEventDestroy(g->pub[c->rank]);
+      if (g->done[c->rank]) (void)hipEventDestroy(g->done[c->rank]);
+      g->pub[c->rank] = g->done[c->rank] = nullptr;
+      g->ctx[c->rank] = nullptr;
+    }
+    c->group = nullptr;
+  }
+  c->nranks = 1;
+  c->rank = 0;
+}
+
+}  // namespace bsa
+
+using bsa::Ctx;
+
+struct bsa_group : bsa::Group {};
+
+extern "C" {
+
+int bsa_comm_unique_id(char *id128) {
+  if (!id128) return -1;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+int bsa_comm_init(bsa_ctx *cc, int nranks, int rank, const char *id128) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!id128 || nranks < 1 || rank < 0 || rank >= nranks) return bsa::fail(c, "bad comm arguments");
+  BSA_HIP(c, hipSetDevice(c->device));
+  bsa::comm_release(c);
+  ncclUniqueId id;
+  memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t comm;
+  BSA_NCCL(c, ncclCommInitRank(&comm, nranks, id, rank));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  c->sim_ready = false;  // the row partition changed
+  return 0;
+}
+
+bsa_group *bsa_group_create(int nranks) {
+  if (nranks < 1 || nranks > bsa::kMaxGroup) return nullptr;
+  bsa_group *g = new (std::nothrow) bsa_group();
+  if (g) g->n = nranks;
+  return g;
+}
+
+void bsa_group_destroy(bsa_group *g) { delete g; }
+
+int bsa_comm_init_group(bsa_ctx *cc, bsa_group *g, int rank) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!g || rank < 0 || rank >= g->n) return bsa::fail(c, "bad group arguments");
+  BSA_HIP(c, hipSetDevice(c->device));
+  bsa::comm_release(c);
+  {
+    std::lock_guard<std::mutex> lk(g->m);
+    if (g->ctx[rank]) return bsa::fail(c, "group rank %d already joined", rank);
+    g->ctx[rank] = c;
+  }
+  BSA_HIP(c, hipEventCreateWithFlags(&g->pub[rank], hipEventDisableTiming));
+  BSA_HIP(c, hipEventCreateWithFlags(&g->done[rank], hipEventDisableTiming));
+  BSA_HIP(c, hipEventRecord(g->pub[rank], c->stream));
+  BSA_HIP(c, hipEventRecord(g->done[rank], c->stream));
+  c->group = g;
+  c->nranks = g->n;
+  c->rank = rank;
+  c->sim_ready = false;
+  return 0;
+}
+
+// C2: per-rank (P, L, rows) of the last detect, all ranks
+static int gather_layout(Ctx *c, std::vector<int64_t> &cnt) {
+  if (bsa::sim_adopt_pairs(c)) return -1;
+  if (!c->have_pairs) return bsa::fail(c, "no detect results to gather");
+  std::vector<double> v((size_t)3 * c->nranks, 0.0);
+  v[3 * c->rank + 0] = (double)c->last_conf;
+  v[3 * c->rank + 1] = (double)c->last_los;
+  v[3 * c->rank + 2] = (double)(c->last_re - c->last_rb);
+  if (bsa::comm_allreduce_host(c, v.data(), (int)v.size(), false)) return -1;
+  cnt.resize(v.size());
+  for (size_t k = 0; k < v.size(); ++k) cnt[k] = (int64_t)v[k];
+  return 0;
+}
+
+// one rank's packed block: ci cj (P int32) | payload 5 x P doubles | li lj (L int32) | inconf (R) | tcpamax (R)
+static size_t al8(size_t b) { return (b + 7) & ~size_t(7); }
+static size_t block_bytes(int64_t P, int64_t L, int64_t R) {
+  return al8((size_t)P * 8) + (size_t)P * 40 + al8((size_t)L * 8) + al8((size_t)R) + (size_t)R * 8;
+}
+
+int bsa_gather_counts(bsa_ctx *cc, int64_t *totals3) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !totals3) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  std::vector<int64_t> cnt;
+  if (gather_layout(c, cnt)) return -1;
+  totals3[0] = totals3[1] = totals3[2] = 0;
+  for (int q = 0; q < c->nranks; ++q)
+    for (int k = 0; k < 3; ++k) totals3[k] += cnt[3 * q + k];
+  return 0;
+}
+
+int bsa_gather_pairs(bsa_ctx *cc, int root, const bsa_pairs_out *out) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (root < 0 || root >= c->nranks) return bsa::fail(c, "bad root rank %d", root);
+  if (c->rank == root && !out) return bsa::fail(c, "NULL output on the root rank");
+  BSA_HIP(c, hipSetDevice(c->device));
+  std::vector<int64_t> cnt;
+  if (gather_layout(c, cnt)) return -1;
+  const int nr = c->nranks;
+  std::vector<size_t> off(nr), len(nr);
+  size_t total = 0;
+  for (int q = 0; q < nr; ++q) {
+    off[q] = total;
+    len[q] = block_bytes(cnt[3 * q], cnt[3 * q + 1], cnt[3 * q + 2]);
+    total += len[q];
+  }
+  // pack this rank's block (device to device, stream-ordered after the detect)
+  const int64_t P = c->last_conf, L = c->last_los, R = c->last_re - c->last_rb;
+  if (!bsa::ensure(c, c->pg_send, len[c->rank], "pair gather block")) return -1;
+  char *b = (char *)c->pg_send.p;
+  hipStream_t s = c->stream;
+  auto d2d = [&](size_t at, const void *src, size_t bytes) -> int {
+    if (bytes) BSA_HIP(c, hipMemcpyAsync(b + at, src, bytes, hipMemcpyDeviceToDevice, s));
+    return 0;
+  };
+  size_t at = 0;
+  if (d2d(at, c->out_ci.p, (size_t)P * 4) || d2d(at + (size_t)P * 4, c->out_cj.p, (size_t)P * 4)) return -1;
+  at += al8((size_t)P * 8);
+  if (d2d(at, c->out_pay.p, (size_t)P * 40)) return -1;
+  at += (size_t)P * 40;
+  if (d2d(at, c->out_li.p, (size_t)L * 4) || d2d(at + (size_t)L * 4, c->out_lj.p, (size_t)L * 4)) return -1;
+  at += al8((size_t)L * 8);
+  if (d2d(at, c->inconf.p, (size_t)R)) return -1;
+  at += al8((size_t)R);
+  if (d2d(at, c->tcpamax.p, (size_t)R * 8)) return -1;
+  if (c->rank == root && !bsa::ensure(c, c->pg_recv, total, "pair gather")) return -1;
+  if (bsa::comm_gatherv(c, root, c->pg_send.p, len[c->rank], c->rank == root ? c->pg_recv.p : nullptr, off.data(),
+                        len.data()))
+    return -1;
+  if (c->rank != root) return 0;
+  std::vector<char> h(total);
+  if (total) BSA_HIP(c, hipMemcpyAsync(h.data(), c->pg_recv.p, total, hipMemcpyDeviceToHost, s));
+  BSA_HIP(c, hipStreamSynchronize(s));
+  // concatenate in rank order = the global row-major order (rows are partitioned contiguously)
+  int64_t pc = 0, pl = 0, pr = 0;
+  for (int q = 0; q < nr; ++q) {
+    const int64_t Pq = cnt[3 * q], Lq = cnt[3 * q + 1], Rq = cnt[3 * q + 2];
+    const char *blk = h.data() + off[q];
+    auto put = [](void *dst, int64_t at_elems, size_t esz, const char *src, int64_t n) {
+      if (dst && n) memcpy((char *)dst + (size_t)at_elems * esz, src, (size_t)n * esz);
+    };
+    put(out->ci, pc, 4, blk, Pq);
+    put(out->cj, pc, 4, blk + (size_t)Pq * 4, Pq);
+    const char *pay = blk + al8((size_t)Pq * 8);
+    double *dst5[5] = {out->qdr, out->dist, out->tcpa, out->tinconf, out->dcpa};
+    for (int f = 0; f < 5; ++f) put(dst5[f], pc, 8, pay + (size_t)f * Pq * 8, Pq);
+    const char *lp = pay + (size_t)Pq * 40;
+    put(out->li, pl, 4, lp, Lq);
+    put(out->lj, pl, 4, lp + (size_t)Lq * 4, Lq);
+    const char *rp = lp + al8((size_t)Lq * 8);
+    put(out->inconf, pr, 1, rp, Rq);
+    put(out->tcpamax, pr, 8, rp + al8((size_t)Rq), Rq);
+    pc += Pq;
+    pl += Lq;
+    pr += Rq;
+  }
+  return 0;
+}
+
+int bsa_comm_allreduce_max(bsa_ctx *cc, double *values, int count) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || (!values && count > 0)) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  return bsa::comm_allreduce_host(c, values, count, true);
+}
+
+int bsa_comm_allreduce_sum(bsa_ctx *cc, double *values, int count) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || (!values && count > 0)) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  return bsa::comm_allreduce_host(c, values, count, false);
+}
+
+}  // extern "C"

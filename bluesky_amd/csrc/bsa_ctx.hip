@@ -218,8 +218,9 @@ int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *d
                     double *tinconf, double *dcpa, int32_t *li, int32_t *lj, uint8_t *inconf,
                     double *tcpamax) {
   if (!c) return -1;
-  if (!c->have_pairs) return bsa::fail(c, "no detect results to fetch");
   BSA_HIP(c, hipSetDevice(c->device));
+  if (bsa::sim_adopt_pairs(c)) return -1;
+  if (!c->have_pairs) return bsa::fail(c, "no detect results to fetch");
   const int64_t P = c->last_conf, L = c->last_los, R = c->last_re - c->last_rb;
   auto cp = [&](void *dst, const void *src, size_t bytes) -> int {
     if (dst && bytes) BSA_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));

@@ -105,7 +105,7 @@ static int feed_poll(Ctx *c, int wait, bsa_acdata *o) {
   }
   const int64_t nr = c->feed_re - c->feed_rb;
   const unsigned long long *hdr = (const unsigned long long *)c->feed_host;
-  const bool counts = c->simp.resume_nav && c->nranks == 1;
+  const bool counts = c->simp.resume_nav != 0;  // global counts, the same on every rank
   o->steps = c->feed_steps;
   o->row_begin = c->feed_rb;
   o->row_end = c->feed_re;

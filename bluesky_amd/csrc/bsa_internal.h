@@ -196,10 +196,13 @@ struct Ctx {
   // MVP / kinematics staging (host-buffer entry points)
   DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl;
 
-  // multi-GPU (RCCL); comm is an ncclComm_t
+  // multi-GPU: comm is an ncclComm_t (one process per GPU) or group an
+  // in-process group of contexts (bsa_comm.hip); at most one is set
   void *comm = nullptr;
+  struct Group *group = nullptr;
   int nranks = 1, rank = 0;
   DevBuf red;  // small reduction scratch
+  DevBuf pg_send, pg_recv;  // C2 pair gather staging (bsa_gather_pairs)
 
   // GPU-resident sim (bsa_sim.hip)
   bool sim_ready = false;
@@ -212,13 +215,18 @@ struct Ctx {
   DevBuf s_atrk, s_atas, s_avs, s_aalt, s_ase, s_asn, s_active;  // ASAS (full n)
   DevBuf g_send, g_recv;                                    // all-gather staging
   DevBuf sim_ctl;  // [0,16) gate {overflow, P}; [16,20) sticky abort; [24,32) steps done;
-                   // [32,40) resopairs demand on a bookkeeping overflow
+                   // [32,40) resopairs demand on a bookkeeping overflow; [40,48) pair-key
+                   // block demand (several ranks)
   // ASAS bookkeeping (bsa_asas.hip, resume_nav = 1): resopairs CSR over own
   // rows (+ next), per-row kept counts, LoS row pointers of the last call,
   // previous call's conflict / LoS CSR (one rank), stats
   DevBuf bk_rptr, bk_rcol, bk_nptr, bk_ncol, bk_cnt, bk_lptr, bk_pcptr, bk_plptr, bk_pccol, bk_plcol;
   DevBuf bk_stats, bk_tmp;
   unsigned long long bk_cap = 0;  // resopairs capacity (pairs)
+  // several ranks: this rank's pair-key block and all ranks' blocks (this / the
+  // previous call), bk_kw words per rank (grown on demand, the step retried)
+  DevBuf bk_ksend, bk_kcur, bk_kprev;
+  unsigned long long bk_kw = 0, bk_kw_alloc = 0;
   bool bk_ready = false;
 
   // 2-D wind field (bsa_set_windfield): lat lon vnorth veast of wf_nvec points
@@ -281,7 +289,8 @@ struct BkDev {
   uint8_t *active;
   unsigned long long *gate;
   unsigned *sticky;
-  unsigned long long *demand;
+  unsigned long long *demand;   // resopairs overflow: pairs needed
+  unsigned long long *kdemand;  // several ranks, key block overflow: words needed
 };
 int bk_count(Ctx *c, const BkDev &d);
 int bk_apply(Ctx *c, const BkDev &d);
@@ -297,9 +306,20 @@ int fail(Ctx *c, const char *fmt, ...);
                          __FILE__, __LINE__);                                         \
   } while (0)
 
+// collectives (bsa_comm.hip): RCCL or the in-process group, stream-ordered;
+// no-ops (plain copies) with one rank
+bool comm_multi(const Ctx *c);
+int comm_allgather(Ctx *c, const void *send, void *recv, size_t bytes);  // recv: nranks x bytes
+int comm_allreduce_max_u64(Ctx *c, unsigned long long *buf, int count); // device words, in place
+int comm_allreduce_host(Ctx *c, double *v, int count, bool max);         // host values (synchronises)
+int comm_gatherv(Ctx *c, int root, const void *send, size_t bytes, void *recv, const size_t *off,
+                 const size_t *len);                                     // rank-order blocks to root
+void comm_release(Ctx *c);
+
 // sim / comm teardown (bsa_sim.hip); ACDATA feed teardown (bsa_feed.hip)
 void sim_release(Ctx *c);
 void feed_release(Ctx *c);
+int sim_adopt_pairs(Ctx *c);  // after resident steps: the last CD call's pairs become fetchable
 
 // detect entry points (bsa_cd.hip): detect = enqueue + finish (+ retries)
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,

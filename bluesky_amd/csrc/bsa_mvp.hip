@@ -187,12 +187,20 @@ __global__ __launch_bounds__(256) void k_mvp_row(int rb, bsa_mvp_params p, MvpIn
 int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned *seg,
                const unsigned long long *gate, unsigned *sticky, const uint8_t *inconf, uint8_t *active,
                bool resolve, bool pairs_done) {
-  const int64_t rb = c->last_rb, re = c->last_re, nrows = re - rb;
-  if (nrows <= 0) return 0;
+  const int64_t rb = c->last_rb, re = c->last_re, nrows = std::max<int64_t>(re - rb, 0);
+  if (nrows == 0 && !gate) return 0;  // (a resident rank without rows still applies the gate)
   const unsigned long long pcap = std::max<unsigned long long>(c->cand_cap, (unsigned long long)c->last_conf);
   if (!ensure(c, c->mvp_pdv, std::max<unsigned long long>(pcap, 1) * sizeof(double4), "mvp pair dv") ||
       !ensure(c, c->mvp_pfl, std::max<unsigned long long>(pcap, 1), "mvp pair flags"))
     return -1;
+  if (nrows == 0) {
+    MvpIn in{};
+    in.gate = gate;
+    in.sticky = sticky;
+    hipLaunchKernelGGL(k_mvp_row, dim3(1), dim3(64), 0, c->stream, (int)rb, p, in);
+    BSA_HIP(c, hipGetLastError());
+    return 0;
+  }
   if (!seg) {
     if (!ensure(c, c->seg, (size_t)(nrows + 1) * 4, "mvp segments")) return -1;
     hipLaunchKernelGGL(k_segments, dim3((unsigned)((nrows + 1 + 255) / 256)), dim3(256), 0, c->stream,

@@ -18,21 +18,11 @@
 // every later kernel that writes persistent state (K3, K4') becomes a no-op,
 // so the state stays exactly as before the failed step; the host then grows
 // the buffers and re-runs the batch from that step.
-#include <rccl/rccl.h>
-
 #include "bsa_kin_math.h"
 
 #pragma clang fp contract(off)
 
 namespace bsa {
-
-#define BSA_NCCL(c, call)                                                                     \
-  do {                                                                                        \
-    ncclResult_t r_ = (call);                                                                 \
-    if (r_ != ncclSuccess)                                                                    \
-      return ::bsa::fail((c), "%s failed: %s (%s:%d)", #call, ncclGetErrorString(r_), __FILE__, \
-                         __LINE__);                                                           \
-  } while (0)
 
 struct SimDev {
   double *lat, *lon, *trk, *gs, *alt, *vs, *tas, *hdg, *gse, *gsn;
@@ -171,18 +161,7 @@ static SimDev sim_dev(Ctx *c) {
   return d;
 }
 
-static int allreduce(Ctx *c, double *v, int count, ncclRedOp_t op) {
-  if (!c->comm || c->nranks == 1 || count <= 0) return 0;
-  if (!ensure(c, c->red, (size_t)count * 8, "reduction scratch")) return -1;
-  BSA_HIP(c, hipMemcpyAsync(c->red.p, v, (size_t)count * 8, hipMemcpyHostToDevice, c->stream));
-  BSA_NCCL(c, ncclAllReduce(c->red.p, c->red.p, (size_t)count, ncclDouble, op, (ncclComm_t)c->comm,
-                            c->stream));
-  BSA_HIP(c, hipMemcpyAsync(v, c->red.p, (size_t)count * 8, hipMemcpyDeviceToHost, c->stream));
-  BSA_HIP(c, hipStreamSynchronize(c->stream));
-  return 0;
-}
-
-// one RCCL all-gather of the listed arrays' rows [sim_rb, sim_re) of every rank
+// one all-gather (RCCL or in-process group) of the listed arrays' rows [sim_rb, sim_re) of every rank
 static int gather_fields(Ctx *c, const Fields &fl) {
   const int64_t rpr = c->sim_rpr, n = c->n;
   const int slots = fl.nf + (fl.u8 ? 1 : 0);
@@ -193,7 +172,7 @@ static int gather_fields(Ctx *c, const Fields &fl) {
   hipLaunchKernelGGL(k_pack, dim3((unsigned)((rpr + 255) / 256)), dim3(256), 0, c->stream, (int)c->sim_rb,
                      (int)c->sim_re, (int)rpr, fl, (double *)c->g_send.p);
   BSA_HIP(c, hipGetLastError());
-  BSA_NCCL(c, ncclAllGather(c->g_send.p, c->g_recv.p, blk, ncclDouble, (ncclComm_t)c->comm, c->stream));
+  if (comm_allgather(c, c->g_send.p, c->g_recv.p, blk * 8)) return -1;
   hipLaunchKernelGGL(k_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, (int)n,
                      (int)rpr, c->rank, fl, slots, (const double *)c->g_recv.p);
   BSA_HIP(c, hipGetLastError());
@@ -222,17 +201,32 @@ static int sim_gather_asas(Ctx *c) {
   return gather_fields(c, fl);
 }
 
+// the resident step's last CD call as "the last detect" (its counts are
+// read from the device; the host never synchronised on that detect)
+int sim_adopt_pairs(Ctx *c) {
+  if (c->have_pairs || !c->sim_ready || c->sim_cd_calls == 0) return 0;
+  if (c->empty_detect) {
+    c->last_conf = c->last_los = 0;
+    c->have_pairs = true;
+    return 0;
+  }
+  Counters h;
+  BSA_HIP(c, hipMemcpyAsync(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  c->last_conf = (int64_t)h.conf;
+  c->last_los = (int64_t)h.los;
+  c->have_pairs = true;
+  return 0;
+}
+
 void sim_release(Ctx *c) {
   DevBuf *all[] = {&c->red, &c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
-                   &c->s_active, &c->g_send, &c->g_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env};
+                   &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env};
   for (auto *b : all) release(*b);
   bk_release(c);
-  if (c->comm) {
-    ncclCommDestroy((ncclComm_t)c->comm);
-    c->comm = nullptr;
-  }
+  comm_release(c);
 }
 
 // one CD step of the batch (enqueue only)
@@ -264,10 +258,10 @@ static int sim_cd(Ctx *c) {
   bk.gate = gate;
   bk.sticky = sticky;
   bk.demand = (unsigned long long *)((char *)c->sim_ctl.p + 32);
+  bk.kdemand = (unsigned long long *)((char *)c->sim_ctl.p + 40);
   // ASAS bookkeeping, first half: kept-pair counts (may flag a resopairs overflow in the gate)
   if (p.resume_nav && bk_count(c, bk)) return -1;
-  if (c->comm && c->nranks > 1)
-    BSA_NCCL(c, ncclAllReduce(gate, gate, 2, ncclUint64, ncclMax, (ncclComm_t)c->comm, c->stream));
+  if (comm_allreduce_max_u64(c, gate, 2)) return -1;
   const int64_t rb = c->sim_rb;
   MvpDev d;
   d.gseast = (const double *)c->s_gse.p;
@@ -304,47 +298,6 @@ static int sim_cd(Ctx *c) {
 using bsa::Ctx;
 
 extern "C" {
-
-int bsa_comm_unique_id(char *id128) {
-  if (!id128) return -1;
-  ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
-  memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
-  return 0;
-}
-
-int bsa_comm_init(bsa_ctx *cc, int nranks, int rank, const char *id128) {
-  Ctx *c = (Ctx *)cc;
-  if (!c) return -1;
-  if (!id128 || nranks < 1 || rank < 0 || rank >= nranks) return bsa::fail(c, "bad comm arguments");
-  BSA_HIP(c, hipSetDevice(c->device));
-  if (c->comm) {
-    ncclCommDestroy((ncclComm_t)c->comm);
-    c->comm = nullptr;
-  }
-  ncclUniqueId id;
-  memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
-  ncclComm_t comm;
-  BSA_NCCL(c, ncclCommInitRank(&comm, nranks, id, rank));
-  c->comm = comm;
-  c->nranks = nranks;
-  c->rank = rank;
-  return 0;
-}
-
-int bsa_comm_allreduce_max(bsa_ctx *cc, double *values, int count) {
-  Ctx *c = (Ctx *)cc;
-  if (!c || (!values && count > 0)) return -1;
-  BSA_HIP(c, hipSetDevice(c->device));
-  return bsa::allreduce(c, values, count, ncclMax);
-}
-
-int bsa_comm_allreduce_sum(bsa_ctx *cc, double *values, int count) {
-  Ctx *c = (Ctx *)cc;
-  if (!c || (!values && count > 0)) return -1;
-  BSA_HIP(c, hipSetDevice(c->device));
-  return bsa::allreduce(c, values, count, ncclSum);
-}
 
 int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_params *p) {
   Ctx *c = (Ctx *)cc;
@@ -420,7 +373,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
   for (int attempt = 0; c->sim_steps < target; ++attempt) {
     if (attempt > 6) return bsa::fail(c, "candidate buffer overflow in the resident step (retries exhausted)");
     const int64_t base = c->sim_steps, base_cd = c->sim_cd_calls;
-    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 24, c->stream));  // sticky, steps_done, demand
+    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 32, c->stream));  // sticky, steps_done, demands
     while (c->sim_steps < target) {
       if (c->sim_steps % c->simp.cd_every == 0)
         if (bsa::sim_cd(c)) return -1;
@@ -433,11 +386,14 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
       c->sim_steps++;
     }
     // the batch's only host synchronisation: did every step complete?
-    unsigned long long ctl[3] = {0, 0, 0};
-    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 24, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long ctl[4] = {0, 0, 0, 0};
+    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 32, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
     if ((unsigned)ctl[0] == 0) break;
-    // aborted at step base + done: the state is that of the step's start
+    // aborted at step base + done: the state is that of the step's start.  The
+    // gate is all-reduced, so every rank aborted at the same step; each rank
+    // grows only the buffers that overflowed on IT (another rank's overflow
+    // re-runs the step with unchanged buffers here) and all ranks re-run it
     c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
     const int64_t done = (int64_t)ctl[1];
     c->sim_steps = base + done;
@@ -445,19 +401,19 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     for (int64_t k = base; k < base + done; ++k) cds += (k % c->simp.cd_every == 0) ? 1 : 0;
     c->sim_cd_calls = base_cd + cds;
     c->sim_gathered = c->nranks == 1;
-    if (ctl[2] > 0) {  // this rank's resopairs outgrew their buffer
+    if (ctl[2] > 0)  // this rank's resopairs outgrew their buffer
       c->bk_cap = std::max(2 * c->bk_cap, ctl[2] + ctl[2] / 4 + 1024);
-      continue;
-    }
-    // candidate overflow (here or on another rank): grow at least double, and
-    // enough for the last detect's demand (its shard counters keep counting
-    // past the capacity)
+    if (ctl[3] > 0)  // this rank's pair keys outgrew their all-gather block
+      c->bk_kw = std::max(2 * c->bk_kw, ctl[3] + ctl[3] / 4 + 1024);
+    // candidate overflow on this rank: enough for the last detect's demand (its
+    // shard counters keep counting past the capacity; every detect after the
+    // abort ran on the same, unchanged state)
     bsa::Counters h;
     BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
     unsigned long long worst = 0;
     for (int q = 0; q < bsa::kCandShards; ++q) worst = std::max(worst, h.cshard[q][0]);
-    c->cand_cap = std::max(2 * c->cand_cap,
-                           (unsigned long long)bsa::kCandShards * (worst + worst / 4 + 1024));
+    if (worst > c->cand_cap / bsa::kCandShards)
+      c->cand_cap = std::max(2 * c->cand_cap, (unsigned long long)bsa::kCandShards * (worst + worst / 4 + 1024));
   }
   return 0;
 }
@@ -573,9 +529,8 @@ int bsa_sim_asas_stats(bsa_ctx *cc, int64_t *out6) {
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   int64_t na = 0;
   for (int64_t k = 0; k < nr; ++k) na += act[k] ? 1 : 0;
-  const bool one = c->nranks == 1;
   out6[0] = (int64_t)st[0];
-  for (int k = 1; k < 5; ++k) out6[k] = one ? (int64_t)st[k] : -1;
+  for (int k = 1; k < 5; ++k) out6[k] = (int64_t)st[k];  // global sets (identical on every rank)
   out6[5] = na;
   return 0;
 }

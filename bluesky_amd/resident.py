@@ -64,14 +64,19 @@ def params(simdt=0.05, rpz=5.0 * NM, hpz=1000.0 * FT, tla=300.0, cd_every=1, res
 class ResidentSim:
     """Device-resident traffic; ``rank``/``world`` > 1 shards the rows over GPUs."""
 
-    def __init__(self, state, p, ctx=None, rank=0, world=1, windfield=None, limits=None):
+    def __init__(self, state, p, ctx=None, rank=0, world=1, windfield=None, limits=None, group=None):
         """``windfield``: dict(lat, lon, vnorth, veast) of the 2-D field's points
         (Windfield.lat / lon / vnorth[0, :] / veast[0, :]) for ``winddim`` 2.
         ``limits``: per-aircraft OpenAP envelope dict(hmax, vmin, vmax, vsmin,
-        vsmax, axmax) for Pilot.applylimits (pilot.py:65-68), or None."""
+        vsmax, axmax) for Pilot.applylimits (pilot.py:65-68), or None.
+        ``group``: an in-process ``_lib.Group`` to join as ``rank`` instead of
+        an RCCL communicator (several ranks in one process, one thread each)."""
         self.ctx = ctx or _lib.default_context()
         self.rank, self.world = rank, world
-        if world > 1:
+        if group is not None:
+            if getattr(self.ctx, 'comm_rank_world', None) != (rank, group.nranks):
+                self.ctx.comm_init_group(group, rank)
+        elif world > 1:
             dist.init_comm(self.ctx, rank, world)
         if windfield is not None:
             self.ctx.set_windfield(windfield['lat'], windfield['lon'], windfield['vnorth'],
@@ -100,6 +105,10 @@ class ResidentSim:
 
     def resopairs(self):
         return self.ctx.sim_resopairs()
+
+    def gather_pairs(self, root=0):
+        """C2: the last CD call's pairs of all ranks, on ``root`` (collective)."""
+        return self.ctx.gather_pairs(root)
 
     def acdata_request(self):
         """Enqueue an ACDATA snapshot of this rank's rows behind the queued steps

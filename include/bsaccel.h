@@ -276,11 +276,41 @@ int bsa_geo_last_ms(bsa_ctx *ctx, double *ms);
  * to the other ranks out of band. */
 int bsa_comm_unique_id(char *id128);
 int bsa_comm_init(bsa_ctx *ctx, int nranks, int rank, const char *id128);
+/* In-process group: several contexts in ONE process form the ranks of a
+ * row-sharded sim, each driven by its own host thread, exchanging with
+ * device-to-device copies ordered by HIP events (RCCL refuses two ranks on one
+ * GPU; this runs the nranks > 1 paths on one GPU and lets one process drive
+ * several).  Create the group, then every rank joins it from its thread; the
+ * group outlives its contexts (destroy it after them). */
+typedef struct bsa_group bsa_group;
+bsa_group *bsa_group_create(int nranks);  /* NULL if nranks is not in [1, 16] */
+void bsa_group_destroy(bsa_group *g);
+int bsa_comm_init_group(bsa_ctx *ctx, bsa_group *g, int rank);
 /* Collective: element-wise max of `count` host doubles over all ranks, in
  * place (also a barrier).  Without a communicator it is a no-op. */
 int bsa_comm_allreduce_max(bsa_ctx *ctx, double *values, int count);
 /* Collective: element-wise sum of `count` host doubles over all ranks. */
 int bsa_comm_allreduce_sum(bsa_ctx *ctx, double *values, int count);
+
+/* C2 pair gather ("pair lists are gathered to the host").
+ * Collective over the ranks' last detect (bsa_detect on each rank's row
+ * slice, or the resident sim's last CD call): totals3 = {conflict pairs, LoS
+ * pairs, rows} summed over all ranks (the root sizes its arrays from them);
+ * then bsa_gather_pairs moves every rank's results to `root` and concatenates
+ * them in rank order, which is the reference's global row-major order
+ * (StateBasedCD.py:93-101) since ranks own contiguous row blocks.  Arrays as
+ * in bsa_fetch_pairs (inconf / tcpamax: one entry per row of all ranks); any
+ * pointer may be NULL; `out` is read on the root only (dcpa is meaningful
+ * only when the detects used BSA_FLAG_WITH_DCPA). */
+typedef struct bsa_pairs_out {
+  int32_t *ci, *cj;
+  double *qdr, *dist, *tcpa, *tinconf, *dcpa;
+  int32_t *li, *lj;
+  uint8_t *inconf;
+  double *tcpamax;
+} bsa_pairs_out;
+int bsa_gather_counts(bsa_ctx *ctx, int64_t *totals3);
+int bsa_gather_pairs(bsa_ctx *ctx, int root, const bsa_pairs_out *out);
 
 /* ---------------------------------------------------------------- GPU-resident sim
  * The synthetic sim step of SURVEY.md 8d with all state resident in HBM:
@@ -353,8 +383,9 @@ int bsa_sim_stats(bsa_ctx *ctx, int64_t *out6);
  * ASAS.update's Python sets, asas.py:490-502):
  * [0] |resopairs| of this rank's rows, [1] |confpairs_unique|,
  * [2] |lospairs_unique|, [3] len(confpairs_all), [4] len(lospairs_all),
- * [5] number of active aircraft of this rank's rows.  [1]-[4] need the
- * whole pair set and are -1 with several ranks. */
+ * [5] number of active aircraft of this rank's rows.  [1]-[4] are counts of
+ * the global pair sets (every rank gathers all ranks' pair keys; the same
+ * values on every rank). */
 int bsa_sim_asas_stats(bsa_ctx *ctx, int64_t *out6);
 /* This rank's resopairs (idx1 ascending, then idx2), at most cap pairs;
  * *count = total (call again with a larger buffer when *count > cap). */
@@ -372,8 +403,8 @@ int bsa_sim_resopairs(bsa_ctx *ctx, int32_t *idx1, int32_t *idx2, int64_t cap, i
  * before the first), cas is traf.cas after the last step (0 before the first),
  * asasn / asase as asas holds them.  nconf_cur / nlos_cur = len(confpairs_unique) /
  * len(lospairs_unique), nconf_tot / nlos_tot = len(confpairs_all) /
- * len(lospairs_all) (screenio.py:207-210); -1 unless resume_nav = 1 on one
- * rank.  A new request first waits for the previous snapshot. */
+ * len(lospairs_all) (screenio.py:207-210), global over all ranks; -1 unless
+ * resume_nav = 1.  A new request first waits for the previous snapshot. */
 typedef struct bsa_acdata {
   int64_t steps, row_begin, row_end;  /* set by _poll */
   int64_t nconf_cur, nconf_tot, nlos_cur, nlos_tot;

@@ -1,0 +1,200 @@
+"""The nranks > 1 paths of libbsaccel on ONE GPU: several
+contexts in one process form the ranks of the row-sharded resident sim through
+the in-process group transport (bsa_group_*, bsa_comm.hip), one host thread per
+rank.  Everything the RCCL path does between ranks runs here too -- the state
+all-gather before each CD (k_pack / k_unpack), the gate all-reduce, the global
+unique-pair key all-gather, the C2 rank-order pair gather -- only the transport
+differs (device-to-device copies instead of xGMI).
+
+The sharded run must equal the one-rank run BITWISE: rows are independent in
+detect, MVP and the kinematics, so rank 0 (+) rank 1 (+) ... is the same
+arithmetic on the same inputs.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from bluesky_amd import _lib, resident, statebased, synth
+
+pytestmark = pytest.mark.gpu
+RPZ, HPZ, TLA = synth.RPZ, synth.HPZ, synth.TLOOKAHEAD
+
+
+def run_ranks(world, fn, timeout=240):
+    """fn(rank, ctx, group) on `world` threads, each with its own context."""
+    group = _lib.Group(world)
+    ctxs = [_lib.Context(0) for _ in range(world)]
+    out, err = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            out[r] = fn(r, ctxs[r], group)
+        except BaseException as e:   # noqa: BLE001 -- reported below
+            err[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    alive = [t.is_alive() for t in th]
+    if not any(alive):
+        for c in ctxs:
+            c.close()
+        group.close()
+    assert not any(alive), 'rank threads hung'
+    for e in err:
+        if e is not None:
+            raise e
+    return out
+
+
+def world1(init, p, steps, ctx):
+    sim = resident.ResidentSim(init, p, ctx=ctx)
+    sim.step(steps)
+    return sim
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_resident_steps_equal_world1(ctx, world):
+    """10 steps with MVP (CD every step): every state array of the sharded run
+    equals the one-rank run bitwise, and the C2 pair gather of the last CD call
+    equals the one-rank pair lists."""
+    t = synth.box(3001, 100.0, seed=61)
+    init = resident.initial_state(t)
+    p = resident.params(cd_every=1, swresohoriz=False)   # horizontal + vertical MVP
+    ref = world1(init, p, 10, ctx)
+    exp, exp_st = ref.read(), ref.stats()
+    exp_pairs = ctx.fetch_pairs(exp_st['n_conf'], exp_st['n_los'])
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=world, group=g)
+        sim.step(4)
+        sim.step(6)
+        return sim.read(), sim.stats(), sim.gather_pairs(root=0)
+
+    res = run_ranks(world, rank)
+    for r, (got, st, pairs) in enumerate(res):
+        for k in exp:
+            assert np.array_equal(got[k], exp[k]), 'rank %d %s' % (r, k)
+        assert st['steps'] == 10 and st['cd_calls'] == 10
+    n_conf = sum(st['n_conf'] for _, st, _ in res)
+    assert n_conf == exp_st['n_conf'] > 0
+    pairs = res[0][2]
+    assert all(x[2] is None for x in res[1:])
+    for k in ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'li', 'lj', 'inconf', 'tcpamax'):
+        assert np.array_equal(pairs[k], exp_pairs[k]), k
+
+
+def test_sharded_resume_nav_global_counts_equal_world1(ctx):
+    """resume_nav: resopairs (union over ranks), asas.active and the GLOBAL
+    unique / cumulative pair counts (asas.py:490-502, all-gathered key blocks)
+    equal the one-rank run at every CD call."""
+    t = synth.box(2500, 70.0, seed=67)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=1.0, resume_nav=True)
+    ref = resident.ResidentSim(init, p, ctx=ctx)
+    exp = []
+    for _ in range(6):
+        ref.step(1)
+        i, j = ref.resopairs()
+        exp.append((ref.asas_stats(), sorted(zip(i.tolist(), j.tolist())), ref.read()['active']))
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=2, group=g)
+        got = []
+        for _ in range(6):
+            sim.step(1)
+            i, j = sim.resopairs()
+            got.append((sim.asas_stats(), list(zip(i.tolist(), j.tolist())), sim.read()['active']))
+        return got
+
+    res = run_ranks(2, rank)
+    for k in range(6):
+        est, ereso, eact = exp[k]
+        reso = sorted(res[0][k][1] + res[1][k][1])
+        assert reso == ereso, k
+        for r in range(2):
+            st = res[r][k][0]
+            for f in ('confpairs_unique', 'lospairs_unique', 'confpairs_all', 'lospairs_all'):
+                assert st[f] == est[f], (k, r, f)
+            assert np.array_equal(res[r][k][2], eact), k
+        assert res[0][k][0]['resopairs'] + res[1][k][0]['resopairs'] == est['resopairs']
+    assert exp[-1][0]['confpairs_all'] > exp[0][0]['confpairs_unique'] > 0
+
+
+def test_sharded_overflow_on_one_rank_is_exact(ctx):
+    """A candidate list far too small on rank 1 only: rank 1 overflows, the gate
+    all-reduce aborts the step on BOTH ranks, rank 1 grows its list while rank 0
+    re-runs with unchanged buffers (bsa_sim_step); the same for a resopairs
+    overflow.  The result is bitwise the undisturbed one-rank run's."""
+    t = synth.box(2000, 80.0, seed=71)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=1.0, resume_nav=True, cd_every=2)
+    ref = world1(init, p, 7, ctx)
+    exp, exp_bk = ref.read(), ref.asas_stats()
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=2, group=g)
+        sim.step(2)
+        if r == 1:
+            c.set_candidate_capacity(16)    # also the resopairs capacity once bookkeeping runs
+        sim.step(5)
+        return sim.read(), sim.asas_stats(), sim.stats()
+
+    res = run_ranks(2, rank)
+    for r, (got, bk, st) in enumerate(res):
+        for k in exp:
+            assert np.array_equal(got[k], exp[k]), 'rank %d %s' % (r, k)
+        for f in ('confpairs_unique', 'lospairs_unique', 'confpairs_all', 'lospairs_all'):
+            assert bk[f] == exp_bk[f], (r, f)
+        assert st['steps'] == 7
+
+
+@pytest.mark.slow
+def test_sharded_100k_key_blocks_regrow(ctx):
+    """At the bench size each rank's pair keys exceed the initial all-gather
+    block (65536 words): the step aborts, the blocks regrow (keeping the
+    previous call's sets) and the counts still equal the one-rank run's."""
+    t = synth.workload('box100k')
+    init = resident.initial_state(t)
+    p = resident.params(resume_nav=True)
+    ref = resident.ResidentSim(init, p, ctx=ctx)
+    exp = []
+    for _ in range(3):
+        ref.step(1)
+        exp.append(ref.asas_stats())
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=2, group=g)
+        got = []
+        for _ in range(3):
+            sim.step(1)
+            got.append(sim.asas_stats())
+        return got
+
+    res = run_ranks(2, rank)
+    for k in range(3):
+        for r in range(2):
+            for f in ('confpairs_unique', 'lospairs_unique', 'confpairs_all', 'lospairs_all'):
+                assert res[r][k][f] == exp[k][f], (k, r, f)
+    assert exp[0]['confpairs_unique'] > 65536
+
+
+def test_sharded_standalone_detect_gather(ctx):
+    """bsa_detect on each rank's row slice, then the C2 gather to rank 1: the
+    8-tuple's arrays of the whole set, in the reference's row-major order."""
+    t = synth.global_traffic(20000, seed=73)
+    full = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx, with_dcpa=True)
+
+    def rank(r, c, g):
+        c.comm_init_group(g, r)
+        rb, re = [(0, 7000), (7000, 7001), (7001, 20000)][r]
+        statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c, row_begin=rb, row_end=re, with_dcpa=True)
+        return c.gather_pairs(root=1, with_dcpa=True)
+
+    res = run_ranks(3, rank)
+    assert res[0] is None and res[2] is None
+    for k in full:
+        assert np.array_equal(res[1][k], full[k]), k
