@@ -16,8 +16,10 @@ sim-steps/s = K / time.  Rows are partitioned, total work is fixed:
 scaling "strong".
 """
 import argparse
+import hashlib
 import json
 import os
+import platform
 import sys
 import time
 
@@ -41,16 +43,34 @@ TIMING_SAMPLE = 4            # detects per HIP-event-timed detect (bsa_set_timin
 
 def pmc_figures():
     """Per-launch memory-side bytes etc. from the committed rocprofv3 --pmc
-    passes of this bench (tools/pmc_roofline.py), or {} if absent."""
+    passes of this bench (tools/pmc_roofline.py) -- only if they were taken on
+    THIS build of libbsaccel.so (sha256 recorded by pmc_roofline.py); else {}."""
     try:
         with open(PMC_JSON) as f:
-            return json.load(f)
+            pmc = json.load(f)
+        with open(_lib.LIB_PATH, 'rb') as f:
+            sha = hashlib.sha256(f.read()).hexdigest()
     except (OSError, ValueError):
         return {}
+    return pmc if pmc.get('_meta', {}).get('lib_sha256') == sha else {}
+
+
+def cpu_model():
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or 'unknown'
 
 
 def cpu_baseline(t, rows_sample):
-    """Oracle (numpy restatement, one process) on a uniform ownship-row sample."""
+    """Oracle (numpy restatement of StateBasedCD.detect, pinned to the
+    reference) in this one process on a uniform ownship-row sample, extrapolated
+    by N / R (every row scans all N columns).  numpy ufuncs are
+    single-threaded; OpenBLAS only serves the k = 1 outer products."""
     from oracle import statebased as ocd
     n = t.ntraf
     rows = np.linspace(0, n - 1, rows_sample).astype(np.int64)
@@ -58,10 +78,54 @@ def cpu_baseline(t, rows_sample):
     ocd.detect_arrays(t, t, synth.RPZ, synth.HPZ, synth.TLOOKAHEAD, rows=rows, budget_bytes=1 << 30)
     dt = time.perf_counter() - t0
     return dict(value=rows_sample * n / dt, unit='pair-evals/s', cores=1, kind='port',
-                sample='oracle detect of %d uniformly spaced ownship rows x %d columns (%.1f s); '
-                       'numpy %s, one process, OPENBLAS_NUM_THREADS=%s, nproc=%d'
+                detect_s_extrapolated=dt * n / rows_sample,
+                sample='oracle detect of %d uniformly spaced ownship rows x %d columns (%.1f s), '
+                       'extrapolated by N/R; numpy %s, one process (single-threaded ufuncs), '
+                       'OPENBLAS_NUM_THREADS=%s, nproc=%d'
                        % (rows_sample, n, dt, np.__version__,
-                          os.environ.get('OPENBLAS_NUM_THREADS', 'unset'), os.cpu_count()))
+                          os.environ.get('OPENBLAS_NUM_THREADS', 'unset'), os.cpu_count()),
+                cpu_model=cpu_model())
+
+
+def dropin_detect_line(ctx, t, reps=3):
+    """The north-star target is stated on the drop-in ``detect()``: the whole
+    StateBasedCD.detect replacement at 100k (host arrays in, the 8-tuple with
+    Python id tuples out), wall time per component (SURVEY.md 7 iii): H2D of the
+    six state arrays, the detect up to completion, D2H of the results, building
+    the confpairs / lospairs lists.  Median of ``reps`` after one warm-up."""
+    from bluesky_amd import statebased
+    tt = []
+    for k in range(reps + 1):
+        tm = {}
+        res = statebased.detect(t, t, synth.RPZ, synth.HPZ, synth.TLOOKAHEAD, timings=tm, ctx=ctx)
+        if k:
+            tt.append(tm)
+    med = {key: float(np.median([x[key] for x in tt])) * 1e3 for key in tt[0]}
+    return dict(n=t.ntraf, ms=med, n_conf=len(res[0]), n_los=len(res[1]),
+                note='wall time of bluesky_amd.statebased.detect (ctypes -> libbsaccel); '
+                     'h2d / detect / d2h / tuples / total in ms, median of %d' % reps)
+
+
+def global1m_line(ctx, rank, world, warmup=2, steps=5):
+    """BASELINE configs[4]: 1M aircraft uniform on the globe (|lat| <= 70 deg),
+    the resident step (ASAS every step) row-sharded over the ranks -- the base
+    of the 1 -> 8 GPU curve the north star asks for (>= 6x at 1M) -- plus one
+    standalone whole-set detect's stage times (rank 0's rows only with several
+    ranks)."""
+    t = synth.workload('global1m')
+    n = t.ntraf
+    sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx,
+                               rank=rank, world=world)
+    dt = timed_steps(ctx, sim, warmup, steps)
+    tm, ts = ctx.timing_summary()
+    st = sim.stats()
+    counts = ctx.allreduce_sum([st['n_conf'], st['n_los']])
+    return dict(workload='global1m N=%d (seed 7)' % n, steps=steps, ms_per_step=dt / steps * 1e3,
+                sim_steps_per_s=steps / dt, pair_evals_per_s=float(n) * n * steps / dt,
+                n_conf=int(counts[0]), n_los=int(counts[1]),
+                kernels_ms_rank0=dict(k0_prep=tm['prep'], prefilter=tm['prefilter'], exact=tm['exact'],
+                                      k2_sort=tm['sort'], detect_total=tm['total']),
+                candidates_rank0=ts['candidates'] / max(ts['detects'], 1))
 
 
 def timed_steps(ctx, sim, warmup, steps):
@@ -136,7 +200,7 @@ def main():
     ap.add_argument('--n', type=int, default=100000)
     ap.add_argument('--workload', default='box100k', choices=['box10k', 'box100k', 'global1m'])
     ap.add_argument('--cd-every', type=int, default=1)
-    ap.add_argument('--cpu-rows', type=int, default=256)
+    ap.add_argument('--cpu-rows', type=int, default=1024)
     ap.add_argument('--no-cpu', action='store_true')
     ap.add_argument('--reuse', type=float, nargs=2, default=None, metavar=('SIGMA_H', 'SIGMA_V'),
                     help='candidate-list reuse budgets [m] (bsa_set_candidate_reuse); default off')
@@ -184,7 +248,9 @@ def main():
                 unit='TFLOP/s')
     roof['frac'] = roof['achieved'] / roof['peak']
     roof['traffic'] = (pf['hbm_read_bytes'] + pf['hbm_write_bytes']) if 'hbm_write_bytes' in pf else None
-    roof['traffic_source'] = 'profiles/pmc_latest.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch)'
+    roof['traffic_source'] = ('profiles/pmc_latest.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per '
+                              'launch), taken on this build of libbsaccel.so' if pmc else
+                              'no PMC summary for this build of libbsaccel.so')
     if 'lds_bank_conflict_rate' in pf:
         roof['lds_bank_conflict_rate'] = pf['lds_bank_conflict_rate']
     kin = pmc.get('k_sim_pilot_kin', {})
@@ -223,13 +289,26 @@ def main():
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),
                propagation=propagation, exact_fp64=exact_fp64)
+    if world > 1:   # C2: the last CD call's pair lists of all ranks to rank 0's host
+        g0 = time.perf_counter()
+        gp = sim.gather_pairs(root=0)
+        gms = float(ctx.allreduce_max([time.perf_counter() - g0])[0]) * 1e3
+        if rank == 0:
+            out['pair_gather'] = dict(ms=gms, n_conf=len(gp['ci']), n_los=len(gp['li']),
+                                      note='bsa_gather_pairs to rank 0 (counts, then rank-order blocks)')
     if not args.no_variants and not args.reuse:
         out['variants'] = variants(ctx, t, rank, world, args.warmup)
         if rank == 0:
             out['variants']['geo_matrix'] = geo_matrix_line(ctx, t)
+        if args.workload == 'box100k':
+            out['variants']['global1m'] = global1m_line(ctx, rank, world)
     if rank == 0 and world == 1 and not args.no_cpu:
         out['cpu_baseline'] = cpu_baseline(t, args.cpu_rows)
         out['speedup_vs_cpu'] = value / out['cpu_baseline']['value']
+        if not args.no_variants:
+            d = dropin_detect_line(ctx, t)
+            d['speedup_vs_cpu_detect'] = out['cpu_baseline']['detect_s_extrapolated'] * 1e3 / d['ms']['total']
+            out['dropin_detect'] = d
     if rank == 0:
         print(json.dumps(out), flush=True)
 

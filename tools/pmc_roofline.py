@@ -15,6 +15,7 @@ Per kernel and per launch (mean over dispatches):
   fp64_flops       = 64 * (2 FMA_F64 + ADD_F64 + MUL_F64 + TRANS_F64)  (per-lane ops)
   dur_ns           = kernel duration in the profiled passes (slower than unprofiled)
 """
+import hashlib
 import json
 import os
 import sys
@@ -50,6 +51,10 @@ def main():
         if all(v is not None for v in f64):
             r['fp64_flops'] = 64.0 * (2 * f64[0] + f64[1] + f64[2] + f64[3])
         res[name] = r
+    # the library these counters belong to: bench.py reports them only for the same build
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'bluesky_amd', 'libbsaccel.so')
+    with open(lib, 'rb') as f:
+        res['_meta'] = {'lib_sha256': hashlib.sha256(f.read()).hexdigest()}
     with open(out, 'w') as f:
         json.dump(res, f, indent=1, sort_keys=True)
     for k in ('k_prefilter', 'k_exact', 'k_sim_pilot_kin'):
