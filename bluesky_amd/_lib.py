@@ -152,6 +152,8 @@ SIGNATURES.update({
                                     ctypes.POINTER(SimParams)]),
     'bsa_sim_step': (ctypes.c_int, [_vp, ctypes.c_int]),
     'bsa_sim_update': (ctypes.c_int, [_vp, ctypes.POINTER(SimState)]),
+    'bsa_sim_create': (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.POINTER(SimState)]),
+    'bsa_sim_delete': (ctypes.c_int, [_vp, ctypes.c_int64, _c_i64p]),
     'bsa_sim_read': (ctypes.c_int, [_vp, ctypes.POINTER(SimOut)]),
     'bsa_sim_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_asas_stats': (ctypes.c_int, [_vp, _c_i64p]),
@@ -162,6 +164,8 @@ SIGNATURES.update({
     'bsa_sim_acdata_request': (ctypes.c_int, [_vp]),
     'bsa_set_windfield': (ctypes.c_int, [_vp, ctypes.c_int64, _c_dp, _c_dp, _c_dp, _c_dp]),
     'bsa_sim_set_limits': (ctypes.c_int, [_vp] + [_c_dp] * 6),
+    'bsa_sim_set_perf': (ctypes.c_int, [_vp, ctypes.c_int64, _c_dp, _c_i32p]),
+    'bsa_sim_read_perf': (ctypes.c_int, [_vp, _c_u8p, _c_dp]),
     'bsa_sim_acdata_poll': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(AcData)]),
 })
 
@@ -515,6 +519,29 @@ class Context:
         st = self.sim_stats()
         self._rows = (st['row_begin'], st['row_end'])   # fetch_pairs after steps: this rank's rows
 
+    def sim_set_perf(self, table=None, type_idx=None):
+        """bsa_sim_set_perf: OpenAP phase-dependent envelope + acceleration in the
+        step (``table``/``type_idx`` from bluesky_amd.perf.type_table); None = off."""
+        if table is None:
+            self.check(self.lib.bsa_sim_set_perf(self.h, 0, None, None), 'bsa_sim_set_perf')
+            return
+        tab = np.ascontiguousarray(table, dtype=np.float64)
+        idx = np.ascontiguousarray(type_idx, dtype=np.int32).ravel()
+        if tab.ndim != 2 or tab.shape[1] != 24:
+            raise ValueError('type table must be ntypes x 24')
+        if len(idx) != self.n:
+            raise ValueError('type index has length %d != %d' % (len(idx), self.n))
+        self._perf_keep = (tab, idx)
+        self.check(self.lib.bsa_sim_set_perf(self.h, tab.shape[0], ptr(tab), ptr(idx, _c_i32p)),
+                   'bsa_sim_set_perf')
+
+    def sim_read_perf(self):
+        """(phase uint8, ax float64) of this rank's rows (full-n arrays, other rows 0)."""
+        ph = np.zeros(self.n, np.uint8)
+        ax = np.zeros(self.n)
+        self.check(self.lib.bsa_sim_read_perf(self.h, ptr(ph, _c_u8p), ptr(ax)), 'bsa_sim_read_perf')
+        return ph, ax
+
     def sim_update(self, **arrays):
         """bsa_sim_update: overwrite the given full-n state arrays (SIM_STATE_FIELDS
         names) of the resident sim, keeping its ASAS bookkeeping."""
@@ -527,6 +554,29 @@ class Context:
                 raise ValueError('sim state %s has length %d != %d' % (k, len(a), self.n))
         st = SimState(**{k: ptr(a) for k, a in keep.items()})
         self.check(self.lib.bsa_sim_update(self.h, ctypes.byref(st)), 'bsa_sim_update')
+
+    def sim_create(self, state):
+        """bsa_sim_create: append aircraft (every SIM_STATE_FIELDS array, m long);
+        they take indices n..n+m-1 (Traffic.create, traffic.py:192-312)."""
+        m = len(state['lat'])
+        keep = {k: f64(state[k]) for k in SIM_STATE_FIELDS}
+        for k, a in keep.items():
+            if len(a) != m:
+                raise ValueError('created state %s has length %d != %d' % (k, len(a), m))
+        st = SimState(**{k: ptr(a) for k, a in keep.items()})
+        self.gen += 1
+        self.check(self.lib.bsa_sim_create(self.h, m, ctypes.byref(st)), 'bsa_sim_create')
+        self.n += m
+        self._rows = (0, self.n)
+
+    def sim_delete(self, idx):
+        """bsa_sim_delete: remove aircraft ``idx``; the rest shift down in order
+        (Traffic.delete, traffic.py:364-378)."""
+        d = np.unique(np.asarray(idx, dtype=np.int64).ravel())
+        self.gen += 1
+        self.check(self.lib.bsa_sim_delete(self.h, len(d), ptr(d, _c_i64p)), 'bsa_sim_delete')
+        self.n -= len(d)
+        self._rows = (0, self.n)
 
     def sim_step(self, nsteps=1):
         self.gen += 1
@@ -557,7 +607,8 @@ class Context:
                     confpairs_all=opt(v[3]), lospairs_all=opt(v[4]), active=int(v[5]))
 
     def sim_resopairs(self):
-        """This rank's resopairs as (idx1, idx2) int32 arrays, idx1-major."""
+        """This rank's resopairs as (idx1, idx2) int32 arrays, idx1-major; idx2 is
+        -1 for an intruder deleted since the last CD call (bsa_sim_delete)."""
         cnt = np.zeros(1, np.int64)
         a = b = np.empty(0, np.int32)
         while True:

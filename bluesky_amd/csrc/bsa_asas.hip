@@ -8,7 +8,7 @@
 //                new confpairs (K2 output, sorted), evaluate ResumeNav's
 //                past-CPA / horizontal-LoS / bouncing test per pair
 //                (asas.py:424-452), count the kept pairs
-//   scan         kept counts -> next CSR
+//   scan         kept counts -> next CSR (single-pass scan_excl)
 //   k_bk_check   next CSR larger than its buffer -> gate bit 1: the step
 //                aborts before MVP touches asas state (all ranks, through the
 //                gate all-reduce); the host grows the buffer and retries
@@ -63,8 +63,11 @@ __device__ __forceinline__ bool bk_aborted(const unsigned long long *gate, const
   return sticky[0] != 0 || gate[0] != 0;
 }
 
-// ResumeNav's decision for resopair (i, j), asas.py:424-452
+// ResumeNav's decision for resopair (i, j), asas.py:424-452.  j == kDangling:
+// the intruder was deleted (bsa_sim_delete) -- idx2 < 0 switches ASAS off for
+// the ownship and drops the pair (asas.py:454-468)
 __device__ __forceinline__ bool bk_keep(const BkIn &in, int i, int j) {
+  if ((unsigned)j == kDangling) return false;
   const double re = 6371000.;
   const double d0 = re * (((in.lon[j] - in.lon[i]) * kD2R) * cos(0.5 * ((in.lat[j] + in.lat[i]) * kD2R)));
   const double d1 = re * ((in.lat[j] - in.lat[i]) * kD2R);
@@ -379,13 +382,7 @@ int bk_count(Ctx *c, const BkDev &d) {
   const BkIn in = bk_in(c, d);
   hipLaunchKernelGGL(k_bk_count, dim3((unsigned)((nrows + 1 + 255) / 256)), dim3(256), 0, c->stream, in);
   BSA_HIP(c, hipGetLastError());
-  size_t tmp = 0;
-  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (const unsigned *)c->bk_cnt.p,
-                                              (unsigned *)c->bk_nptr.p, (int)(nrows + 1), c->stream));
-  if (!ensure(c, c->bk_tmp, std::max<size_t>(tmp, 16), "bookkeeping scan scratch")) return -1;
-  tmp = c->bk_tmp.bytes;
-  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->bk_tmp.p, tmp, (const unsigned *)c->bk_cnt.p,
-                                              (unsigned *)c->bk_nptr.p, (int)(nrows + 1), c->stream));
+  if (scan_excl(c, (const unsigned *)c->bk_cnt.p, (unsigned *)c->bk_nptr.p, (int)(nrows + 1))) return -1;
   hipLaunchKernelGGL(k_bk_check, dim3(1), dim3(1), 0, c->stream, (int)nrows, (const unsigned *)c->bk_nptr.p,
                      ncap, d.gate, (const unsigned *)d.sticky, d.demand);
   BSA_HIP(c, hipGetLastError());

@@ -259,7 +259,8 @@ struct ReuseParams {
 };
 constexpr double kRefineChord = 0.03;  // the refine keeps (without refining) pairs with a longer chord
 
-constexpr int kWorkShards = 8;   // one dequeue counter per XCD group
+constexpr int kWorkShards = 32;  // dequeue counters (4 per XCD group): a returning atomic on one
+                                 // word saturates at ~88 dequeues/us (MI355X_MICROARCH 'dequeue')
 constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
 
 // Per-detect state to zero (k_zero, or fused into k_prep_cols: cnt != nullptr)
@@ -275,9 +276,10 @@ __device__ __forceinline__ bool list_word(int k);
 __device__ __forceinline__ void zero_state(const ZeroArgs &z, int t, int nt) {
   constexpr int kWords = (int)(sizeof(Counters) / 8);
   constexpr int kTilesWord = (int)(offsetof(Counters, tiles) / 8);
+  constexpr int kNearWord = (int)(offsetof(Counters, tiles_near) / 8);
   const int m = max(max(2 * (z.nrows + 1), kWorkShards * kWorkStride), kWords);
   for (int k = t; k < m; k += nt) {
-    if (k < kWords && (z.full || k != kTilesWord) && !(z.keep && list_word(k)))
+    if (k < kWords && (z.full || (k != kTilesWord && k != kNearWord)) && !(z.keep && list_word(k)))
       reinterpret_cast<unsigned long long *>(z.cnt)[k] = 0;
     if (k < kWorkShards * kWorkStride) z.work[k] = 0;
     if (k < z.nrows) {
@@ -449,7 +451,8 @@ __device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b)
 __device__ __forceinline__ bool list_word(int k) {
   constexpr int kCand = (int)(offsetof(Counters, cand) / 8), kTiles = (int)(offsetof(Counters, tiles) / 8);
   constexpr int kGroups = (int)(offsetof(Counters, groups) / 8), kStamp = (int)(offsetof(Counters, stamp) / 8);
-  return k == kCand || k == kTiles || k == kGroups || k >= kStamp;
+  constexpr int kNear = (int)(offsetof(Counters, tiles_near) / 8);
+  return k == kCand || k == kTiles || k == kNear || k == kGroups || k >= kStamp;
 }
 
 __device__ __forceinline__ float xmin(float v, int o) { return fminf(v, __shfl_xor(v, o)); }
@@ -544,6 +547,18 @@ __global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restric
   tile_boxes(cnt, blockIdx.x, P, gb, sbox, gbox, tbox);
 }
 
+// inclusive wave64 prefix sum on the DPP crossbar (no LDS round trips):
+// row_shr 1/2/4/8 within each 16-lane row, then row_bcast 15 / 31 across rows
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned x) {
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
 // ------------------------------------------------------------------ K0d tile pairs
 __device__ __forceinline__ float gap(float alo, float ahi, float blo, float bhi) {
   return fmaxf(0.f, fmaxf(alo - bhi, blo - ahi));
@@ -561,45 +576,69 @@ __device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileB
   return !(d2 >= st * st) && (b.vlo < a.vhi) && (b.vhi > a.vlo);
 }
 
-// One atomic per 1024-thread workgroup on the shared list counter (a
-// returning atomic per wave serialised ~600 of them on one address: 6.8 us).
+// K0d: the kept tile pairs, listed in two classes: pairs whose boxes overlap
+// ("near": a row tile against itself and its neighbours, the costly items)
+// from the front of the list, the others from its back (cap - 1 - k), so the
+// sweep dequeues the near pairs first -- longest items first keeps the tail of
+// the dynamic schedule short (measured -5 us at box100k).  Each thread
+// classifies kTPPer consecutive candidate pairs; one returning atomic per
+// class and 1024-thread workgroup (a returning atomic on one word saturates
+// at ~88 per us, MI355X_MICROARCH 'dequeue').
 constexpr int kTPThreads = 1024;
+constexpr int kTPPerMax = 8;  // candidate pairs per thread (fewer when there are few: parallelism)
+__device__ __forceinline__ uint2 tile_at(const uint2 *__restrict__ list, unsigned long long k,
+                                         unsigned long long near, unsigned long long cap) {
+  return list[k < near ? k : cap - 1 - (k - near)];
+}
 __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, const TileBox *__restrict__ rb,
                                                           const TileBox *__restrict__ cb, int noprune,
-                                                          uint2 *__restrict__ out,
-                                                          unsigned long long *__restrict__ count,
+                                                          uint2 *__restrict__ out, unsigned long long cap,
+                                                          Counters *__restrict__ cnt, int kTPPer,
                                                           const unsigned *__restrict__ build) {
   if (build && !build[0]) return;
-  __shared__ unsigned wpre[kTPThreads / 64];
-  __shared__ unsigned long long bbase;
-  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = id < (long long)nrt * nct;
-  bool keep = false;
-  int rt = 0, ct = 0;
-  if (valid) {
-    rt = (int)(id / nct);
-    ct = (int)(id % nct);
-    keep = noprune ? true : boxes_may_interact(rb[rt], cb[ct]);
+  __shared__ unsigned wpre[2][kTPThreads / 64];
+  __shared__ unsigned long long bbase[2];
+  const long long total = (long long)nrt * nct;
+  const long long id0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * kTPPer;
+  unsigned kn = 0, kf = 0;  // bit q: candidate id0 + q kept as near / far
+  for (int q = 0; q < kTPPer; ++q) {
+    const long long id = id0 + q;
+    if (id >= total) break;
+    const int rt = (int)(id / nct), ct = (int)(id % nct);
+    const TileBox a = rb[rt], b = cb[ct];
+    if (!(noprune || boxes_may_interact(a, b))) continue;
+    const bool near = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]) == 0.f &&
+                      gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]) == 0.f &&
+                      gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]) == 0.f;
+    if (near) kn |= 1u << q; else kf |= 1u << q;
   }
-  const unsigned long long m = __ballot(keep);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) wpre[w] = (unsigned)__popcll(m);
+  const unsigned cn = (unsigned)__popc(kn), cf = (unsigned)__popc(kf);
+  const unsigned xn = wave_incl_scan(cn), xf = wave_incl_scan(cf);
+  if (lane == 63) {
+    wpre[0][w] = xn;
+    wpre[1][w] = xf;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 2) {
     unsigned run = 0;
     for (int q = 0; q < kTPThreads / 64; ++q) {
-      const unsigned v = wpre[q];
-      wpre[q] = run;
+      const unsigned v = wpre[threadIdx.x][q];
+      wpre[threadIdx.x][q] = run;
       run += v;
     }
-    bbase = run ? atomicAdd(count, (unsigned long long)run) : 0ull;
+    unsigned long long *ctr = threadIdx.x == 0 ? &cnt->tiles_near : &cnt->pad[0];
+    bbase[threadIdx.x] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+    if (run) atomicAdd(&cnt->tiles, (unsigned long long)run);
   }
   __syncthreads();
-  if (keep) {
-    const unsigned pos = (unsigned)(bbase + wpre[w] +
-                                    __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u)));
-    out[pos] = make_uint2((unsigned)rt, (unsigned)ct);
+  unsigned pn = (unsigned)bbase[0] + wpre[0][w] + xn - cn;
+  unsigned pf = (unsigned)bbase[1] + wpre[1][w] + xf - cf;
+  for (int q = 0; q < kTPPer; ++q) {
+    const long long id = id0 + q;
+    const uint2 v = make_uint2((unsigned)(id / nct), (unsigned)(id % nct));
+    if (kn >> q & 1u) out[pn++] = v;
+    if (kf >> q & 1u) out[cap - 1 - pf++] = v;
   }
 }
 
@@ -630,18 +669,6 @@ __device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long 
 __device__ __forceinline__ unsigned lane_prefix(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
-// inclusive wave64 prefix sum on the DPP crossbar (no LDS round trips):
-// row_shr 1/2/4/8 within each 16-lane row, then row_bcast 15 / 31 across rows
-__device__ __forceinline__ unsigned wave_incl_scan(unsigned x) {
-  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);
-  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);
-  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);
-  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);
-  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
-  x += (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-  return x;
-}
-
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 // stage 2: conservative closest-approach refine of one (row, column) pair.
@@ -694,26 +721,67 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
   return !(qe * qe + qn * qn > prm.lim2);
 }
 
-constexpr int PF_Q1 = 1024;  // per-wave stage-1 queue: u16 (row_local << 6 | column slot)
+#ifndef PF_Q1
+#define PF_Q1 512  // per-wave stage-1 queue: u16 (row_local << 6 | column slot)
+#endif
 constexpr int PF_Q2 = 128;   // per-wave stage-2 queue: uint2 (sorted row, sorted column)
 constexpr int PF_WROWS = 64;   // rows per wave (one per lane)
 constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
+// Work distribution knob of the sweep (BSA_PF_SHARDS overrides it for
+// measurements; results never depend on it)
+struct PfKnobs {
+  int shards;  // dequeue counters in use (power of two <= kWorkShards)
+};
 constexpr int PF_BLOCKS_PER_CU = 5;  // LDS-limited (~7.8 KB per wave) and BSA_PF_WAVES_PER_EU
 constexpr int kSubsPerTile = kTile / kSub;
 static_assert(kSubsPerTile == 64, "one sub-group box per lane");
 constexpr int kSubsPerBatch = 64 / kSub;  // sub-groups per 64-column batch
 static_assert(PF_Q1 >= 64 * 8, "one 8-column chunk of survivors fits the stage-1 queue");
 
-__device__ __forceinline__ void pf_flush(uint2 *q, unsigned qn, int lane, uint2 *__restrict__ cand,
-                                         unsigned long long *__restrict__ count,
-                                         unsigned long long cap) {
-  __builtin_amdgcn_wave_barrier();
-  unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd(count, (unsigned long long)qn);
-  base = wave_bcast_u64(base);
-  for (unsigned k = lane; k < qn; k += 64)
-    if (base + k < cap) cand[base + k] = q[k];
-  __builtin_amdgcn_wave_barrier();
+// K0e: for every work item (tile pair, 64-row slice) the 64-bit mask of the
+// column tile's 8-column sub-groups whose boxes may interact with the slice's
+// row box (boxes_may_interact: the stage-1 test applied to box gaps), so the
+// sweep starts an item with one scalar load instead of a chain of dependent
+// loads (tile pair -> row box -> 64 sub-group boxes, 3 KB per item).  One wave
+// per tile pair: its 64 sub-group boxes are loaded once (one per lane) and
+// tested against the 8 row-slice boxes (lanes 0..7, all loads up front).
+__global__ __launch_bounds__(256) void k_items(int nrows, int ncols, const TileBox *__restrict__ gbox_r,
+                                               const TileBox *__restrict__ sbox_c, const uint2 *__restrict__ tiles,
+                                               unsigned long long tcap, const Counters *__restrict__ cnt, int noprune,
+                                               unsigned long long *__restrict__ masks,
+                                               const unsigned *__restrict__ build) {
+  if (build && !build[0]) return;
+  const unsigned long long ntiles = cnt->tiles, near = cnt->tiles_near;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long nw = ((unsigned long long)gridDim.x * blockDim.x) >> 6;
+  for (unsigned long long tp = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; tp < ntiles;
+       tp += nw) {
+    const uint2 rc = tile_at(tiles, tp, near, tcap);
+    const int cbase = (int)rc.y * kTile;
+    const int nsub = min(kSubsPerTile, (ncols - cbase + kSub - 1) / kSub);
+    const bool have = lane < nsub;
+    TileBox sb, rbl;
+    if (have) sb = sbox_c[cbase / kSub + lane];
+    const int nslice = min(PF_ITEMS_PER_TILE, (nrows - (int)rc.x * kTile + PF_WROWS - 1) / PF_WROWS);
+    if (lane < nslice) rbl = gbox_r[((int)rc.x * kTile) / kGroup + lane];
+    for (int sl = 0; sl < PF_ITEMS_PER_TILE; ++sl) {
+      bool gk = false;
+      if (sl < nslice) {
+        TileBox a;
+        auto bc = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), sl)); };
+        for (int q = 0; q < 3; ++q) {
+          a.lo[q] = bc(rbl.lo[q]);
+          a.hi[q] = bc(rbl.hi[q]);
+        }
+        a.vlo = bc(rbl.vlo);
+        a.vhi = bc(rbl.vhi);
+        a.smax = bc(rbl.smax);
+        gk = have && (noprune || boxes_may_interact(a, sb));
+      }
+      const unsigned long long m = __ballot(gk);
+      if (lane == 0) masks[tp * PF_ITEMS_PER_TILE + sl] = m;
+    }
+  }
 }
 
 // Diagnostic phase timers (build with -DBSA_PF_STAMPS; `make stamps`):
@@ -771,12 +839,12 @@ template <bool NOPRUNE>
 __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, const float4 *__restrict__ pprow, int nrows,
     const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, const float4 *__restrict__ ppcol, int ncols,
-    const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ sbox_c,
-    const uint2 *__restrict__ tiles, Counters *__restrict__ cnt,
+    const unsigned long long *__restrict__ masks, const uint2 *__restrict__ tiles, unsigned long long tcap,
+    Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
-    uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build) {
+    uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
-  __shared__ uint2 q2s[PF_WAVES][PF_Q2];
+  __shared__ uint2 q2s[PF_WAVES][2][PF_Q2];  // double-buffered: one fills while the other's flush atomic flies
   __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
   __shared__ float4 cen[PF_WAVES][32];      //                      e e' n n'     (stage 1)
   __shared__ float4 clh[PF_WAVES][32];      //                      lo lo' hi hi' (stage 1)
@@ -786,9 +854,12 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:       u v vs alt    (refine)
   if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const unsigned long long ntiles = cnt->tiles;
+  const unsigned long long ntiles = cnt->tiles, near = cnt->tiles_near;
   unsigned short *q1 = q1s[w];
-  uint2 *q2 = q2s[w];
+  unsigned fb = 0;           // fill buffer of q2 (wave-uniform)
+  uint2 *q2 = q2s[w][0];
+  unsigned long long pbase = 0;  // pending flush: lane 0's atomic result, consumed one flush later
+  unsigned pn = 0;               // entries of the pending buffer (wave-uniform)
   float *ska = (float *)cka[w];
   float *sen = (float *)cen[w];
   float *slh = (float *)clh[w];
@@ -799,19 +870,45 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   unsigned n2 = 0;        // wave-uniform
   unsigned subs = 0;      // 8-column sub-groups swept by this wave (for the roofline)
   const float qnan = __builtin_nanf("");
-  // Dynamic work distribution: an item is one (tile pair, 64-row slice);
-  // each wave dequeues items from the counter of its XCD group (blockIdx % 8)
-  // so no single word takes every dequeue (MI355X_MICROARCH 'dequeue').
-  // (Giving each XCD a contiguous eighth of the tile pairs for L2 locality
-  // measured slower: 231 vs 224 us at box100k.)
+  // Dynamic work distribution: an item is one (tile pair, 64-row slice); each
+  // wave dequeues items from the counter of its shard (blockIdx % shards,
+  // 128 B apart; a returning atomic on one word saturates at ~88 per us).
+  // Near tile pairs (the costly ones) come first in the list.  An item's
+  // sub-group mask comes from K0e (k_items): one scalar load, no dependent
+  // box loads.  (Measured slower: claiming the next item ahead (+20 us: the
+  // claimed items lengthen the tail, each wave sweeps only ~8 items), several
+  // items per dequeue, and streaming several column tiles of a slice per item
+  // (fewer, longer items: the near tiles of a row group end up serialised on
+  // one wave).)
   const unsigned long long nitems = ntiles * PF_ITEMS_PER_TILE;
-  const unsigned shard = blockIdx.x & (kWorkShards - 1);
+  const unsigned shard = blockIdx.x & (kn.shards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
   // its own counter (spreads the flush atomics over kCandShards addresses)
   const unsigned long long ccap = cap / kCandShards;
   uint2 *ccand = cand + (unsigned long long)(shard % kCandShards) * ccap;
   unsigned long long *cshard = &cnt->cshard[shard % kCandShards][0];
+  // q2 flush, double-buffered: reserve room for the fill buffer with a
+  // returning atomic and write the PREVIOUS buffer out to the room its atomic
+  // (issued one flush earlier) returned -- no wave waits on a fresh atomic
+  auto write_pending = [&]() {
+    if (!pn) return;
+    const unsigned long long base = wave_bcast_u64(pbase);
+    const uint2 *pq = q2s[w][fb ^ 1];
+    for (unsigned k = lane; k < pn; k += 64)
+      if (base + k < ccap) ccand[base + k] = pq[k];
+    pn = 0;
+  };
+  auto flush2 = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    write_pending();
+    if (lane == 0) pbase = atomicAdd(cshard, (unsigned long long)n2);
+    pn = n2;
+    fb ^= 1u;
+    q2 = q2s[w][fb];
+    n2 = 0;
+    __builtin_amdgcn_wave_barrier();
+  };
 #ifdef BSA_PF_STAMPS
   unsigned long long st_acc[4] = {0, 0, 0, 0};
   unsigned long long st_last = __builtin_amdgcn_s_memtime();
@@ -821,19 +918,17 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     {
       unsigned long long m0 = 0;
       if (lane == 0) m0 = atomicAdd(wq, 1ull);
-      item = wave_bcast_u64(m0) * kWorkShards + shard;
+      item = wave_bcast_u64(m0) * kn.shards + shard;
     }
     if (item >= nitems) break;
     do {  // one item; `break` ends it
-    const uint2 rc = tiles[item / PF_ITEMS_PER_TILE];
+    const unsigned long long tp = item / PF_ITEMS_PER_TILE;
+    const uint2 rc = tile_at(tiles, tp, near, tcap);
     const int rbase = (int)rc.x * kTile + (int)(item % PF_ITEMS_PER_TILE) * PF_WROWS;
     if (rbase >= nrows) break;
     const int cbase = (int)rc.y * kTile;
-    // column sub-groups of this tile that may interact with the wave's row box
-    const int nsub = min(kSubsPerTile, (ncols - cbase + kSub - 1) / kSub);
-    const TileBox rbx = gbox_r[rbase / kGroup];
-    const bool gk = lane < nsub && (NOPRUNE || boxes_may_interact(rbx, sbox_c[cbase / kSub + lane]));
-    unsigned long long gm = __ballot(gk);
+    // column sub-groups of this tile that may interact with the wave's row box (K0e)
+    unsigned long long gm = masks[item];
     if (!gm) break;
     subs += (unsigned)__popcll(gm);
 
@@ -954,8 +1049,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
           n2 = __builtin_amdgcn_readfirstlane(n2 + (unsigned)__popcll(mk));
           if (n2 > (unsigned)(PF_Q2 - 64)) {
             PF_STAMP(2);
-            pf_flush(q2, n2, lane, ccand, cshard, ccap);
-            n2 = 0;
+            flush2();
             PF_STAMP(3);
           }
         }
@@ -1003,7 +1097,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         colmask = __ballot(jn >= 0);
       }
       gm = drop_batch(gm);
-      if (gm) {  // prefetch the next batch while this one is swept
+      const bool more = gm != 0;
+      if (more) {  // prefetch the next batch while this one is swept
         jn = batch_col(gm);
         load_col(jn, nx, nv, np);
       }
@@ -1051,18 +1146,125 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       // refine this batch's survivors while its columns are staged
       if (n1) drain();
       PF_STAMP(1);
-      if (!gm) break;
+      if (!more) break;
     }
     } while (0);
   }
   PF_STAMP(0);
-  if (n2) pf_flush(q2, n2, lane, ccand, cshard, ccap);
+  if (n2) flush2();
+  write_pending();
   if (lane == 0 && subs) atomicAdd(&cnt->groups, (unsigned long long)subs);
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
   if (lane == 0)
     for (int k = 0; k < 4; ++k) atomicAdd(&cnt->stamp[k], st_acc[k]);
 #endif
+}
+
+
+// ------------------------------------------------------------------ single-pass scan
+// Exclusive prefix sum of n unsigned words in ONE launch (replaces hipcub's
+// three: look-back init + scan, ~16 us per detect at 100k): decoupled
+// look-back over 8192-word tiles.  Tiles are numbered by a ticket (a running
+// device counter; the host knows its base), so a tile only ever waits on tiles
+// that already started.  Tile status words carry the launch's epoch, so they
+// need no zeroing between launches: {epoch:30 | flag:2 | value:32}, flag 1 =
+// the tile's own total, 2 = inclusive prefix through the tile.
+constexpr int kScanThreads = 1024, kScanItems = 8, kScanTile = kScanThreads * kScanItems;
+__device__ __forceinline__ unsigned long long scan_word(unsigned epoch, unsigned flag, unsigned v) {
+  return ((unsigned long long)(epoch & 0x3fffffffu) << 34) | ((unsigned long long)flag << 32) | v;
+}
+__global__ __launch_bounds__(kScanThreads) void k_scan_excl(const unsigned *__restrict__ in, unsigned *__restrict__ out,
+                                                            int n, unsigned long long *__restrict__ ticket,
+                                                            unsigned long long base,
+                                                            unsigned long long *__restrict__ status, unsigned epoch) {
+  __shared__ unsigned wsum[kScanThreads / 64];
+  __shared__ unsigned s_tile, s_excl;
+  if (threadIdx.x == 0) s_tile = (unsigned)(atomicAdd(ticket, 1ull) - base);
+  __syncthreads();
+  const unsigned tile = s_tile;
+  const long long i0 = (long long)tile * kScanTile + (long long)threadIdx.x * kScanItems;
+  unsigned v[kScanItems], tsum = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    v[k] = (i0 + k < n) ? in[i0 + k] : 0u;
+    tsum += v[k];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned x = wave_incl_scan(tsum);
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  // wave 0: tile total, then a wave-wide look-back (64 predecessors per round:
+  // the nearest inclusive prefix, plus the aggregates after it)
+  if (w == 0) {
+    const unsigned wv = lane < kScanThreads / 64 ? wsum[lane] : 0u;
+    const unsigned wx = wave_incl_scan(wv);
+    if (lane < kScanThreads / 64) wsum[lane] = wx - wv;  // exclusive per-wave offsets
+    const unsigned total = __builtin_amdgcn_readlane(wx, 63);
+    unsigned excl = 0;
+    if (tile == 0) {
+      if (lane == 0)
+        __hip_atomic_store(&status[0], scan_word(epoch, 2, total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0)
+        __hip_atomic_store(&status[tile], scan_word(epoch, 1, total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      int top = (int)tile - 1;  // highest predecessor not yet summed
+      for (;;) {
+        const int j = top - lane;
+        unsigned long long st = 0;
+        if (j >= 0) st = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned flag = ((unsigned)(st >> 34) == (epoch & 0x3fffffffu)) ? ((unsigned)(st >> 32) & 3u) : 0u;
+        // lanes past tile 0 count as "inclusive 0"
+        const bool incl = j < 0 || flag == 2, ready = j < 0 || flag != 0;
+        const unsigned long long mi = __ballot(incl), mr = __ballot(ready);
+        // first lane (nearest predecessor) holding an inclusive prefix, or 64
+        const int fi = mi ? __builtin_ctzll(mi) : 64;
+        // every lane up to fi must be ready, else spin on this window
+        const unsigned long long need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
+        if ((mr & need) != need) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        unsigned part = (lane <= fi && j >= 0) ? (unsigned)st : 0u;
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        excl += part;
+        if (fi < 64) break;
+        top -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[tile], scan_word(epoch, 2, excl + total), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  unsigned run = s_excl + wsum[w] + x - tsum;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    if (i0 + k < n) out[i0 + k] = run;
+    run += v[k];
+  }
+}
+
+int scan_excl(Ctx *c, const unsigned *in, unsigned *out, int n) {
+  if (n <= 0) return 0;
+  const unsigned tiles = (unsigned)((n + kScanTile - 1) / kScanTile);
+  const size_t had = c->scan_ws.bytes;
+  if (!ensure_keep(c, c->scan_ws, 8 * (size_t)(1 + tiles), "scan tile status")) return -1;
+  if (c->scan_ws.bytes != had) c->scan_ready = false;  // grown: the new words are uninitialised
+  if (!c->scan_ready) {  // ticket counter and tile status start at 0
+    BSA_HIP(c, hipMemsetAsync(c->scan_ws.p, 0, c->scan_ws.bytes, c->stream));
+    c->scan_ready = true;
+    c->scan_tickets = 0;
+    c->scan_epoch = 0;
+  }
+  const unsigned epoch = ++c->scan_epoch;  // never 0: fresh (zeroed) status words are never ready
+  unsigned long long *ws = (unsigned long long *)c->scan_ws.p;
+  hipLaunchKernelGGL(k_scan_excl, dim3(tiles), dim3(kScanThreads), 0, c->stream, in, out, n, ws, c->scan_tickets,
+                     ws + 1, epoch);
+  BSA_HIP(c, hipGetLastError());
+  c->scan_tickets += tiles;
+  return 0;
 }
 
 // ------------------------------------------------------------------ K1b exact
@@ -1148,6 +1350,8 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
   return o;
 }
 
+constexpr int kPayStride = 6;  // doubles per candidate record (cpay): key, qdr, dist, tcpa, tin, dcpa
+
 // Results are stored per candidate (flag, key, payload) rather than appended
 // to a shared list: appending needs an atomic with return on ONE counter per
 // wave, which serialises at ~88/us (MI355X_MICROARCH 'dequeue') and cost
@@ -1157,8 +1361,7 @@ __global__ __launch_bounds__(256) void k_exact(
     const unsigned *__restrict__ perm_r, const unsigned *__restrict__ perm_c,
     const uint2 *__restrict__ cand, const Counters *__restrict__ cnt,
     unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
-    unsigned char *__restrict__ cflag, unsigned long long *__restrict__ ckey,
-    double *__restrict__ cpay, unsigned char *__restrict__ inconf,
+    unsigned char *__restrict__ cflag, double *__restrict__ cpay, unsigned char *__restrict__ inconf,
     unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int kwik,
     unsigned *__restrict__ rctl, const Snap *__restrict__ snap_cur, Snap *__restrict__ snap_build, int nsnap) {
   if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
@@ -1186,13 +1389,15 @@ __global__ __launch_bounds__(256) void k_exact(
                                 : eval_pair<false>(R[p.x], C[p.y], rpz, hpz, tla);
       flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
       const int row = (int)oi - rb;
-      if (flag) ckey[idx] = ((unsigned long long)oi << 32) | oj;
+      // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
+      double *rec = cpay + idx * kPayStride;
+      if (flag) rec[0] = __longlong_as_double((long long)(((unsigned long long)oi << 32) | oj));
       if (o.conf) {
-        cpay[0 * cap + idx] = o.qdr;
-        cpay[1 * cap + idx] = o.dist;
-        cpay[2 * cap + idx] = o.tcpa;
-        cpay[3 * cap + idx] = o.tin;
-        cpay[4 * cap + idx] = o.dcpa;
+        rec[1] = o.qdr;
+        rec[2] = o.dist;
+        rec[3] = o.tcpa;
+        rec[4] = o.tin;
+        rec[5] = o.dcpa;
         inconf[row] = 1;
         // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
         // positive tcpa can raise it, and positive doubles order as integers.
@@ -1217,7 +1422,7 @@ __global__ __launch_bounds__(256) void k_exact(
 // when the candidate list overflowed: the caller retries with more room.
 __global__ __launch_bounds__(256) void k_scatter(const Counters *__restrict__ cnt, unsigned long long cap,
                                                  int rb, int nrows, const unsigned char *__restrict__ cflag,
-                                                 const unsigned long long *__restrict__ ckey,
+                                                 const double *__restrict__ cpay,
                                                  const unsigned *__restrict__ rowoff,
                                                  unsigned *__restrict__ rowcnt,
                                                  unsigned long long *__restrict__ skey,
@@ -1232,7 +1437,7 @@ __global__ __launch_bounds__(256) void k_scatter(const Counters *__restrict__ cn
        k += stride) {
     const unsigned char f = cflag[k];
     if (!f) continue;
-    const unsigned long long key = ckey[k];
+    const unsigned long long key = (unsigned long long)__double_as_longlong(cpay[k * kPayStride]);
     const int row = (int)(key >> 32) - rb;
     if (f & 1) {
       const unsigned pos = rowoff[row] + atomicSub(&rowcnt[row], 1u) - 1u;
@@ -1318,7 +1523,7 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
       double pay[5];
 #pragma unroll
       for (int f = 0; f < 5; ++f) {
-        pay[f] = cpay[f * cap + v];
+        pay[f] = cpay[(size_t)v * kPayStride + 1 + f];
         out[(size_t)f * P + pos] = pay[f];
       }
       if (mf.pdv) {  // resident step: MVP's per-pair vector (MVP.py:33-56) for k_mvp_row
@@ -1543,8 +1748,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const unsigned *perm_c = (const unsigned *)c->perm_c.p;
 
   // ---- buffers sized by the candidate capacity (every pair list <= candidates)
-  if (!ensure(c, c->cflag, cap, "candidate flags") || !ensure(c, c->ckey, cap * 8, "candidate keys") ||
-      !ensure(c, c->cpay, cap * 5 * 8, "candidate payload") ||
+  if (!ensure(c, c->cflag, cap, "candidate flags") ||
+      !ensure(c, c->cpay, cap * kPayStride * 8, "candidate records") ||
       !ensure(c, c->ckey2, cap * 8, "conflict keys") || !ensure(c, c->cval2, cap * 4, "conflict slots") ||
       !ensure(c, c->lkey2, cap * 8, "los keys") || !ensure(c, c->out_ci, cap * 4, "ci") ||
       !ensure(c, c->out_cj, cap * 4, "cj") || !ensure(c, c->out_pay, cap * 5 * 8, "conflict outputs") ||
@@ -1581,7 +1786,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (!ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
       !ensure(c, c->gbox_c, ngc * sizeof(TileBox), "column group boxes") ||
       !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
-      !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
+      !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs") ||
+      !ensure(c, c->itemmask, (size_t)ntp * PF_ITEMS_PER_TILE * 8, "item masks"))
     return -1;
   FusedBoxes fb{nullptr, nullptr, nullptr};
   ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -1607,9 +1813,17 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (reuse)
     hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
                        (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
-  hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + kTPThreads - 1) / kTPThreads)), dim3(kTPThreads), 0,
-                     c->stream, nrt, nct,
-                     tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p, &dcnt->tiles, build);
+  // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
+  const int tpper = (int)std::min<long long>(kTPPerMax, std::max<long long>(1, ntp / (1024LL * kTPThreads)));
+  hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + (long long)kTPThreads * tpper - 1) / ((long long)kTPThreads * tpper))),
+                     dim3(kTPThreads), 0, c->stream, nrt, nct, tbox_r, (const TileBox *)c->tbox_c.p, noprune,
+                     (uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt, tpper, build);
+  BSA_HIP(c, hipGetLastError());
+  // K0e: per (tile pair, 64-row slice) the mask of interacting column sub-groups
+  hipLaunchKernelGGL(k_items, dim3((unsigned)std::min<long long>(2048, (ntp + 3) / 4)), dim3(256), 0,
+                     c->stream, (int)nrows, (int)n, gbox_r, (const TileBox *)c->sbox_c.p,
+                     (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, (const Counters *)dcnt, noprune,
+                     (unsigned long long *)c->itemmask.p, build);
   BSA_HIP(c, hipGetLastError());
   if (mark(1)) return -1;
 
@@ -1618,27 +1832,33 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : lim * lim};
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
+  static const PfKnobs kn = [] {
+    const char *v = getenv("BSA_PF_SHARDS");
+    PfKnobs z{v ? atoi(v) : kWorkShards};
+    if (z.shards < 1 || z.shards > kWorkShards || (z.shards & (z.shards - 1))) z.shards = kWorkShards;
+    return z;
+  }();
   const unsigned pf_grid = (unsigned)std::max<long long>(
       kWorkShards, std::min<long long>(ntp * PF_ITEMS_PER_TILE / PF_WAVES + 1, 256 * PF_BLOCKS_PER_CU));
   if (noprune)
     hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
-                       (const float4 *)c->pfpcol.p, (int)n, gbox_r,
-                       (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build);
+                       (const float4 *)c->pfpcol.p, (int)n, (const unsigned long long *)c->itemmask.p,
+                       (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt,
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
-                       (const float4 *)c->pfpcol.p, (int)n, gbox_r,
-                       (const TileBox *)c->sbox_c.p, (const uint2 *)c->tilepairs.p, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build);
+                       (const float4 *)c->pfpcol.p, (int)n, (const unsigned long long *)c->itemmask.p,
+                       (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt,
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count, one
   // resident round (4 workgroups per CU at its register budget)
   hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
                      perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, cap, rpz, hpz, tla, (int)rb, (int)nrows,
-                     (unsigned char *)c->cflag.p, (unsigned long long *)c->ckey.p, (double *)c->cpay.p,
+                     (unsigned char *)c->cflag.p, (double *)c->cpay.p,
                      (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
                      (unsigned *)c->rowcnt.p, kwik, reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
                      (const Snap *)c->snap_cur.p, (Snap *)c->snap_build.p, (int)n);
@@ -1646,15 +1866,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (mark(3)) return -1;
   // ---- K2: row offsets, scatter into row segments, per-row rank + gather
   const int nscan = (int)(2 * (nrows + 1));
-  size_t scan_tmp = 0;
-  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, (const unsigned *)c->rowcnt.p,
-                                              (unsigned *)c->rowoff.p, nscan, c->stream));
-  if (!ensure(c, c->sort_tmp, std::max<size_t>(scan_tmp, 16), "scan scratch")) return -1;
-  scan_tmp = c->sort_tmp.bytes;
-  BSA_HIP(c, hipcub::DeviceScan::ExclusiveSum(c->sort_tmp.p, scan_tmp, (const unsigned *)c->rowcnt.p,
-                                              (unsigned *)c->rowoff.p, nscan, c->stream));
+  if (scan_excl(c, (const unsigned *)c->rowcnt.p, (unsigned *)c->rowoff.p, nscan)) return -1;
   hipLaunchKernelGGL(k_scatter, dim3(256 * 4), dim3(256), 0, c->stream, (const Counters *)dcnt, cap, (int)rb,
-                     (int)nrows, (const unsigned char *)c->cflag.p, (const unsigned long long *)c->ckey.p,
+                     (int)nrows, (const unsigned char *)c->cflag.p, (const double *)c->cpay.p,
                      (const unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
                      (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
                      (unsigned long long *)c->lkey2.p);

@@ -107,6 +107,7 @@ constexpr int kResortEveryReuse = 64;  // ... with a reusable candidate list (a 
 constexpr int kEvSets = 4096;    // detect timing event sets kept between resets
 
 constexpr int kCandShards = 8;  // candidate list shards (one counter each, 128 B apart)
+constexpr unsigned kDangling = 0xffffffffu;  // resopairs column of a deleted intruder (sorts last in a row)
 
 // counters block on the device
 struct Counters {
@@ -115,7 +116,8 @@ struct Counters {
   unsigned long long los;
   unsigned long long tiles;
   unsigned long long groups;  // (64-row x 8-column) blocks swept by the prefilter
-  unsigned long long pad[3];
+  unsigned long long tiles_near;  // of `tiles`: pairs whose boxes overlap (listed first, swept first)
+  unsigned long long pad[2];
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];
   unsigned long long cshard[kCandShards][16];  // candidates per shard (word 0 of each line)
@@ -145,8 +147,12 @@ struct Ctx {
   DevBuf rowrec, colrec, pfrow, pfcol, pfvrow, pfvcol, pfprow, pfpcol;
   // spatial order: Morton keys and the sorted-position -> original-index maps
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
-  DevBuf tbox_r, tbox_c, gbox_r, gbox_c, sbox_c, tilepairs, workq;
+  DevBuf tbox_r, tbox_c, gbox_r, gbox_c, sbox_c, tilepairs, itemmask, workq;
   DevBuf rowcnt, rowoff, lslot;  // K2 counting sort
+  DevBuf scan_ws;                // single-pass scan: [0] ticket counter, then tile status words
+  bool scan_ready = false;
+  unsigned long long scan_tickets = 0;
+  unsigned scan_epoch = 0;
   // reusable spatial order (any permutation gives identical results)
   bool perm_valid = false, perm_shared = false, perm_distinct = false;
   double perm_f = 0.0;  // midpoint factor the spatial order was computed with (k_keys)
@@ -250,6 +256,11 @@ struct Ctx {
   // OpenAP flight envelope of the resident sim (bsa_sim_set_limits) + traf.ax
   DevBuf s_env, s_ax;
   bool sim_limits = false;
+  // OpenAP flight-phase envelope (bsa_sim_set_perf): type table, per-aircraft
+  // type index (int32) and the phase of the last step (u8)
+  DevBuf s_ptab, s_ptype, s_phase;
+  bool sim_perf = false;
+  int64_t sim_ntypes = 0;
   void *feed_host = nullptr;
   size_t feed_host_bytes = 0;
   hipEvent_t feed_ev = nullptr;
@@ -295,6 +306,9 @@ struct BkDev {
 int bk_count(Ctx *c, const BkDev &d);
 int bk_apply(Ctx *c, const BkDev &d);
 void bk_release(Ctx *c);
+
+// exclusive prefix sum of n words, one launch (bsa_cd.hip)
+int scan_excl(Ctx *c, const unsigned *in, unsigned *out, int n);
 
 // error helpers
 int fail(Ctx *c, const char *fmt, ...);

@@ -120,6 +120,32 @@ __device__ __forceinline__ void openap_limits(const Envelope &e, double ax, doub
   h = allow_h;
 }
 
+// OpenAP type table (bsa_sim_set_perf, bluesky_amd/perf.py): per type, vmin by
+// phase NA..GD, vmax by phase, vsmin, vsmax, hmax, axmax, lifttype, pad
+constexpr int kPerfCols = 24;
+constexpr int kPhaseGD = 8;
+
+// OpenAP flight phase (phase.py:14-62, unit SI): the fixed-wing rule on the
+// pre-step state, rotors (and any other lift type) NA
+__device__ __forceinline__ int openap_phase(double lift, double vs, double alt) {
+  if (lift != 1.0) return 0;
+  const double roc = vs / 0.00508, a = alt / 0.3048;
+  int ph = 0;
+  if (a <= 10 && roc <= 100 && roc >= -100) ph = kPhaseGD;
+  if (a >= 0 && a <= 1000 && roc >= 0) ph = 2;     // IC
+  if (a >= 0 && a <= 1000 && roc <= 0) ph = 6;     // AP
+  if (a >= 1000 && roc >= 100) ph = 3;             // CL
+  if (a >= 1000 && roc <= -100) ph = 5;            // DE
+  if (a >= 5000 && roc <= 100 && roc >= -100) ph = 4;  // CR
+  return ph;
+}
+
+// __construct_limit_matrix (perfoap.py:211-262) for one aircraft: its type
+// row at its phase
+__device__ __forceinline__ Envelope openap_envelope(const double *row, int ph) {
+  return Envelope{row[20], row[ph], row[9 + ph], row[18], row[19], row[21]};
+}
+
 struct In {
   double tas, hdg, alt, vs, lat, lon;       // state before the step
   double ptas, phdg, palt, pvs;             // pilot targets

@@ -30,6 +30,9 @@ struct SimDev {
                                    // vtas2cas(tas, altprev) (traffic.py:434) off the step
   double *ax;                      // traf.ax (traffic.py:431), read by the OpenAP limits next step
   const double *env;               // OpenAP envelope, 6 x n (hmax vmin vmax vsmin vsmax axmax) or NULL
+  const double *ptab;              // OpenAP type table (bsa_sim_set_perf) or NULL: envelope and
+  const int *ptype;                //   acceleration follow each aircraft's flight phase
+  uint8_t *phase;
   int n;
   const double *aptrk, *aptas, *apalt, *apvs, *bank, *eps, *accel;
   const double *atrk, *atas, *avs, *aalt;
@@ -72,7 +75,14 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   } else {
     s.phdg = kin::nprem(ptrk, 360.);                  // pilot.py:63
   }
-  if (d.env) {  // Pilot.applylimits (pilot.py:65-68, OpenAP), traffic.py:404
+  s.accel = d.accel[k];
+  if (d.ptab) {  // OpenAP.update (perfoap.py:115-131) on the pre-step state, then applylimits
+    const double *row = d.ptab + (size_t)d.ptype[k] * kin::kPerfCols;
+    const int ph = kin::openap_phase(row[22], d.vs[k], d.alt[k]);
+    d.phase[k] = (uint8_t)ph;
+    kin::openap_limits(kin::openap_envelope(row, ph), d.ax[k], s.ptas, s.pvs, s.palt);
+    s.accel = ph == kin::kPhaseGD ? 2.0 : 0.5;  // OpenAP.acceleration (perfoap.py:271-280)
+  } else if (d.env) {  // Pilot.applylimits (pilot.py:65-68, OpenAP), traffic.py:404
     const kin::Envelope e{d.env[k], d.env[d.n + k], d.env[2 * d.n + k], d.env[3 * d.n + k],
                           d.env[4 * d.n + k], d.env[5 * d.n + k]};
     kin::openap_limits(e, d.ax[k], s.ptas, s.pvs, s.palt);
@@ -85,7 +95,6 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   s.lon = d.lon[k];
   s.bank = d.bank[k];
   s.eps = d.eps[k];
-  s.accel = d.accel[k];
   const kin::Out o = kin::step(s, simdt, winddim, vwn, vwe);
   d.tas[k] = o.tas;
   d.hdg[k] = o.hdg;
@@ -143,6 +152,9 @@ static SimDev sim_dev(Ctx *c) {
   d.altprev = (double *)c->s_altprev.p;
   d.ax = (double *)c->s_ax.p;
   d.env = c->sim_limits ? (const double *)c->s_env.p : nullptr;
+  d.ptab = c->sim_perf ? (const double *)c->s_ptab.p : nullptr;
+  d.ptype = (const int *)c->s_ptype.p;
+  d.phase = (uint8_t *)c->s_phase.p;
   d.n = (int)c->n;
   d.aptrk = (const double *)c->s_aptrk.p;
   d.aptas = (const double *)c->s_aptas.p;
@@ -223,7 +235,8 @@ void sim_release(Ctx *c) {
   DevBuf *all[] = {&c->red, &c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
-                   &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env};
+                   &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env,
+                   &c->s_ptab, &c->s_ptype, &c->s_phase};
   for (auto *b : all) release(*b);
   bk_release(c);
   comm_release(c);
@@ -335,6 +348,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
     return -1;
   BSA_HIP(c, hipMemsetAsync(c->s_ax.p, 0, N8, c->stream));   // traf.ax: 0 at create
   c->sim_limits = false;
+  c->sim_perf = false;
   BSA_HIP(c, hipMemcpyAsync(c->s_atrk.p, s->trk, N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemcpyAsync(c->s_atas.p, s->tas, N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipMemsetAsync(c->s_avs.p, 0, N8, c->stream));
@@ -437,6 +451,54 @@ int bsa_sim_set_limits(bsa_ctx *cc, const double *hmax, const double *vmin, cons
     BSA_HIP(c, hipMemcpyAsync((char *)c->s_env.p + k * N8, src[k], N8, hipMemcpyHostToDevice, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   c->sim_limits = true;
+  return 0;
+}
+
+int bsa_sim_set_perf(bsa_ctx *cc, int64_t ntypes, const double *table, const int32_t *type_idx) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_set_perf before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (!table) {
+    c->sim_perf = false;
+    return 0;
+  }
+  if (ntypes < 1 || !type_idx) return bsa::fail(c, "bsa_sim_set_perf: bad type table");
+  // every index and lift type is checked here: the kernel reads the table unguarded
+  for (int64_t t = 0; t < ntypes; ++t) {
+    const double lt = table[t * bsa::kin::kPerfCols + 22];
+    if (lt != 0.0 && lt != 1.0 && lt != 2.0) return bsa::fail(c, "type %lld: lifttype must be 0, 1 or 2", (long long)t);
+  }
+  const int64_t n = c->n;
+  for (int64_t k = 0; k < n; ++k)
+    if (type_idx[k] < 0 || type_idx[k] >= ntypes)
+      return bsa::fail(c, "aircraft %lld: type index %d outside [0, %lld)", (long long)k, type_idx[k], (long long)ntypes);
+  const size_t tb = (size_t)ntypes * bsa::kin::kPerfCols * 8;
+  if (!bsa::ensure(c, c->s_ptab, tb, "OpenAP type table") || !bsa::ensure(c, c->s_ptype, (size_t)n * 4, "type index") ||
+      !bsa::ensure(c, c->s_phase, (size_t)n, "flight phase"))
+    return -1;
+  BSA_HIP(c, hipMemcpyAsync(c->s_ptab.p, table, tb, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipMemcpyAsync(c->s_ptype.p, type_idx, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipMemsetAsync(c->s_phase.p, 0, (size_t)n, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  c->sim_perf = true;
+  c->sim_ntypes = ntypes;
+  return 0;
+}
+
+int bsa_sim_read_perf(bsa_ctx *cc, uint8_t *phase, double *ax) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_read_perf before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  const int64_t rb = c->sim_rb, nr = c->sim_re - c->sim_rb;
+  if (phase) {
+    if (!c->sim_perf) return bsa::fail(c, "no flight phase: bsa_sim_set_perf is off");
+    if (nr > 0) BSA_HIP(c, hipMemcpyAsync(phase + rb, (uint8_t *)c->s_phase.p + rb, nr, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (ax && nr > 0)
+    BSA_HIP(c, hipMemcpyAsync(ax + rb, (double *)c->s_ax.p + rb, (size_t)nr * 8, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
   return 0;
 }
 

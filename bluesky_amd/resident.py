@@ -94,6 +94,26 @@ class ResidentSim:
         steps) keeping the ASAS bookkeeping (bsa_sim_update)."""
         self.ctx.sim_update(**arrays)
 
+    def set_perf(self, table=None, type_idx=None):
+        """OpenAP.update's flight phase, phase-dependent envelope and
+        acceleration in every step (bsa_sim_set_perf; bluesky_amd.perf builds
+        ``table`` / ``type_idx``); None switches it off."""
+        self.ctx.sim_set_perf(table, type_idx)
+
+    def read_perf(self):
+        """(flight phase of the last step, traf.ax) of this rank's rows."""
+        return self.ctx.sim_read_perf()
+
+    def create(self, state):
+        """Append aircraft (Traffic.create; ``state`` as ``initial_state`` returns,
+        m long each): indices n..n+m-1 (bsa_sim_create, one rank)."""
+        self.ctx.sim_create(state)
+
+    def delete(self, idx):
+        """Remove aircraft ``idx`` (Traffic.delete: the rest shift down in order),
+        keeping the callsign-keyed ASAS bookkeeping of the others (bsa_sim_delete)."""
+        self.ctx.sim_delete(idx)
+
     def read(self):
         return self.ctx.sim_read()
 

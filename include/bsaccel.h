@@ -365,6 +365,23 @@ int bsa_sim_step(bsa_ctx *ctx, int nsteps);
  * hmax == NULL switches the limits off (the default after bsa_sim_init). */
 int bsa_sim_set_limits(bsa_ctx *ctx, const double *hmax, const double *vmin, const double *vmax,
                        const double *vsmin, const double *vsmax, const double *axmax);
+/* OpenAP.update (performance/openap/perfoap.py:115-131) inside the step:
+ * each aircraft's flight phase is inferred from its pre-step vs / alt
+ * (phase.py:14-62), its envelope looked up in its type's row at that phase
+ * (__construct_limit_matrix, perfoap.py:211-262) and applied as
+ * bsa_sim_set_limits does, and UpdateAirSpeed's acceleration is
+ * OpenAP.acceleration() (2 m/s^2 in phase GD, else 0.5; perfoap.py:271-280)
+ * instead of the frozen accel.  table: ntypes rows of 24 doubles -- vmin by
+ * phase NA..GD (9), vmax by phase (9), vsmin, vsmax, hmax, axmax, lifttype
+ * (1 fixed wing, 2 rotor, 0 other), 0 (bluesky_amd/perf.py builds it from the
+ * reference's Coefficient tables); type_idx: full-n row per aircraft
+ * (validated).  Takes precedence over bsa_sim_set_limits; table == NULL
+ * switches it off (the default after bsa_sim_init). */
+int bsa_sim_set_perf(bsa_ctx *ctx, int64_t ntypes, const double *table, const int32_t *type_idx);
+/* This rank's rows [row_begin, row_end) of the flight phase of the last step
+ * (0..8, phase.py:4-12; needs bsa_sim_set_perf) and of traf.ax, written into
+ * full-n host arrays; either pointer may be NULL. */
+int bsa_sim_read_perf(bsa_ctx *ctx, uint8_t *phase, double *ax);
 /* Overwrite per-aircraft arrays of the resident sim (full-n host arrays, all
  * ranks pass the same) while keeping the ASAS bookkeeping (resopairs, the
  * previous call's pair sets, asas.active / trk / tas / vs) and traf.ax: the
@@ -373,6 +390,21 @@ int bsa_sim_set_limits(bsa_ctx *ctx, const double *hmax, const double *vmin, con
  * before Traffic.update's kinematics).  NULL pointers leave that array as it
  * is; asas_alt overwrites the persistent asas.alt. */
 int bsa_sim_update(bsa_ctx *ctx, const bsa_sim_state *s);
+/* Traffic.create for the resident sim (traffic.py:192-312 + ASAS.create,
+ * asas.py:402-407): append m aircraft whose state is s (m-long host arrays,
+ * every field required); asas.trk / tas start at trk / tas, asas.alt at
+ * s->asas_alt, asas.vs / active / traf.ax at 0.  They take indices n..n+m-1.
+ * One rank only; fails while OpenAP limits are on (set them again after). */
+int bsa_sim_create(bsa_ctx *ctx, int64_t m, const bsa_sim_state *s);
+/* Traffic.delete for the resident sim (traffic.py:364-378 ->
+ * trafficarrays.py:99-117): remove the k aircraft idx[0..k) (any order,
+ * duplicates ignored); the rest keep their order and shift down, as np.delete
+ * does.  The ASAS bookkeeping follows the reference's callsign-keyed sets:
+ * resopairs of a deleted ownship go; a resopair whose intruder was deleted
+ * stays (bsa_sim_resopairs reports idx2 = -1) until the next CD call's
+ * ResumeNav switches the ownship's ASAS off and drops it (asas.py:419-468).
+ * One rank only; removing every aircraft is an error (re-init instead). */
+int bsa_sim_delete(bsa_ctx *ctx, int64_t k, const int64_t *idx);
 /* Full-n host copies of the state (collective: gathers all ranks' rows).
  * Any pointer may be NULL. */
 int bsa_sim_read(bsa_ctx *ctx, bsa_sim_out *o);
@@ -387,7 +419,8 @@ int bsa_sim_stats(bsa_ctx *ctx, int64_t *out6);
  * the global pair sets (every rank gathers all ranks' pair keys; the same
  * values on every rank). */
 int bsa_sim_asas_stats(bsa_ctx *ctx, int64_t *out6);
-/* This rank's resopairs (idx1 ascending, then idx2), at most cap pairs;
+/* This rank's resopairs (idx1 ascending, then idx2; idx2 = -1, last in its
+ * row, for an intruder deleted since the last CD call), at most cap pairs;
  * *count = total (call again with a larger buffer when *count > cap). */
 int bsa_sim_resopairs(bsa_ctx *ctx, int32_t *idx1, int32_t *idx2, int64_t cap, int64_t *count);
 

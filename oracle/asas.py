@@ -11,7 +11,15 @@ unique, so the sets correspond one to one).  One call = the part of
 * ``confpairs_all.extend(unique - previous unique)``      asas.py:497-498
 * ``ResumeNav()``                                         asas.py:409-471,504
 
-ResumeNav per resopair (no deleted aircraft in the resident sim):
+Deleted aircraft (Traffic.delete, traffic.py:364-378): the reference's sets
+are keyed by callsign and untouched by a delete; ``delete()`` / ``create()``
+restate that on indices -- a pair of a deleted ownship goes (ResumeNav drops it
+at the next call, asas.py:420-422, before anything reads it), a pair whose
+intruder was deleted becomes (i, -1) and is dropped by the next ResumeNav with
+``active[i] = False`` (idx2 < 0, asas.py:454-468), and previous-call unique
+pairs with a deleted member can never match again, so they go.
+
+ResumeNav per resopair:
 flat-earth ``dist`` vector (re = 6371000, cos of the mean latitude),
 ``past_cpa = dot(dist, vrel) > 0``, ``hor_los = |dist| < R``,
 ``is_bouncing = |trk1 - trk2| < 30 and |dist| < Rm``; keep the pair and set
@@ -30,7 +38,10 @@ RE = 6371000.     # asas.py:426
 
 
 def pair_keep(i, j, lat, lon, gseast, gsnorth, trk, R, Rm):
-    """ResumeNav's decision for resopair (i, j) (asas.py:424-452)."""
+    """ResumeNav's decision for resopair (i, j) (asas.py:424-452); j < 0: the
+    intruder was deleted -- recovery starts (asas.py:454-468)."""
+    if j < 0:
+        return False
     dist = RE * np.array([np.radians(lon[j] - lon[i]) * np.cos(0.5 * np.radians(lat[j] + lat[i])),
                           np.radians(lat[j] - lat[i])])
     vrel = np.array([gseast[j] - gseast[i], gsnorth[j] - gsnorth[i]])
@@ -74,6 +85,23 @@ class Bookkeeping:
         self.resopairs = {p for p, k in keep.items() if k}
         self.last_keep = keep
         return keep
+
+    def delete(self, idx):
+        """np.delete of aircraft ``idx`` (the rest shift down in order)."""
+        n = len(self.active)
+        gone = np.zeros(n, dtype=bool)
+        gone[np.asarray(idx, dtype=np.int64)] = True
+        new = np.cumsum(~gone) - 1
+        new[gone] = -1
+        self.resopairs = {(int(new[i]), -1 if j < 0 else int(new[j])) for i, j in self.resopairs if not gone[i]}
+        remap = lambda s: {frozenset(int(new[x]) for x in p) for p in s if not any(gone[x] for x in p)}
+        self.confpairs_unique = remap(self.confpairs_unique)
+        self.lospairs_unique = remap(self.lospairs_unique)
+        self.active = self.active[~gone]
+
+    def create(self, m):
+        """Traffic.create of m aircraft (appended, asas.active False)."""
+        self.active = np.concatenate([self.active, np.zeros(m, dtype=bool)])
 
     def ambiguous(self, keep):
         """Aircraft whose resopairs disagree (reference result hash-order dependent)."""

@@ -12,12 +12,16 @@ wind (``p['wind'] = (vnorth, veast)``, windfield.py:150-152) or a 2-D field
 UpdateGroundSpeed / UpdatePosition (traffic.py:425-483).  With a
 ``Bookkeeping`` (oracle/asas.py) the CD step instead runs ASAS.update's
 resopairs bookkeeping and ResumeNav (asas.py:409-504) and takes asas.active
-from it.
+from it.  ``p['perf']`` (dict actypes, lifttype, limits_fixwing,
+limits_rotor) runs OpenAP.update's phase / envelope / acceleration
+(oracle/perf.py) before the limits, as Traffic.update does
+(traffic.py:397-404).
 """
 import numpy as np
 
 from . import kinematics as okin
 from . import mvp as omvp
+from . import perf as operf
 from . import statebased as ocd
 
 
@@ -80,11 +84,19 @@ def sim_step(st, p, do_cd, bk=None, cd=None):
     else:
         phdg = ptrk % 360.
     env = p.get('limits')
+    accel = st['accel']
+    pf = p.get('perf')
+    if pf is not None:                                        # OpenAP.update (perfoap.py:115-131)
+        ph = operf.phase(pf['lifttype'], st['tas'], st['vs'], st['alt'])
+        env = operf.envelope(operf.limit_matrix(pf['limits_fixwing'], pf['limits_rotor'], pf['actypes'],
+                                                pf['lifttype'], ph))
+        accel = operf.acceleration(ph)                        # UpdateAirSpeed (traffic.py:429)
+        st['phase'] = ph
     if env is not None:                                       # pilot.py:65-68 (OpenAP)
         ptas, pvs, palt = okin.openap_limits(ptas, pvs, palt, st.get('ax', np.zeros(n)), env)
     s = dict(tas=st['tas'], hdg=st['hdg'], alt=st['alt'], vs=st['vs'], lat=st['lat'], lon=st['lon'],
              ptas=ptas, phdg=phdg, palt=palt, pvs=pvs, bank=st['bank'], eps=st['eps'],
-             accel=st['accel'])
+             accel=accel)
     if wind is not None:
         o = okin.step(s, p['simdt'], winddim=1, windnorth=wind[0], windeast=wind[1])
     else:

@@ -293,3 +293,135 @@ def test_resident_openap_limits_match_oracle(ctx):
     a, b = ostep.sim_step(s0, op, do_cd=True), ostep.sim_step(s0, free, do_cd=True)
     assert np.mean(a['tas'] != b['tas']) > 0.1 and np.any(a['vs'] != b['vs'])
     ctx.sim_set_limits(None)
+
+
+def test_resident_create_delete_matches_oracle(ctx):
+    """Traffic.delete / create between steps (bsa_sim_delete / bsa_sim_create,
+    traffic.py:192-378): every per-aircraft array is compacted / appended on the
+    device and the ASAS bookkeeping follows the reference's callsign-keyed sets
+    (oracle/asas.py delete / create, pinned by tests/golden/trace_super8del.npz).
+    Each step is compared with the oracle step from the same state."""
+    from oracle import asas as oasas
+    t = synth.box(1500, 60.0, seed=83)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=2.0, resume_nav=True)
+    sim = resident.ResidentSim(init, p, ctx=ctx)
+    op = oracle_params(p)
+    bk = oasas.Bookkeeping(t.ntraf)
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(t.ntraf), active=np.zeros(t.ntraf, bool))
+    rng = np.random.default_rng(83)
+    dangling = 0
+    for k in range(9):
+        if k == 3:   # delete 10 %: intruders of live resopairs among them
+            i, j = sim.resopairs()
+            gone = np.unique(np.concatenate([rng.choice(j, 40, replace=False),
+                                             rng.choice(t.ntraf, 110, replace=False)]))
+            sim.delete(gone)
+            bk.delete(gone)
+            keep = np.ones(len(prev['lat']), bool)
+            keep[gone] = False
+            init = {a: v[keep] for a, v in init.items()}
+            prev = {a: v[keep] for a, v in prev.items()}
+            i, j = sim.resopairs()
+            dangling = int((j < 0).sum())
+            assert sorted(zip(i.tolist(), j.tolist())) == sorted(bk.resopairs)
+            st = full_state(init, sim.read())
+            for a in SCALES:
+                assert np.array_equal(st[a], prev[a]), a
+            assert np.array_equal(st['active'], prev['active'])
+        if k == 5:   # create 60 aircraft in the same airspace
+            u = synth.box(60, 60.0, seed=84)
+            new = resident.initial_state(u)
+            sim.create(new)
+            bk.create(60)
+            init = {a: np.concatenate([init[a], new[a]]) for a in init}
+            add = dict(new, asas_trk=new['trk'], asas_tas=new['tas'], asas_vs=np.zeros(60),
+                       active=np.zeros(60, bool))
+            prev = {a: np.concatenate([prev[a], add[a]]) for a in prev}
+        exp = ostep.sim_step(prev, op, do_cd=True, bk=bk)
+        sim.step(1)
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        i, j = sim.resopairs()
+        assert list(zip(i.tolist(), j.tolist())) == sorted(bk.resopairs), 'step %d resopairs' % k
+        st = sim.asas_stats()
+        assert st == dict(resopairs=len(bk.resopairs), confpairs_unique=len(bk.confpairs_unique),
+                          lospairs_unique=len(bk.lospairs_unique), confpairs_all=bk.confpairs_all,
+                          lospairs_all=bk.lospairs_all, active=int(exp['active'].sum())), k
+        assert sim.stats()['n_conf'] == exp['n_conf']
+        prev = got
+    assert dangling > 0 and len(got['lat']) == t.ntraf - len(gone) + 60
+
+
+def test_resident_create_delete_errors(ctx):
+    t = synth.box(300, 30.0, seed=89)
+    init = resident.initial_state(t)
+    sim = resident.ResidentSim(init, resident.params(), ctx=ctx)
+    with pytest.raises(RuntimeError):
+        sim.delete(np.arange(300))            # every aircraft
+    with pytest.raises(RuntimeError):
+        sim.delete([300])                     # out of range
+    env = {k: np.full(300, v) for k, v in dict(hmax=2e4, vmin=50., vmax=300., vsmin=-20., vsmax=20.,
+                                               axmax=1.).items()}
+    sim.ctx.sim_set_limits(env)
+    with pytest.raises(RuntimeError):
+        sim.create({k: v[:2] for k, v in init.items()})   # limits on
+    sim.delete([0, 0, 5])                     # duplicates ignored; limits compacted
+    assert sim.ctx.n == 298 and len(sim.read()['lat']) == 298
+    sim.step(1)
+
+
+def test_resident_openap_phase_matches_oracle(ctx):
+    """OpenAP.update in the step (bsa_sim_set_perf): flight phase from the
+    pre-step vs / alt, the type x phase envelope of the reference's own
+    coefficient tables (tests/golden/perf_openap3000.npz) and acceleration()
+    -- against oracle/perf.py composed into the oracle step; the phase and
+    traf.ax of every step exact."""
+    from bluesky_amd import perf
+    from tests.test_perf_oracle import load
+    g, fw, rot = load()
+    t = synth.box(2000, 60.0, seed=91)
+    init = resident.initial_state(t)
+    rng = np.random.default_rng(91)
+    n = t.ntraf
+    types = np.array(sorted(fw) + sorted(rot))
+    actypes = types[rng.integers(0, len(types), n)]
+    lifttype = np.where(np.isin(actypes, sorted(rot)), perf.LIFT_ROTOR, perf.LIFT_FIXWING)
+    # ground, initial climb / approach band, climb / descent, cruise
+    init['alt'] = rng.choice([0.5, 150.0, 900.0, 3000.0, 10000.0], n) + rng.uniform(-1.0, 1.0, n)
+    init['vs'] = rng.choice([0.0, 0.3, -0.3, 4.0, -4.0], n)
+    init['ap_alt'] = init['alt'] + rng.choice([0.0, 600.0, -600.0], n)
+    init['ap_vs'] = rng.choice([2.0, 8.0, 30.0], n)
+    init['ap_tas'] = init['tas'] * rng.choice([0.3, 1.0, 1.4], n)
+    init['asas_alt'] = init['alt'].copy()
+    # rotors never get axmax (perfoap.py:254-261): a climb above their vsmax
+    # would be (1 - 0/0) * vsmax = NaN in the reference too; keep them below it
+    init['ap_vs'][lifttype == perf.LIFT_ROTOR] = 2.0
+    table, tidx = perf.type_table(fw, rot, actypes, lifttype)
+    p = resident.params(cd_every=2)
+    sim = resident.ResidentSim(init, p, ctx=ctx)
+    sim.set_perf(table, tidx)
+    op = oracle_params(p)
+    op['perf'] = dict(actypes=actypes, lifttype=lifttype, limits_fixwing=fw, limits_rotor=rot)
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(n), active=np.zeros(n, bool), ax=np.zeros(n))
+    seen = set()
+    for k in range(5):
+        exp = ostep.sim_step(prev, op, do_cd=(k % 2 == 0))
+        sim.step(1)
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        ph, ax = sim.read_perf()
+        assert np.array_equal(ph, exp['phase'].astype(np.uint8)), k
+        ok, msg = util.close(ax, exp['ax'], 2.0)
+        assert ok, 'step %d ax: %s' % (k, msg)
+        seen |= set(np.unique(ph).tolist())
+        got['ax'] = ax
+        prev = got
+    assert {perf.NA, perf.IC, perf.CL, perf.CR, perf.DE, perf.AP, perf.GD} <= seen, seen
+    sim.set_perf(None)
+    with pytest.raises(RuntimeError):
+        sim.set_perf(table, np.full(n, len(table), np.int32))   # index outside the table

@@ -1,6 +1,8 @@
 """GPU parity on the reference's own full-simulator traces: BASELINE.json
 configs[0] (scenario/ASAS-SUPER8.scn, StateBased CD + MVP, RMETHH BOTH) and
-configs[1] (scenario/1000.scn, N = 606, StateBased CD, CR OFF).
+configs[1] (scenario/1000.scn, N = 606, StateBased CD, CR OFF), and SUPER8
+with stack DEL / CRE commands mid-run (trace_super8del: Traffic.delete /
+create between calls, replayed with bsa_sim_delete / bsa_sim_create).
 
 tests/golden/trace_*.npz hold, per ASAS.update call of the reference's
 detached simulator (tools/make_trace.py), the state the detector read and the
@@ -27,6 +29,7 @@ import pytest
 from bluesky_amd import mvp, resident, statebased
 from oracle import asas as oasas
 from tests import util
+from tests.test_oracle_trace import traffic_change
 
 pytestmark = pytest.mark.gpu
 
@@ -85,17 +88,23 @@ def test_dropin_detect_and_mvp_match_reference_trace(ctx, path):
                 assert np.array_equal(asas2.__dict__[k], asas.__dict__[k]), k
 
 
+def sim_state(r, sel):
+    """bsa_sim_state of aircraft ``sel`` of trace call ``r``."""
+    g = lambda k: np.array(r[k])[sel]
+    m = len(g('lat'))
+    return dict(lat=g('lat'), lon=g('lon'), alt=g('alt'), tas=g('tas'), hdg=g('trk'), vs=g('vs'), gs=g('gs'),
+                trk=g('trk'), gseast=g('gseast'), gsnorth=g('gsnorth'), ap_trk=g('aptrk'), ap_tas=g('aptas'),
+                ap_alt=g('apalt'), ap_vs=g('apvs'), selalt=g('selalt'), bank=np.full(m, np.radians(25.)),
+                eps=np.full(m, 0.01), accel=np.full(m, 0.5), asas_alt=g('asas_alt_in'))
+
+
 @pytest.mark.parametrize('path', TRACES, ids=[util.case_name(p) for p in TRACES])
 def test_resident_resume_nav_matches_reference_trace(ctx, path):
     st, calls = util.load_trace(path)
     reso = str(st['cr']).endswith('MVP')
     r0 = calls[0]
     n = len(r0['lat'])
-    init = dict(lat=r0['lat'], lon=r0['lon'], alt=r0['alt'], tas=r0['tas'], hdg=r0['trk'], vs=r0['vs'],
-                gs=r0['gs'], trk=r0['trk'], gseast=r0['gseast'], gsnorth=r0['gsnorth'],
-                ap_trk=r0['aptrk'], ap_tas=r0['aptas'], ap_alt=r0['apalt'], ap_vs=r0['apvs'], selalt=r0['selalt'],
-                bank=np.full(n, np.radians(25.)), eps=np.full(n, 0.01), accel=np.full(n, 0.5),
-                asas_alt=r0['asas_alt_in'])
+    init = sim_state(r0, slice(None))
     p = resident.params(rpz=float(st['rpz']), hpz=float(st['hpz']), tla=float(st['tla']), mar=float(st['mar']),
                         reso=reso, swresohoriz=bool(st['swresohoriz']), swresospd=bool(st['swresospd']),
                         swresohdg=bool(st['swresohdg']), swresovert=bool(st['swresovert']),
@@ -104,6 +113,18 @@ def test_resident_resume_nav_matches_reference_trace(ctx, path):
     bk = oasas.Bookkeeping(n)
     assert not r0['active_in'].any()
     for c, r in enumerate(calls):
+        n = len(r['lat'])
+        if c and 'ids' in r:   # stack DEL / CRE between the calls
+            deleted, created = traffic_change(calls[c - 1]['ids'], r['ids'])
+            if deleted:
+                sim.delete(deleted)
+                bk.delete(deleted)
+            if created:
+                sim.create(sim_state(r, slice(n - created, n)))
+                bk.create(created)
+            i, j = sim.resopairs()
+            live = sorted(set((a, b) for a, b in zip(r['reso_in_i'].tolist(), r['reso_in_j'].tolist()) if a >= 0))
+            assert sorted(set(zip(i.tolist(), j.tolist()))) == live, c
         sim.update(lat=r['lat'], lon=r['lon'], trk=r['trk'], gs=r['gs'], alt=r['alt'], vs=r['vs'], tas=r['tas'],
                    gseast=r['gseast'], gsnorth=r['gsnorth'], selalt=r['selalt'], ap_vs=r['apvs'],
                    ap_trk=r['aptrk'], ap_tas=r['aptas'], ap_alt=r['apalt'])
@@ -117,8 +138,10 @@ def test_resident_resume_nav_matches_reference_trace(ctx, path):
         assert [s['confpairs_unique'], s['lospairs_unique'], s['confpairs_all'], s['lospairs_all']] == \
             r['counts'].tolist(), c
         got = sim.read()
-        una = np.setdiff1d(np.arange(n), np.array(bk.ambiguous(keep), dtype=np.int64))
+        amb = np.array(bk.ambiguous(keep), dtype=np.int64)
+        una = np.setdiff1d(np.arange(n), amb)
         assert np.array_equal(got['active'][una], r['active'][una]), c
+        bk.active[amb] = got['active'][amb]   # the device's order-free outcome
         for k, sc in (('trk', 360.0), ('tas', 300.0), ('vs', 20.0), ('alt', 1e4)):
             ok, msg = util.close(got['asas_' + k], r['asas_' + k], sc)
             assert ok, 'call %d asas.%s: %s' % (c, k, msg)

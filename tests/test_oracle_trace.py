@@ -1,5 +1,6 @@
 """CPU: the oracle against the reference's own full-simulator traces
-(BASELINE.json configs[0] SUPER8 and configs[1] 1000.scn, N = 606).
+(BASELINE.json configs[0] SUPER8 and configs[1] 1000.scn, N = 606, plus
+SUPER8 with stack DEL / CRE commands mid-run: trace_super8del).
 
 tests/golden/trace_*.npz were recorded by tools/make_trace.py, which runs the
 reference's detached simulator (bluesky.init + Simulation.step) and records
@@ -28,9 +29,24 @@ def mvp_params(st):
                                      bool(st['swresovert']), bool(st['swprio']), str(st['priocode']))
 
 
+def traffic_change(prev_ids, ids):
+    """(deleted indices of the previous call, number created) between two calls;
+    Traffic.create appends, Traffic.delete keeps the others' order."""
+    prev_ids, ids = [str(x) for x in prev_ids], [str(x) for x in ids]
+    deleted = [k for k, a in enumerate(prev_ids) if a not in ids]
+    kept = [a for a in prev_ids if a in ids]
+    assert ids[:len(kept)] == kept, 'created aircraft are appended'
+    return deleted, len(ids) - len(kept)
+
+
 def test_traces_present():
     names = {util.case_name(p) for p in TRACES}
-    assert names == {'trace_super8', 'trace_1000scn'}
+    assert names == {'trace_super8', 'trace_1000scn', 'trace_super8del'}
+    st, calls = util.load_trace(util.golden('trace_super8del.npz')[0])
+    changes = [traffic_change(a['ids'], b['ids']) for a, b in zip(calls, calls[1:])]
+    assert [c for c in changes if c != ([], 0)] == [([2], 0), ([], 1), ([4], 0), ([0, 6], 0)]
+    # a resopair whose intruder was deleted is still there at the next call (idx2 = -1)
+    assert any((calls[7]['reso_in_j'] < 0).tolist())
     st, calls = util.load_trace(util.golden('trace_1000scn.npz')[0])
     assert len(calls[0]['lat']) == 606           # SURVEY.md 0.6: 1000.scn yields 606 aircraft
     st, calls = util.load_trace(util.golden('trace_super8.npz')[0])
@@ -47,6 +63,17 @@ def test_oracle_matches_reference_trace(path):
     bk = oasas.Bookkeeping(n)
     bk.active = calls[0]['active_in'].copy()
     for c, r in enumerate(calls):
+        n = len(r['lat'])
+        if c and 'ids' in r:   # stack DEL / CRE between the calls (Traffic.delete / create)
+            deleted, created = traffic_change(calls[c - 1]['ids'], r['ids'])
+            if deleted:
+                bk.delete(deleted)
+            if created:
+                bk.create(created)
+            # the reference still holds pairs of deleted ownships here (its ResumeNav drops them)
+            live = sorted(set((i, j) for i, j in zip(r['reso_in_i'].tolist(), r['reso_in_j'].tolist()) if i >= 0))
+            assert sorted(bk.resopairs) == live, c
+            assert np.array_equal(bk.active, r['active_in']), c
         t = synth.Traffic(r['lat'], r['lon'], r['alt'], r['trk'], r['gs'], r['vs'])
         o = ocd.detect_arrays(t, t, rpz, hpz, tla)
         exp = dict(r, tinconf=r['tLOS'])
@@ -69,8 +96,10 @@ def test_oracle_matches_reference_trace(path):
         assert sorted(bk.resopairs) == sorted(zip(r['reso_i'].tolist(), r['reso_j'].tolist())), c
         counts = [len(bk.confpairs_unique), len(bk.lospairs_unique), bk.confpairs_all, bk.lospairs_all]
         assert counts == r['counts'].tolist(), c
-        una = np.setdiff1d(np.arange(n), np.array(bk.ambiguous(keep), dtype=np.int64))
+        amb = np.array(bk.ambiguous(keep), dtype=np.int64)
+        una = np.setdiff1d(np.arange(n), amb)
         assert np.array_equal(bk.active[una], r['active'][una]), c
-        if c + 1 < len(calls):   # nothing outside ASAS.update touches asas.alt / asas.active in these runs
+        bk.active[amb] = r['active'][amb]   # carry the reference's hash-order outcome forward
+        if c + 1 < len(calls) and len(calls[c + 1]['lat']) == n:   # nothing outside ASAS.update touches asas.alt / asas.active in these runs
             assert np.array_equal(calls[c + 1]['asas_alt_in'], r['asas_alt'])
             assert np.array_equal(calls[c + 1]['active_in'], r['active'])

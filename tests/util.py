@@ -73,7 +73,8 @@ def load_trace(path):
     gseast gsnorth selalt apvs), asas.alt / asas.active before the call, the detect
     outputs (ci cj li lj inconf tcpamax qdr dist tcpa tLOS), asas.trk/tas/vs/alt and
     asase/asasn after it, resopairs before / after, asas.active after, the four
-    bookkeeping counts and whether MVP ran."""
+    bookkeeping counts and whether MVP ran; with created / deleted traffic also
+    the callsigns (``ids``) and per-aircraft arrays of varying length."""
     z = dict(np.load(path, allow_pickle=False))
     n = int(z['ncalls'])
     settings = {k[4:]: z[k][()] for k in z if k.startswith('set_')}
@@ -83,10 +84,10 @@ def load_trace(path):
         for k, v in z.items():
             if k.startswith('set_') or k == 'ncalls' or k.endswith('_off'):
                 continue
-            if k in TRACE_PAIRS:
-                off = z[TRACE_PAIRS[k] + '_off']
+            if k + '_off' in z or k in TRACE_PAIRS:  # concatenated over calls
+                off = z[k + '_off'] if k + '_off' in z else z[TRACE_PAIRS[k] + '_off']
                 rec[k] = v[off[c]:off[c + 1]]
-            else:
+            else:                                     # stacked [call, ...]
                 rec[k] = v[c]
         calls.append(rec)
     return settings, calls

@@ -16,6 +16,10 @@ and outputs as small ``.npz`` files under ``tests/golden/``:
 * ``geo_<case>.npz``   -- standalone ``geo.qdrdist_matrix`` / ``geo.kwikqdrdist_matrix``
                          (geo.py:110-162, 347-363) with row-vector (outer) and 1-D
                          (pairwise) operands, incl. the result types / shapes
+* ``perf_<case>.npz``   -- OpenAP's flight phase (phase.py:14-62), its type x phase
+                         envelope (perfoap.py:211-262) and acceleration()
+                         (perfoap.py:271-280) with the reference's own coefficient
+                         tables (data/performance/OpenAP)
 * ``cdkwik_<case>.npz`` -- the opt-in KWIK variant: ``StateBasedCD.detect`` with
                          ``geo.qdrdist_matrix`` swapped for ``geo.kwikqdrdist_matrix``
                          (geo.py:347-363), its metre distance handed over / nm
@@ -397,6 +401,61 @@ def run_limits(name, n, seed):
     print('limits_%-14s N=%5d' % (name, n))
 
 
+FIXWING_FIELDS = ('vminto', 'vmaxto', 'vminic', 'vmaxic', 'vminer', 'vmaxer', 'vminap', 'vmaxap', 'vminld',
+                  'vmaxld', 'vsmin', 'vsmax', 'hmax', 'axmax')
+ROTOR_FIELDS = ('vmin', 'vmax', 'vsmin', 'vsmax', 'hmax')
+
+
+def run_perf(name, n, seed):
+    """OpenAP.update's phase + limit matrix and OpenAP.acceleration, by the
+    reference's own functions on its own coefficient tables (the OpenAP
+    instance is made without __init__: only coeff / lifttype / phase are read)."""
+    import bluesky as bs
+    from bluesky.traffic.performance.openap import coeff as refcoeff
+    from bluesky.traffic.performance.openap import phase as refphase
+    from bluesky.traffic.performance.openap.perfoap import OpenAP
+    from oracle import perf as operf
+    cwd = os.getcwd()
+    os.chdir(REF)                      # perf_path_openap is relative to the reference root
+    try:
+        C = refcoeff.Coefficient()
+    finally:
+        os.chdir(cwd)
+    wing = sorted(C.limits_fixwing)
+    rot = sorted(k for k in C.limits_rotor if k in C.acs_rotor)[:3]
+    rng = np.random.default_rng(seed)
+    names = np.array(wing + rot)
+    actypes = names[rng.integers(0, len(names), n)]
+    lifttype = np.where(np.isin(actypes, rot), refcoeff.LIFT_ROTOR, refcoeff.LIFT_FIXWING)
+    alt = rng.uniform(-30., 12500., n)
+    vs = rng.uniform(-25., 25., n)
+    tas = rng.uniform(0., 280., n)
+    # flight-phase boundaries exactly: alt 0 / 10 / 1000 / 5000 ft, roc +-100 fpm and 0
+    k = n // 4
+    alt[:k] = rng.choice(np.array([-1.0, 0.0, 10., 1000., 5000., 4999., 12000.]) * ft, k)
+    vs[:k] = rng.choice(np.array([-200., -100., -50., 0., 50., 100., 200.]) * 0.00508, k)
+    alt[k:2 * k] = rng.uniform(-5., 400., k)
+    vs[k:2 * k] = rng.uniform(-1.5, 1.5, k)
+    perf = OpenAP.__new__(OpenAP)
+    object.__setattr__(perf, 'coeff', C)
+    object.__setattr__(perf, 'lifttype', lifttype)
+    ph = refphase.get(lifttype, tas, vs, alt, unit='SI')
+    lim = perf._OpenAP__construct_limit_matrix(actypes, ph)
+    object.__setattr__(perf, 'phase', ph)
+    bs.traf = types.SimpleNamespace(ntraf=n)
+    acc = OpenAP.acceleration(perf)
+    oph = operf.phase(lifttype, tas, vs, alt)
+    olim = operf.limit_matrix(C.limits_fixwing, C.limits_rotor, actypes, lifttype, oph)
+    assert np.array_equal(oph, ph) and np.array_equal(olim, lim) and np.array_equal(operf.acceleration(oph), acc)
+    assert len(np.unique(ph)) >= 6, np.unique(ph)
+    fw = {'fw_' + f: np.array([C.limits_fixwing[m][f] for m in wing], dtype=np.float64) for f in FIXWING_FIELDS}
+    rt = {'rot_' + f: np.array([C.limits_rotor[m][f] for m in rot], dtype=np.float64) for f in ROTOR_FIELDS}
+    np.savez_compressed(os.path.join(OUT, 'perf_%s.npz' % name), actypes=actypes, lifttype=lifttype, tas=tas,
+                        vs=vs, alt=alt, phase=ph, limits=lim, accel=acc, fw_types=np.array(wing),
+                        rot_types=np.array(rot), **fw, **rt)
+    print('perf_%-16s N=%5d phases %s' % (name, n, np.unique(ph)))
+
+
 def run_asas(name, traf, ncalls=4, dt=20.0):
     """Reference ASAS.update (asas.py:473-504) incl. ResumeNav on a stand-in
     bs.traf; state advanced along straight tracks between CD calls."""
@@ -528,6 +587,9 @@ def main():
     if '--limits-only' in sys.argv:
         run_limits('openap2000', 2000, 71)
         return
+    if '--perf-only' in sys.argv:
+        run_perf('openap3000', 3000, 73)
+        return
     if '--windfield-only' in sys.argv:
         run_kin('windfield1500', 1500, 34, 0.05, wind=WIND_FIELD)
         return
@@ -552,6 +614,7 @@ def main():
     run_kin('wind1000', 1000, 33, 0.05, wind=(270.0, 25.0 * kts))
     run_kin('windfield1500', 1500, 34, 0.05, wind=WIND_FIELD)
     run_limits('openap2000', 2000, 71)
+    run_perf('openap3000', 3000, 73)
     for case in geo_cases():
         run_geo(*case)
 

@@ -17,6 +17,13 @@ detector reads and the MVP inputs are saved before the call, and the detector
 * ``trace_1000scn.npz``  -- scenario/1000.scn (606 aircraft after the duplicate /
   colliding CRE lines), StateBased CD, CR OFF (asas.py:76-77
   defaults).  The first ASAS calls.
+* ``trace_super8del.npz`` -- SUPER8 as above with traffic created and deleted
+  while the conflicts are being resolved (TrafficArrays create / delete,
+  trafficarrays.py:73-118, traffic.py:192-378): ``DEL`` of an aircraft that
+  is in other aircraft's resopairs, ``CRE`` of a new one into the conflict,
+  then another ``DEL``; every ASAS call of the first 60 s.  Per call the
+  callsigns are stored too (``ids``), so a replay can map indices across the
+  index shifts of a delete.
 
 Offline shims, all in a scratch run directory outside the repo:
 numpy-2 aliases, stub ``zmq`` / ``semver`` modules (bluesky/network/__init__.py
@@ -123,11 +130,11 @@ class Recorder:
         self.orig(simt)
         idx = {k: i for i, k in enumerate(ids)}
 
-        def pairs(lst):
-            a = np.array([(idx[p], idx[q]) for p, q in lst], dtype=np.int64).reshape(-1, 2)
+        def pairs(lst):  # ids of deleted aircraft (still in resopairs until ResumeNav) -> -1
+            a = np.array([(idx.get(p, -1), idx.get(q, -1)) for p, q in lst], dtype=np.int64).reshape(-1, 2)
             return a[:, 0], a[:, 1]
 
-        rec = dict(simt=simt, ids=ids, **pre)
+        rec = dict(simt=simt, ids=np.array(ids, dtype='U16'), **pre)
         rec['ci'], rec['cj'] = pairs(asas.confpairs)
         rec['li'], rec['lj'] = pairs(asas.lospairs)
         rec['inconf'] = np.array(asas.inconf, dtype=bool)
@@ -157,21 +164,24 @@ def asas_settings(asas):
 
 PAIR_KEYS = ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tLOS', 'li', 'lj', 'reso_in_i', 'reso_in_j',
              'reso_i', 'reso_j')
+SCALAR_KEYS = ('simt', 'mvp_ran')
 
 
 def save(name, calls, settings):
-    """Per-aircraft arrays stacked as [call, aircraft]; pair arrays of all calls
-    concatenated, with ``<key>_off`` offsets [ncalls + 1] (conflict-pair keys
-    share ``ci_off``, LoS keys ``li_off``, resopairs ``reso_i_off`` /
-    ``reso_in_i_off``)."""
+    """Per-aircraft arrays stacked as [call, aircraft] when every call has the
+    same traffic, else (create / delete) concatenated like the pair arrays;
+    pair arrays of all calls concatenated, with ``<key>_off`` offsets
+    [ncalls + 1] (conflict-pair keys share ``ci_off``, LoS keys ``li_off``,
+    resopairs ``reso_i_off`` / ``reso_in_i_off``)."""
     d = {'ncalls': np.array(len(calls))}
     for k, v in settings.items():
         d['set_' + k] = np.array(v)
+    same_n = len({len(rec['lat']) for rec in calls}) == 1
     for k in calls[0]:
-        if k == 'ids':
+        if k == 'ids' and same_n:
             continue
         vals = [np.asarray(rec[k]) for rec in calls]
-        if k in PAIR_KEYS:
+        if k in PAIR_KEYS or (not same_n and k not in SCALAR_KEYS):
             d[k] = np.concatenate(vals)
             d[k + '_off'] = np.concatenate([[0], np.cumsum([len(v) for v in vals])]).astype(np.int64)
         else:
@@ -204,6 +214,40 @@ def run_super8(bs, seconds=360.0):
     return rec.calls, settings
 
 
+def run_super8del(bs, seconds=60.0):
+    """SUPER8 with a delete, a create into the conflict and another delete."""
+    from bluesky import stack
+    from bluesky.tools.aero import ft
+    traf = bs.traf
+    numac, distance, alt, spd = 8, 0.50, 20000 * ft, 200
+    for i in range(numac):
+        angle = 2 * np.pi / numac * i
+        traf.create(acid='SUP' + str(i), actype='SUPER', aclat=float(distance * -np.cos(angle)),
+                    aclon=float(distance * np.sin(angle)), achdg=float(360.0 - 360.0 / numac * i),
+                    acalt=float(alt), acspd=float(spd))
+    for cmd in ('ASAS ON', 'RESO MVP', 'RMETHH BOTH', 'RMETHV OFF'):
+        stack.stack(cmd)
+    rec = Recorder(bs)
+    events = {int(round(6.5 / bs.sim.simdt)): lambda: traf.delete(traf.id.index('SUP2')),
+              int(round(9.5 / bs.sim.simdt)): lambda: traf.create(acid='NEW1', actype='SUPER', aclat=0.05,
+                                                                     aclon=-0.3, achdg=80.0,
+                                                                     acalt=float(alt), acspd=float(spd)),
+              int(round(14.5 / bs.sim.simdt)): lambda: traf.delete(traf.id.index('SUP5')),
+              int(round(20.5 / bs.sim.simdt)): lambda: traf.delete(np.array([traf.id.index('SUP0'),
+                                                                             traf.id.index('NEW1')]))}
+    nsteps = int(round(seconds / bs.sim.simdt))
+    bs.sim.step()
+    bs.sim.fastforward()
+    for k in range(nsteps):
+        if k in events:
+            events[k]()
+        bs.sim.step()
+    settings = asas_settings(traf.asas)
+    settings['cd'] = traf.asas.cd.__name__
+    settings['cr'] = traf.asas.cr.__name__
+    return rec.calls, settings
+
+
 def run_1000(bs, ncalls=8):
     rec = Recorder(bs)
     bs.sim.step()
@@ -222,7 +266,7 @@ def main():
     if which in ('all', 'super8'):
         if which == 'all':   # one reference process per scenario (bluesky is a singleton)
             import subprocess
-            for w in ('super8', '1000'):
+            for w in ('super8', '1000', 'super8del'):
                 subprocess.run([sys.executable, os.path.abspath(__file__), w], check=True)
             return
         bs, run = init_reference()
@@ -230,6 +274,13 @@ def main():
         save('trace_super8.npz', calls, st)
         print('trace_super8: %d ASAS calls, conf per call %s, mvp %s' % (
             len(calls), [len(c['ci']) for c in calls], [int(c['mvp_ran']) for c in calls]))
+        shutil.rmtree(run, ignore_errors=True)
+    elif which == 'super8del':
+        bs, run = init_reference()
+        calls, st = run_super8del(bs)
+        save('trace_super8del.npz', calls, st)
+        print('trace_super8del: %d ASAS calls, N %s, conf %s' % (
+            len(calls), [len(c['lat']) for c in calls], [len(c['ci']) for c in calls]))
         shutil.rmtree(run, ignore_errors=True)
     elif which == '1000':
         bs, run = init_reference(scnfile=os.path.join('scenario', '1000.scn'))
