@@ -732,7 +732,10 @@ constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 struct PfKnobs {
   int shards;  // dequeue counters in use (power of two <= kWorkShards)
 };
-constexpr int PF_BLOCKS_PER_CU = 5;  // LDS-limited (~7.8 KB per wave) and BSA_PF_WAVES_PER_EU
+#ifndef BSA_PF_WAVES_PER_EU
+#define BSA_PF_WAVES_PER_EU 4
+#endif
+constexpr int PF_BLOCKS_PER_CU = BSA_PF_WAVES_PER_EU;  // resident workgroups per CU (4 waves each): LDS and VGPR limits
 constexpr int kSubsPerTile = kTile / kSub;
 static_assert(kSubsPerTile == 64, "one sub-group box per lane");
 constexpr int kSubsPerBatch = 64 / kSub;  // sub-groups per 64-column batch
@@ -829,12 +832,9 @@ __global__ __launch_bounds__(256) void k_items(int nrows, int ncols, const TileB
 // ds_bpermute).  Stage-2 survivors go to a second queue flushed to HBM with
 // one atomic on the wave's candidate shard.
 template <bool NOPRUNE>
-// 5 waves per SIMD = PF_BLOCKS_PER_CU resident workgroups (the LDS limit):
-// caps the kernel at 96 VGPRs (a few spill to scratch; measured 2% faster
-// than 4 waves per SIMD at 102 VGPRs)
-#ifndef BSA_PF_WAVES_PER_EU
-#define BSA_PF_WAVES_PER_EU 5
-#endif
+// 4 waves per SIMD = PF_BLOCKS_PER_CU resident workgroups: up to 128 VGPRs,
+// no spills (at 5 waves the 96-VGPR cap spilled to scratch, and every scratch
+// reload in the batch loop waited for the in-flight prefetch: 8 us slower)
 #define PF_OCC __attribute__((amdgpu_waves_per_eu(BSA_PF_WAVES_PER_EU, 8)))
 __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, const float4 *__restrict__ pprow, int nrows,
@@ -852,6 +852,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ float4 csv[PF_WAVES][64];      //                      u v vs alt    (refine)
   __shared__ unsigned cix[PF_WAVES][64];    //                      sorted column index
   __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:       u v vs alt    (refine)
+  __shared__ float4 rsp[PF_WAVES][PF_WROWS];  //                    x y z sigma   (refine)
   if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned long long ntiles = cnt->tiles, near = cnt->tiles_near;
@@ -910,7 +911,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     __builtin_amdgcn_wave_barrier();
   };
 #ifdef BSA_PF_STAMPS
-  unsigned long long st_acc[4] = {0, 0, 0, 0};
+  // [4] stage-1 survivors, [5] refine rounds, [6] batches, [7] enqueue loop trips
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
   for (;;) {
@@ -945,20 +947,14 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       for (int t = 0; t < kSubsPerBatch && m; ++t) m &= m - 1;
       return m;
     };
+    // unconditional loads (an empty slot reads column 0; its survivor bits are
+    // masked by colmask and it is never queued): a load under a branch makes
+    // the compiler wait for it right there, which would expose the prefetch
     auto load_col = [&](int j, PFRec &r, PFVel &v, float4 &q) {
-      if (j >= 0) {
-        r = pcol[j];
-        v = vcol[j];
-        q = ppcol[j];
-      } else {
-        r.x = r.y = r.z = r.s = qnan;
-        r.lo = INFINITY;
-        r.hi = -INFINITY;
-        r.alt = r.pad = 0.f;
-        v.u = v.v = v.vs = qnan;
-        v.flags = 1;
-        q = make_float4(qnan, qnan, qnan, 0.f);
-      }
+      const int jj = j >= 0 ? j : 0;
+      r = pcol[jj];
+      v = vcol[jj];
+      q = ppcol[jj];
     };
     int jn = batch_col(gm);
     PFRec nx;
@@ -968,20 +964,12 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 
     const int krow = rbase + lane;
     const bool va = krow < nrows;
-    PFRec A;
-    PFVel AV;
-    float4 AP;
-    if (va) {
-      A = prow[krow];
-      AV = vrow[krow];
-      AP = pprow[krow];
-    } else {
-      A.x = A.y = A.z = A.s = A.alt = A.pad = 0.f;
-      A.lo = A.hi = 0.f;
-      AV.u = AV.v = AV.vs = 0.f;
-      AV.flags = 1;
-      AP = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    // (unconditional, as load_col: a lane past the last row reads row rbase and
+    // its survivor bits are masked)
+    const int krw = va ? krow : rbase;
+    const PFRec A = prow[krw];
+    const PFVel AV = vrow[krw];
+    const float4 AP = pprow[krw];
     // the item's plane: o = first row of the slice, E / N an orthonormal
     // tangent pair at o (any orthonormal pair is exact-safe; near a pole, or
     // for a non-finite o, the x / y axes)
@@ -1016,32 +1004,31 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const float kr = 0.5f * A.s * A.s - 0.5f * (re_ * re_ + rn_ * rn_) + kPlaneMargin;
     const f2 K = {kr, kr};
     const f2 HI = {A.hi, A.hi}, LO = {A.lo, A.lo};
-    const float rx = AP.x, ry = AP.y, rz = AP.z, rsig = A.pad;  // refine: position at t = 0
-    // the row of this lane for the refine (u = NaN: never refine)
+    // the row of this lane for the refine (u = NaN: never refine), position at
+    // t = 0 and vertical budget; read from LDS by the drain (a register
+    // broadcast would make it wait for the in-flight batch prefetch)
     rv[lane] = make_float4(AV.flags ? qnan : AV.u, AV.v, AV.vs, A.alt);
-    const unsigned rowmask = va ? 0xffu : 0u;
+    rsp[w][lane] = make_float4(AP.x, AP.y, AP.z, A.pad);
     unsigned n1 = 0;                 // wave-uniform
     unsigned long long colmask = 0;  // valid slots of the swept batch
 
     auto drain = [&]() {
       __builtin_amdgcn_wave_barrier();
       PF_STAMP(1);
+#ifdef BSA_PF_STAMPS
+      st_acc[4] += n1;
+      st_acc[5] += (n1 + 63) / 64;
+#endif
       for (unsigned b0 = 0; b0 < n1; b0 += 64) {
         const unsigned k = b0 + lane;
         const unsigned e = q1[k < n1 ? k : b0];
         const unsigned rl = e >> 6, cl = e & 63u;
-        // the row's unit vector from its owner lane's registers
-        const int src = (int)(rl << 2);
-        const float px = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rx)));
-        const float py = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(ry)));
-        const float pz = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rz)));
-        const float psg = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(rsig)));
         bool keep = false;
         unsigned gi = 0, gj = 0;
         if (k < n1) {
           gi = (unsigned)rbase + rl;
           gj = sci[cl];
-          keep = NOPRUNE ? true : pf_refine(make_float4(px, py, pz, psg), rv[rl], sx[cl], sv[cl], prm);
+          keep = NOPRUNE ? true : pf_refine(rsp[w][rl], rv[rl], sx[cl], sv[cl], prm);
         }
         const unsigned long long mk = __ballot(keep);
         if (mk) {
@@ -1059,8 +1046,9 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       PF_STAMP(2);
     };
 
-    // survivors of an 8-column chunk arrive as a per-lane bit mask (bit 7 - u
-    // = slot col0 + u) and are queued once per chunk
+    // survivors of 8-column chunk(s) arrive as a per-lane bit mask (bit u =
+    // slot col0 + u); `enqueue` queues one chunk (the rare path when a whole
+    // batch overflows the queue)
     auto enqueue = [&](unsigned bm, unsigned col0) {
       const unsigned c = (unsigned)__popc(bm);
       const unsigned x = wave_incl_scan(c);
@@ -1068,12 +1056,37 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       if (total == 0) return;
       if (n1 + total > (unsigned)PF_Q1) drain();
       unsigned pos = n1 + x - c;
+#ifdef BSA_PF_STAMPS
+      {
+        unsigned mx = c;
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+        st_acc[7] += mx;
+      }
+#endif
       while (bm) {
-        const unsigned b = 31u - (unsigned)__builtin_clz(bm);
-        q1[pos++] = (unsigned short)(((unsigned)lane << 6) | (col0 + 7u - b));
-        bm ^= 1u << b;
+        q1[pos++] = (unsigned short)(((unsigned)lane << 6) | (col0 + (unsigned)__builtin_ctz(bm)));
+        bm &= bm - 1u;
       }
       n1 = __builtin_amdgcn_readfirstlane(n1 + total);
+    };
+    // the whole batch's survivors (bit = slot) with ONE wave scan; the queue is
+    // empty here (drained after every batch)
+    auto enqueue_batch = [&](unsigned long long M) {
+      const unsigned c = (unsigned)__popcll(M);
+      const unsigned x = wave_incl_scan(c);
+      const unsigned total = __builtin_amdgcn_readlane(x, 63);
+      if (total == 0) return;
+      if (total > (unsigned)PF_Q1) {
+#pragma unroll 1
+        for (unsigned ch = 0; ch < 8; ++ch) enqueue((unsigned)(M >> (8 * ch)) & 0xffu, 8 * ch);
+        return;
+      }
+      unsigned pos = x - c;
+      while (M) {
+        q1[pos++] = (unsigned short)(((unsigned)lane << 6) | (unsigned)__builtin_ctzll(M));
+        M &= M - 1ull;
+      }
+      n1 = total;
     };
 
     PF_STAMP(0);
@@ -1096,14 +1109,17 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         sci[lane] = (unsigned)jn;
         colmask = __ballot(jn >= 0);
       }
+#ifdef BSA_PF_STAMPS
+      st_acc[6] += 1;
+#endif
       gm = drop_batch(gm);
       const bool more = gm != 0;
-      if (more) {  // prefetch the next batch while this one is swept
-        jn = batch_col(gm);
-        load_col(jn, nx, nv, np);
-      }
+      // prefetch the next batch while this one is swept (unconditionally: see load_col)
+      jn = more ? batch_col(gm) : -1;
+      load_col(jn, nx, nv, np);
       // sweep only the chunks holding valid slots
       const int nchunk = colmask ? (64 - __builtin_clzll(colmask) + 7) >> 3 : 0;
+      unsigned long long M = 0;  // this lane's stage-1 survivors of the batch, bit = slot
       for (int ch = 0; ch < nchunk; ++ch) {
         const int j0 = ch * 8;
         unsigned bm = 0;
@@ -1138,16 +1154,22 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         }
         __builtin_amdgcn_sched_barrier(0);
         }
-        const unsigned cm = (unsigned)(colmask >> j0) & 0xffu;
-        // bit 7 - u <-> slot j0 + u: reverse the 8 slot-valid bits
-        const unsigned cmr = __builtin_bitreverse32(cm) >> 24;
-        enqueue(bm & cmr & rowmask, (unsigned)j0);
+        // bit 7 - u <-> slot j0 + u: reverse into bit u
+        M |= (unsigned long long)(__builtin_bitreverse32(bm) >> 24) << j0;
       }
+      enqueue_batch(M & colmask & (va ? ~0ull : 0ull));
       // refine this batch's survivors while its columns are staged
       if (n1) drain();
       PF_STAMP(1);
       if (!more) break;
     }
+    // reserve room for the item's candidates now (the atomic's result is
+    // consumed one flush later): at the end of the sweep every wave would
+    // otherwise flush at once, queueing on the shard counters
+#ifndef PF_ITEM_FLUSH
+#define PF_ITEM_FLUSH 1
+#endif
+    if (PF_ITEM_FLUSH && n2) flush2();
     } while (0);
   }
   PF_STAMP(0);
@@ -1157,7 +1179,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
   if (lane == 0)
-    for (int k = 0; k < 4; ++k) atomicAdd(&cnt->stamp[k], st_acc[k]);
+    for (int k = 0; k < 8; ++k) atomicAdd(&cnt->stamp[k], st_acc[k]);
 #endif
 }
 
@@ -1692,7 +1714,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // this perm / parameters / buffers unless an aircraft overran its budget
   // (decided on the device by K0b; ctl[0] = build this detect)
   if (c->cand_cap == 0)
-    c->cand_cap = (unsigned long long)kCandShards * (unsigned long long)std::max<int64_t>(1 << 17, 4 * nrows);
+    // 8 x max(128 k, 4 rows) candidates in all (at 100k rows ~12x the demand), whole shards
+    c->cand_cap = (unsigned long long)kCandShards *
+                  (((unsigned long long)8 * std::max<int64_t>(1 << 17, 4 * nrows) + kCandShards - 1) / kCandShards);
   const unsigned long long cap = c->cand_cap;
   if (!ensure(c, c->cand, cap * sizeof(uint2), "candidate pairs")) return -1;
   ReuseParams rz{};
@@ -1929,8 +1953,10 @@ int detect_finish(Ctx *c, bool *retry) {
   c->last_los = (int64_t)h.los;
   c->have_pairs = true;
 #ifdef BSA_PF_STAMPS
-  fprintf(stderr, "[bsa stamps] prefilter wave-cycles: setup %.4g stage1 %.4g drain %.4g flush %.4g\n",
-          (double)h.stamp[0], (double)h.stamp[1], (double)h.stamp[2], (double)h.stamp[3]);
+  fprintf(stderr, "[bsa stamps] prefilter wave-cycles: setup %.4g stage1 %.4g drain %.4g flush %.4g | "
+          "stage-1 survivors %.4g refine rounds %.4g batches %.4g enqueue trips %.4g\n",
+          (double)h.stamp[0], (double)h.stamp[1], (double)h.stamp[2], (double)h.stamp[3], (double)h.stamp[4],
+          (double)h.stamp[5], (double)h.stamp[6], (double)h.stamp[7]);
 #endif
   return 0;
 }
