@@ -853,6 +853,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ unsigned cix[PF_WAVES][64];    //                      sorted column index
   __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:       u v vs alt    (refine)
   __shared__ float4 rsp[PF_WAVES][PF_WROWS];  //                    x y z sigma   (refine)
+  __shared__ unsigned char sgs[PF_WAVES][kSubsPerBatch];  // the next batch's sub-groups (tile-local)
   if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned long long ntiles = cnt->tiles, near = cnt->tiles_near;
@@ -881,7 +882,13 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // items per dequeue, and streaming several column tiles of a slice per item
   // (fewer, longer items: the near tiles of a row group end up serialised on
   // one wave).)
-  const unsigned long long nitems = ntiles * PF_ITEMS_PER_TILE;
+  // Item numbering: the low 3 bits of an item id pick the tile pair within a
+  // group of 8 consecutive tile pairs, the next 3 the 64-row slice.  Shard =
+  // item id mod shards and workgroups go to the XCDs round-robin (blockIdx % 8),
+  // so ONE XCD sweeps all 8 slices of a tile pair, close together in time: the
+  // column tile is fetched into that XCD's L2 once instead of into all eight.
+  static_assert(PF_ITEMS_PER_TILE == 8, "item id layout: 3 bits of slice");
+  const unsigned long long nitems = ((ntiles + 7) / 8) * 64;
   const unsigned shard = blockIdx.x & (kn.shards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
@@ -924,29 +931,36 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     }
     if (item >= nitems) break;
     do {  // one item; `break` ends it
-    const unsigned long long tp = item / PF_ITEMS_PER_TILE;
+#ifndef PF_XCD_ITEMS
+#define PF_XCD_ITEMS 1
+#endif
+    const unsigned long long tp = PF_XCD_ITEMS ? (item & 7ull) + ((item >> 6) << 3) : item >> 3;
+    const unsigned slice = PF_XCD_ITEMS ? (unsigned)(item >> 3) & 7u : (unsigned)item & 7u;
+    if (tp >= ntiles) break;
     const uint2 rc = tile_at(tiles, tp, near, tcap);
-    const int rbase = (int)rc.x * kTile + (int)(item % PF_ITEMS_PER_TILE) * PF_WROWS;
+    const int rbase = (int)rc.x * kTile + (int)slice * PF_WROWS;
     if (rbase >= nrows) break;
     const int cbase = (int)rc.y * kTile;
     // column sub-groups of this tile that may interact with the wave's row box (K0e)
-    unsigned long long gm = masks[item];
+    unsigned long long gm = masks[tp * PF_ITEMS_PER_TILE + slice];
     if (!gm) break;
     subs += (unsigned)__popcll(gm);
 
-    // this lane's slot of the next batch: the (lane / kSub)-th remaining
-    // sub-group, column lane % kSub of it (sub-groups taken in ascending order)
+    // the next batch = the first kSubsPerBatch remaining sub-groups (ascending):
+    // lane b holding the r-th set bit of m (r < 8, r = set bits below b) posts
+    // b to slot r; this lane takes column lane % kSub of the sub-group in slot
+    // lane / kSub.  `taken` = the batch's bits, removed from the mask after it.
+    unsigned long long taken = 0;
     auto batch_col = [&](unsigned long long m) -> int {
+      const bool mine = ((m >> lane) & 1ull) && lane_prefix(m) < (unsigned)kSubsPerBatch;
+      if (mine) sgs[w][lane_prefix(m)] = (unsigned char)lane;
+      taken = __ballot(mine);
       const unsigned q = (unsigned)lane / kSub;
-      for (unsigned t = 0; t < q && m; ++t) m &= m - 1;
-      if (!m) return -1;
-      const int j = cbase + __builtin_ctzll(m) * kSub + (lane & (kSub - 1));
+      if (q >= (unsigned)__popcll(taken)) return -1;
+      const int j = cbase + (int)sgs[w][q] * kSub + (lane & (kSub - 1));
       return j < ncols ? j : -1;
     };
-    auto drop_batch = [](unsigned long long m) {
-      for (int t = 0; t < kSubsPerBatch && m; ++t) m &= m - 1;
-      return m;
-    };
+    auto drop_batch = [&](unsigned long long m) { return m & ~taken; };
     // unconditional loads (an empty slot reads column 0; its survivor bits are
     // masked by colmask and it is never queued): a load under a branch makes
     // the compiler wait for it right there, which would expose the prefetch
