@@ -877,11 +877,14 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // 128 B apart; a returning atomic on one word saturates at ~88 per us).
   // Near tile pairs (the costly ones) come first in the list.  An item's
   // sub-group mask comes from K0e (k_items): one scalar load, no dependent
-  // box loads.  (Measured slower: claiming the next item ahead (+20 us: the
-  // claimed items lengthen the tail, each wave sweeps only ~8 items), several
-  // items per dequeue, and streaming several column tiles of a slice per item
-  // (fewer, longer items: the near tiles of a row group end up serialised on
-  // one wave).)
+  // box loads.  (Measured slower: claiming the next item ahead (+20 us, also
+  // without spills: a returning atomic in flight joins every later in-order
+  // vmcnt wait, so its latency is moved, not hidden); several items per
+  // dequeue, or PF_GROUP consecutive tile pairs of one slice per item sharing
+  // the row setup, with the next pair's first batch prefetched (+10 / +30 /
+  // +90 us at 2 / 4 / 8: fewer, longer items balance worse); stealing items
+  // from other shards once a wave's shard is dry (+130 us: the drained shards'
+  // counters are hammered by failing returning atomics).)
   // Item numbering: the low 3 bits of an item id pick the tile pair within a
   // group of 8 consecutive tile pairs, the next 3 the 64-row slice.  Shard =
   // item id mod shards and workgroups go to the XCDs round-robin (blockIdx % 8),
