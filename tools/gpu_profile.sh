@@ -3,12 +3,12 @@
 # bench line (with the CPU baseline).  Counter passes are separate runs with
 # --kernel-trace only (no sys/runtime trace), each under its own time limit.
 set -u
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 if [ "${PYTEST:-1}" = 1 ]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log
   [ $rc -eq 0 ] || exit $rc
 fi
