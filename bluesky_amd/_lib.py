@@ -156,6 +156,8 @@ SIGNATURES.update({
     'bsa_sim_delete': (ctypes.c_int, [_vp, ctypes.c_int64, _c_i64p]),
     'bsa_sim_read': (ctypes.c_int, [_vp, ctypes.POINTER(SimOut)]),
     'bsa_sim_stats': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_sim_row_ids': (ctypes.c_int, [_vp, _c_i32p]),
+    'bsa_sim_detect_rows': (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _c_i64p, _c_i64p]),
     'bsa_sim_asas_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_resopairs': (ctypes.c_int, [_vp, _c_i32p, _c_i32p, ctypes.c_int64, _c_i64p]),
     'bsa_qdrdist': (ctypes.c_int, [_vp, ctypes.c_int64, _c_dp, _c_dp, ctypes.c_int64, _c_dp, _c_dp,
@@ -596,6 +598,23 @@ class Context:
         self.check(self.lib.bsa_sim_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_stats')
         return dict(steps=int(v[0]), cd_calls=int(v[1]), n_conf=int(v[2]), n_los=int(v[3]),
                     row_begin=int(v[4]), row_end=int(v[5]))
+
+    def sim_row_ids(self):
+        """Aircraft indices of this rank's rows, ascending (bsa_sim_row_ids): the
+        rows of acdata / fetch_pairs' inconf and tcpamax after resident steps."""
+        st = self.sim_stats()
+        ids = np.empty(st['row_end'] - st['row_begin'], np.int32)
+        self.check(self.lib.bsa_sim_row_ids(self.h, ptr(ids, _c_i32p)), 'bsa_sim_row_ids')
+        return ids
+
+    def sim_detect_rows(self, row_begin, row_end):
+        """bsa_sim_detect_rows: the sim's detect of home rows [row_begin, row_end)
+        (one rank's share, measured on one GPU); returns (n_conf, n_los)."""
+        nc, nl = ctypes.c_int64(), ctypes.c_int64()
+        self.check(self.lib.bsa_sim_detect_rows(self.h, int(row_begin), int(row_end), ctypes.byref(nc),
+                                                ctypes.byref(nl)), 'bsa_sim_detect_rows')
+        self.gen += 1
+        return nc.value, nl.value
 
     def sim_asas_stats(self):
         """ASAS bookkeeping counts after the last CD call (resume_nav on); the

@@ -48,7 +48,8 @@ struct BkIn {
   const unsigned *rcol;
   const unsigned *cptr;    // this call's conflict rows: K2 row offsets, nrows + 1
   const int *ccol;         // K2 cj (original column index, ascending per row)
-  const double *lat, *lon, *gse, *gsn, *trk;  // full-N state
+  const double *lat, *lon, *gse, *gsn, *trk;  // full-N state (home order)
+  const unsigned *id2h;    // aircraft index -> home (the CSR columns are indices)
   double R, Rm;
   const unsigned long long *gate;
   const unsigned *sticky;
@@ -68,6 +69,7 @@ __device__ __forceinline__ bool bk_aborted(const unsigned long long *gate, const
 // the ownship and drops the pair (asas.py:454-468)
 __device__ __forceinline__ bool bk_keep(const BkIn &in, int i, int j) {
   if ((unsigned)j == kDangling) return false;
+  j = (int)in.id2h[j];  // i: home row, j: the intruder's index
   const double re = 6371000.;
   const double d0 = re * (((in.lon[j] - in.lon[i]) * kD2R) * cos(0.5 * ((in.lat[j] + in.lat[i]) * kD2R)));
   const double d1 = re * ((in.lat[j] - in.lat[i]) * kD2R);
@@ -154,7 +156,8 @@ __device__ __forceinline__ bool csr_has(const unsigned *ptr, const int *col, int
 }
 
 struct BkUniq {
-  const int *ci, *cj;         // this call's pairs (row-major)
+  const int *ci, *cj;         // this call's pairs (row-major): ci home rows, cj indices
+  const unsigned *h2id, *id2h;
   const unsigned *ptr;        // this call's row offsets (conf: rowoff; los: lptr)
   const unsigned *np;         // device pair count
   const unsigned *pptr;       // previous call's CSR
@@ -169,9 +172,11 @@ __global__ __launch_bounds__(256) void k_bk_unique(BkUniq u, const unsigned long
   for (unsigned x = blockIdx.x * blockDim.x + threadIdx.x; x - lane < P; x += gridDim.x * blockDim.x) {
     bool rep = false, fresh = false;
     if (x < P) {
+      // (i, j) in home-row / index terms; the representative rule compares indices
       const int i = u.ci[x], j = u.cj[x];
-      rep = i < j || !csr_has(u.ptr, u.cj, j, i);
-      if (rep) fresh = !(csr_has(u.pptr, u.pcol, i, j) || csr_has(u.pptr, u.pcol, j, i));
+      const int ii = (int)u.h2id[i], jh = (int)u.id2h[j];
+      rep = ii < j || !csr_has(u.ptr, u.cj, jh, ii);
+      if (rep) fresh = !(csr_has(u.pptr, u.pcol, i, j) || csr_has(u.pptr, u.pcol, jh, ii));
     }
     const unsigned long long mr = __ballot(rep), mf = __ballot(fresh);
     if (lane == 0) {
@@ -252,7 +257,8 @@ __global__ __launch_bounds__(256) void k_bk_pack(int nrows, const unsigned *rowo
 struct KeyBlocks {
   const unsigned long long *cur, *prev;  // nranks x W words each
   unsigned long long W;
-  int nranks, rpr;                       // rows per rank: row i lives in block i / rpr
+  int nranks, rpr;                       // rows per rank: home row i lives in block i / rpr
+  const unsigned *h2id, *id2h;
 };
 
 // is (i, j) a pair of the global list (los = 0: conflicts, 1: LoS)?
@@ -283,9 +289,11 @@ __global__ __launch_bounds__(256) void k_bk_unique_g(KeyBlocks kb, unsigned long
        x += (unsigned long long)gridDim.x * blockDim.x) {
     bool rep = false, fresh = false;
     if (x < P) {
+      // key = home row << 32 | index; the representative rule compares indices
       const unsigned i = (unsigned)(keys[x] >> 32), j = (unsigned)keys[x];
-      rep = i < j || !key_has(kb.cur, kb.W, kb.rpr, los, j, i);
-      if (rep) fresh = !(key_has(kb.prev, kb.W, kb.rpr, los, i, j) || key_has(kb.prev, kb.W, kb.rpr, los, j, i));
+      const unsigned ii = kb.h2id[i], jh = kb.id2h[j];
+      rep = ii < j || !key_has(kb.cur, kb.W, kb.rpr, los, jh, ii);
+      if (rep) fresh = !(key_has(kb.prev, kb.W, kb.rpr, los, i, j) || key_has(kb.prev, kb.W, kb.rpr, los, jh, ii));
     }
     const unsigned long long mr = __ballot(rep), mf = __ballot(fresh);
     if (lane == 0) {
@@ -317,6 +325,7 @@ static BkIn bk_in(Ctx *c, const BkDev &d) {
   in.gse = d.gse;
   in.gsn = d.gsn;
   in.trk = d.trk;
+  in.id2h = d.id2h;
   in.R = c->simp.rpz;        // asas.R
   in.Rm = c->simp.mvp.Rm;    // asas.R * asas.mar (MVP.py:24)
   in.gate = d.gate;
@@ -417,6 +426,8 @@ int bk_apply(Ctx *c, const BkDev &d) {
     u.np = (const unsigned *)c->rowoff.p + nrows;
     u.pptr = (const unsigned *)c->bk_pcptr.p;
     u.pcol = (const int *)c->bk_pccol.p;
+    u.h2id = d.h2id;
+    u.id2h = d.id2h;
     u.uniq = st + 1;
     u.all = st + 3;
     hipLaunchKernelGGL(k_bk_unique, dim3(256), dim3(256), 0, c->stream, u, (const unsigned long long *)d.gate,
@@ -437,7 +448,7 @@ int bk_apply(Ctx *c, const BkDev &d) {
     const size_t blk = (size_t)c->bk_kw * 8;
     if (comm_allgather(c, c->bk_ksend.p, c->bk_kcur.p, blk)) return -1;
     KeyBlocks kb{(const unsigned long long *)c->bk_kcur.p, (const unsigned long long *)c->bk_kprev.p,
-                 (unsigned long long)c->bk_kw, c->nranks, (int)c->sim_rpr};
+                 (unsigned long long)c->bk_kw, c->nranks, (int)c->sim_rpr, d.h2id, d.id2h};
     hipLaunchKernelGGL(k_bk_unique_g, dim3(64, c->nranks, 2), dim3(256), 0, c->stream, kb, st,
                        (const unsigned long long *)d.gate, (const unsigned *)d.sticky);
     BSA_HIP(c, hipGetLastError());

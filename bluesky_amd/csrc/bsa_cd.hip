@@ -302,7 +302,9 @@ struct FusedBoxes {
 
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
 // Workgroup = kTile lanes (one tile of sorted records).
-__global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__restrict__ perm,
+// presorted: the state arrays are already in sorted (home) order, perm only
+// names the aircraft (the resident sim): record k reads index k, coalesced.
+__global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__restrict__ perm, int presorted,
                                                      SoA6 own, SoA6 intr, int distinct, int shared,
                                                      double rpz, double hpz, double tla,
                                                      ColRec *__restrict__ C, PFRec *__restrict__ PC,
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
   if (k < cnt) {
-    const int o = (int)perm[k];
+    const int o = presorted ? k : (int)perm[k];
     const double tlap = tla > 0.0 ? tla : 0.0;
     const double la = intr.lat[o], lo = intr.lon[o];
     const double rad = la * kD2R;
@@ -1421,9 +1423,12 @@ __global__ __launch_bounds__(256) void k_exact(
 #pragma unroll
     for (int q = 1; q < kCandShards; ++q) sh += (idx >= pre[q]) ? 1 : 0;
     const uint2 p = cand[(unsigned long long)sh * ccap + (idx - pre[sh])];
-    const unsigned oi = perm_r[p.x], oj = perm_c[p.y];
+    // home mode (perm_r == NULL, the resident sim): rows are the home slice
+    // [rb, rb + nrows) of the columns; the key's row is the home row, its
+    // column the aircraft index (so K2 orders each row's pairs by index)
+    const unsigned oi = perm_r ? perm_r[p.x] : (unsigned)rb + p.x, oj = perm_c[p.y];
     unsigned char flag = 0;
-    if (oi != oj) {
+    if (perm_r ? oi != oj : oi != p.y) {
       const PairResult o = kwik ? eval_pair<true>(R[p.x], C[p.y], rpz, hpz, tla)
                                 : eval_pair<false>(R[p.x], C[p.y], rpz, hpz, tla);
       flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
@@ -1621,6 +1626,29 @@ static int spatial_order(Ctx *c, int cnt, int base, const double *lat, const dou
   return 0;
 }
 
+// Home order of the resident sim (bsa_sim_init): the spatial order of the
+// traffic in own[] (aircraft-index order) at the look-ahead midpoints the
+// detect's stage 1 uses -> h2id (home position -> aircraft index).  Every rank
+// computes the same permutation from the same state (deterministic sort).
+int home_order(Ctx *c, double tla, std::vector<unsigned> &h2id) {
+  const int64_t n = c->n;
+  const double kf = 0.5 * (tla > 0.0 ? tla : 0.0) / 6371000.0;
+  DevBuf key, idx, key2, perm;
+  struct Rel {
+    DevBuf *b[4];
+    ~Rel() {
+      for (auto *x : b) release(*x);
+    }
+  } rel{{&key, &idx, &key2, &perm}};
+  if (spatial_order(c, (int)n, 0, (const double *)c->own[0].p, (const double *)c->own[1].p,
+                    (const double *)c->own[2].p, (const double *)c->own[3].p, kf, key, idx, key2, perm))
+    return -1;
+  h2id.assign((size_t)n, 0u);
+  BSA_HIP(c, hipMemcpyAsync(h2id.data(), perm.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 // event set of this detect (the pool keeps one set per detect since the last
 // bsa_timing_reset, up to kEvSets; later detects reuse the last set)
 static int next_events(Ctx *c, hipEvent_t **ev) {
@@ -1664,6 +1692,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->rowoff, (size_t)(2 * (nrows + 1)) * 4, "row offsets"))
     return -1;
   const bool distinct = c->has_intruder;
+  // home mode (the resident sim, bsa_sim.hip): own[] is already in spatial
+  // (home) order, h2id names the aircraft; the rows are the 512-aligned home
+  // slice [rb, re) of the columns (no re-sort, no gather)
+  const bool home = c->det_home;
+  c->last_home = home;
+  if (home && (distinct || rb % kTile != 0 || (flags & BSA_FLAG_KWIK)))
+    return fail(c, "home-order detect needs own == intruder, a %d-aligned row slice, no KWIK", kTile);
   const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;
   // KWIK: stage 1 is exact-safe only with the pair's own mean latitude in
   // cavelat (own == intruder), and the CPA refine's geometry
@@ -1672,8 +1707,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const int noprune = ((flags & BSA_FLAG_NOPRUNE) || (kwik && distinct)) ? 1 : 0;
   // rows share the column order and records when own == intruder and the
   // whole range is detected; only then can the candidate list be reused
-  const bool shared = !distinct && rb == 0 && re == n;
-  const bool reuse = c->reuse_on && shared && !noprune && !kwik && n > 0;
+  const bool shared = home || (!distinct && rb == 0 && re == n);
+  const int64_t roff = home ? rb : 0;  // the rows' offset in the shared records
+  const bool reuse = c->reuse_on && shared && rb == 0 && re == n && !noprune && !kwik && n > 0;
   if (!reuse) c->reuse_valid = false;
   // stage 1 at the look-ahead midpoints: its bound is derived
   // for the great-circle geometry and fixed reaches, so not with KWIK nor with
@@ -1724,9 +1760,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // tiles span ~100 km (with a reusable list: 64 calls, and every re-sort
   // rebuilds the list).
   const double kf = mid ? 0.5 * (tla > 0.0 ? tla : 0.0) / 6371000.0 : 0.0;  // k_keys midpoint factor
-  const bool resort = !c->perm_valid || c->perm_n != n || c->perm_rb != rb || c->perm_re != re ||
+  const bool resort = !home && (!c->perm_valid || c->perm_n != n || c->perm_rb != rb || c->perm_re != re ||
                       c->perm_shared != shared || c->perm_distinct != distinct || c->perm_f != kf ||
-                      (flags & BSA_FLAG_RESORT) || c->perm_age >= (reuse ? kResortEveryReuse : kResortEvery);
+                      (flags & BSA_FLAG_RESORT) || c->perm_age >= (reuse ? kResortEveryReuse : kResortEvery));
   // ---- candidate-list reuse: the list of the last build stays valid for
   // this perm / parameters / buffers unless an aircraft overran its budget
   // (decided on the device by K0b; ctl[0] = build this detect)
@@ -1784,9 +1820,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     c->perm_distinct = distinct;
     c->perm_age = 0;
   }
-  c->perm_age++;
-  const unsigned *perm_r = (const unsigned *)(shared ? c->perm_c.p : c->perm_r.p);
-  const unsigned *perm_c = (const unsigned *)c->perm_c.p;
+  if (!home) c->perm_age++;
+  const unsigned *perm_c = (const unsigned *)(home ? c->h2id.p : c->perm_c.p);
+  const unsigned *perm_r = home ? nullptr : (const unsigned *)(shared ? c->perm_c.p : c->perm_r.p);
 
   // ---- buffers sized by the candidate capacity (every pair list <= candidates)
   if (!ensure(c, c->cflag, cap, "candidate flags") ||
@@ -1808,10 +1844,10 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                   !ensure(c, c->pfvrow, nrows * sizeof(PFVel), "prefilter row velocities") ||
                   !ensure(c, c->pfprow, nrows * sizeof(float4), "prefilter row positions")))
     return -1;
-  const RowRec *rowrec = shared ? (const RowRec *)c->colrec.p : (const RowRec *)c->rowrec.p;
-  const PFRec *pfrow = shared ? (const PFRec *)c->pfcol.p : (const PFRec *)c->pfrow.p;
-  const PFVel *pfvrow = shared ? (const PFVel *)c->pfvcol.p : (const PFVel *)c->pfvrow.p;
-  const float4 *pfprow = shared ? (const float4 *)c->pfpcol.p : (const float4 *)c->pfprow.p;
+  const RowRec *rowrec = shared ? (const RowRec *)c->colrec.p + roff : (const RowRec *)c->rowrec.p;
+  const PFRec *pfrow = shared ? (const PFRec *)c->pfcol.p + roff : (const PFRec *)c->pfrow.p;
+  const PFVel *pfvrow = shared ? (const PFVel *)c->pfvcol.p + roff : (const PFVel *)c->pfvrow.p;
+  const float4 *pfprow = shared ? (const float4 *)c->pfpcol.p + roff : (const float4 *)c->pfprow.p;
   if (!shared) {
     hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows,
                        perm_r, own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p, (PFRec *)c->pfrow.p,
@@ -1837,7 +1873,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     zs = ZeroArgs{(int)nrows, 1, 0, dcnt, (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
                   (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p};
   }
-  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, kTile)), dim3(kTile), 0, c->stream, (int)n, perm_c, own,
+  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, kTile)), dim3(kTile), 0, c->stream, (int)n, perm_c,
+                     home ? 1 : 0, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs);
   BSA_HIP(c, hipGetLastError());
@@ -1846,8 +1883,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (!shared && (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
                   !ensure(c, c->gbox_r, ngr * sizeof(TileBox), "row group boxes")))
     return -1;
-  const TileBox *gbox_r = shared ? (const TileBox *)c->gbox_c.p : (const TileBox *)c->gbox_r.p;
-  const TileBox *tbox_r = shared ? (const TileBox *)c->tbox_c.p : (const TileBox *)c->tbox_r.p;
+  const TileBox *gbox_r = shared ? (const TileBox *)c->gbox_c.p + roff / kGroup : (const TileBox *)c->gbox_r.p;
+  const TileBox *tbox_r = shared ? (const TileBox *)c->tbox_c.p + roff / kTile : (const TileBox *)c->tbox_r.p;
   if (!shared)
     hipLaunchKernelGGL(k_boxes, dim3(nrt), dim3(kTile), 0, c->stream, (int)nrows, pfrow, (TileBox *)nullptr,
                        (TileBox *)c->gbox_r.p, (TileBox *)c->tbox_r.p, build, (Counters *)nullptr);
@@ -1921,7 +1958,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
         !ensure(c, c->mvp_pfl, std::max<unsigned long long>(cap, 1), "mvp pair flags"))
       return -1;
     mf.p = *c->fuse_mvp;
-    mf.in = MvpPairIn{c->fuse_gse, c->fuse_gsn, c->fuse_vs, c->fuse_alt, nullptr};
+    mf.in = MvpPairIn{c->fuse_gse, c->fuse_gsn, c->fuse_vs, c->fuse_alt, nullptr,
+                      c->det_home ? (const unsigned *)c->id2h.p : nullptr};
     mf.pdv = (double4 *)c->mvp_pdv.p;
     mf.pfl = (uint8_t *)c->mvp_pfl.p;
     c->fuse_done = true;

@@ -361,29 +361,56 @@ int bsa_gather_pairs(bsa_ctx *cc, int root, const bsa_pairs_out *out) {
   std::vector<char> h(total);
   if (total) BSA_HIP(c, hipMemcpyAsync(h.data(), c->pg_recv.p, total, hipMemcpyDeviceToHost, s));
   BSA_HIP(c, hipStreamSynchronize(s));
-  // concatenate in rank order = the global row-major order (rows are partitioned contiguously)
+  // concatenate in rank order: the ranks' rows are consecutive home ranges,
+  // so this is all rows in home order; home rows -> aircraft indices in
+  // global row-major order (home_pairs_to_ids)
+  int64_t Pt = 0, Lt = 0, Rt = 0;
+  for (int q = 0; q < nr; ++q) {
+    Pt += cnt[3 * q];
+    Lt += cnt[3 * q + 1];
+    Rt += cnt[3 * q + 2];
+  }
+  bsa::HostPairs hp;
+  hp.ci.resize((size_t)Pt);
+  hp.cj.resize((size_t)Pt);
+  hp.pay.resize((size_t)Pt * 5);
+  hp.li.resize((size_t)Lt);
+  hp.lj.resize((size_t)Lt);
+  hp.inconf.resize((size_t)Rt);
+  hp.tcpamax.resize((size_t)Rt);
   int64_t pc = 0, pl = 0, pr = 0;
   for (int q = 0; q < nr; ++q) {
     const int64_t Pq = cnt[3 * q], Lq = cnt[3 * q + 1], Rq = cnt[3 * q + 2];
     const char *blk = h.data() + off[q];
     auto put = [](void *dst, int64_t at_elems, size_t esz, const char *src, int64_t n) {
-      if (dst && n) memcpy((char *)dst + (size_t)at_elems * esz, src, (size_t)n * esz);
+      if (n) memcpy((char *)dst + (size_t)at_elems * esz, src, (size_t)n * esz);
     };
-    put(out->ci, pc, 4, blk, Pq);
-    put(out->cj, pc, 4, blk + (size_t)Pq * 4, Pq);
+    put(hp.ci.data(), pc, 4, blk, Pq);
+    put(hp.cj.data(), pc, 4, blk + (size_t)Pq * 4, Pq);
     const char *pay = blk + al8((size_t)Pq * 8);
-    double *dst5[5] = {out->qdr, out->dist, out->tcpa, out->tinconf, out->dcpa};
-    for (int f = 0; f < 5; ++f) put(dst5[f], pc, 8, pay + (size_t)f * Pq * 8, Pq);
+    for (int f = 0; f < 5; ++f) put(hp.pay.data() + (size_t)f * Pt, pc, 8, pay + (size_t)f * Pq * 8, Pq);
     const char *lp = pay + (size_t)Pq * 40;
-    put(out->li, pl, 4, lp, Lq);
-    put(out->lj, pl, 4, lp + (size_t)Lq * 4, Lq);
+    put(hp.li.data(), pl, 4, lp, Lq);
+    put(hp.lj.data(), pl, 4, lp + (size_t)Lq * 4, Lq);
     const char *rp = lp + al8((size_t)Lq * 8);
-    put(out->inconf, pr, 1, rp, Rq);
-    put(out->tcpamax, pr, 8, rp + al8((size_t)Rq), Rq);
+    put(hp.inconf.data(), pr, 1, rp, Rq);
+    put(hp.tcpamax.data(), pr, 8, rp + al8((size_t)Rq), Rq);
     pc += Pq;
     pl += Lq;
     pr += Rq;
   }
+  if (c->last_home) bsa::home_pairs_to_ids(c, 0, hp);
+  auto out_put = [](void *dst, const void *src, size_t bytes) {
+    if (dst && bytes) memcpy(dst, src, bytes);
+  };
+  out_put(out->ci, hp.ci.data(), (size_t)Pt * 4);
+  out_put(out->cj, hp.cj.data(), (size_t)Pt * 4);
+  double *dst5[5] = {out->qdr, out->dist, out->tcpa, out->tinconf, out->dcpa};
+  for (int f = 0; f < 5; ++f) out_put(dst5[f], hp.pay.data() + (size_t)f * Pt, (size_t)Pt * 8);
+  out_put(out->li, hp.li.data(), (size_t)Lt * 4);
+  out_put(out->lj, hp.lj.data(), (size_t)Lt * 4);
+  out_put(out->inconf, hp.inconf.data(), (size_t)Rt);
+  out_put(out->tcpamax, hp.tcpamax.data(), (size_t)Rt * 8);
   return 0;
 }
 

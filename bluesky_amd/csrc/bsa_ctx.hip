@@ -1,6 +1,7 @@
 // Context, device buffers, state upload and the C ABI entry points of
 // include/bsaccel.h.  No exception crosses the ABI: every entry point
 // returns a status and keeps its message in the context.
+#include <algorithm>
 #include <cstdarg>
 #include <new>
 
@@ -69,6 +70,66 @@ void release(DevBuf &b) {
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.bytes = 0;
+}
+
+// the last detect's outputs as they lie on the device (rows of the detect, K2 order)
+int download_pairs(Ctx *c, HostPairs &h) {
+  const int64_t P = c->last_conf, L = c->last_los, R = c->last_re - c->last_rb;
+  h.ci.resize((size_t)P);
+  h.cj.resize((size_t)P);
+  h.pay.resize((size_t)P * 5);
+  h.li.resize((size_t)L);
+  h.lj.resize((size_t)L);
+  h.inconf.resize((size_t)R);
+  h.tcpamax.resize((size_t)R);
+  auto cp = [&](void *dst, const void *src, size_t bytes) -> int {
+    if (bytes) BSA_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  };
+  if (cp(h.ci.data(), c->out_ci.p, P * 4) || cp(h.cj.data(), c->out_cj.p, P * 4) ||
+      cp(h.pay.data(), c->out_pay.p, P * 40) || cp(h.li.data(), c->out_li.p, L * 4) ||
+      cp(h.lj.data(), c->out_lj.p, L * 4) || cp(h.inconf.data(), c->inconf.p, R) ||
+      cp(h.tcpamax.data(), c->tcpamax.p, R * 8))
+    return -1;
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// Home rows -> aircraft indices: ci / li are home positions, cj / lj already
+// indices, each row's pairs contiguous and ordered by cj (K2), so a stable
+// sort of the pairs by their row's index gives np.where's row-major order
+// (StateBasedCD.py:93-95); the per-row outputs of homes rb.. follow their
+// rows' ascending indices.
+void home_pairs_to_ids(const Ctx *c, int64_t rb, HostPairs &h) {
+  const unsigned *H = c->h2id_h.data();
+  std::vector<uint32_t> ord;
+  auto sort_rows = [&](std::vector<int32_t> &ri) {
+    for (auto &x : ri) x = (int32_t)H[x];
+    ord.resize(ri.size());
+    for (size_t k = 0; k < ord.size(); ++k) ord[k] = (uint32_t)k;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return ri[a] < ri[b]; });
+  };
+  auto apply = [&](auto &v, size_t stride, size_t fields) {
+    auto w = v;
+    const size_t m = ord.size();
+    for (size_t f = 0; f < fields; ++f)
+      for (size_t k = 0; k < m; ++k) v[f * stride + k] = w[f * stride + ord[k]];
+  };
+  const size_t P = h.ci.size(), L = h.li.size(), R = h.inconf.size();
+  sort_rows(h.ci);
+  apply(h.ci, P, 1);
+  apply(h.cj, P, 1);
+  apply(h.pay, P, 5);
+  sort_rows(h.li);
+  apply(h.li, L, 1);
+  apply(h.lj, L, 1);
+  std::vector<int32_t> rid(R);
+  for (size_t r = 0; r < R; ++r) rid[r] = (int32_t)H[rb + (int64_t)r];
+  ord.resize(R);
+  for (size_t k = 0; k < R; ++k) ord[k] = (uint32_t)k;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return rid[a] < rid[b]; });
+  apply(h.inconf, R, 1);
+  apply(h.tcpamax, R, 1);
 }
 
 static int upload6(Ctx *c, DevBuf *dst, int64_t n, const double *const src[6]) {
@@ -176,6 +237,7 @@ int bsa_set_state(bsa_ctx *c, int64_t n, const double *lat, const double *lon, c
   if (n < 0) return bsa::fail(c, "negative n");
   BSA_HIP(c, hipSetDevice(c->device));
   c->sim_ready = false;  // a new state replaces any resident sim
+  c->home = false;       // ... and its home order: aircraft-index order again
   const double *src[6] = {lat, lon, trk, gs, alt, vs};
   if (n == 0) {
     c->n = 0;
@@ -210,6 +272,9 @@ int bsa_detect(bsa_ctx *c, double rpz, double hpz, double tla, int flags, int64_
                int64_t row_end, int64_t *n_conf, int64_t *n_los) {
   if (!c) return -1;
   if (!n_conf || !n_los) return bsa::fail(c, "NULL count pointer");
+  if (c->home)
+    return bsa::fail(c, "bsa_detect on a context whose state is a resident sim's (home order): "
+                        "bsa_set_state first, or use another context");
   BSA_HIP(c, hipSetDevice(c->device));
   return bsa::detect(c, rpz, hpz, tla, flags, row_begin, row_end, n_conf, n_los);
 }
@@ -227,15 +292,30 @@ int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *d
     return 0;
   };
   const double *pay = (const double *)c->out_pay.p;
+  if (dcpa && !(c->last_flags & BSA_FLAG_WITH_DCPA)) return bsa::fail(c, "dcpa requested without BSA_FLAG_WITH_DCPA");
+  if (c->last_home) {  // resident sim: rows are home positions, translated on the host
+    bsa::HostPairs h;
+    if (bsa::download_pairs(c, h)) return -1;
+    bsa::home_pairs_to_ids(c, c->last_rb, h);
+    auto put = [](void *dst, const void *src, size_t bytes) {
+      if (dst && bytes) memcpy(dst, src, bytes);
+    };
+    put(ci, h.ci.data(), P * 4);
+    put(cj, h.cj.data(), P * 4);
+    double *dst5[5] = {qdr, dist, tcpa, tinconf, dcpa};
+    for (int f = 0; f < 5; ++f) put(dst5[f], h.pay.data() + (size_t)f * P, P * 8);
+    put(li, h.li.data(), L * 4);
+    put(lj, h.lj.data(), L * 4);
+    put(inconf, h.inconf.data(), R);
+    put(tcpamax, h.tcpamax.data(), R * 8);
+    return 0;
+  }
   if (cp(ci, c->out_ci.p, P * 4) || cp(cj, c->out_cj.p, P * 4) || cp(qdr, pay + 0 * P, P * 8) ||
       cp(dist, pay + 1 * P, P * 8) || cp(tcpa, pay + 2 * P, P * 8) || cp(tinconf, pay + 3 * P, P * 8) ||
       cp(li, c->out_li.p, L * 4) || cp(lj, c->out_lj.p, L * 4) || cp(inconf, c->inconf.p, R) ||
       cp(tcpamax, c->tcpamax.p, R * 8))
     return -1;
-  if (dcpa) {
-    if (!(c->last_flags & BSA_FLAG_WITH_DCPA)) return bsa::fail(c, "dcpa requested without BSA_FLAG_WITH_DCPA");
-    if (cp(dcpa, pay + 4 * P, P * 8)) return -1;
-  }
+  if (dcpa && cp(dcpa, pay + 4 * P, P * 8)) return -1;
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   return 0;
 }

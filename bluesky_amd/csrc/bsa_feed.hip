@@ -113,14 +113,20 @@ static int feed_poll(Ctx *c, int wait, bsa_acdata *o) {
   o->nlos_cur = counts ? (int64_t)hdr[2] : -1;
   o->nconf_tot = counts ? (int64_t)hdr[3] : -1;
   o->nlos_tot = counts ? (int64_t)hdr[4] : -1;
+  // the mirror holds the rows in home order: row r goes to lpos[r], its place
+  // among the rank's rows in ascending aircraft index (all aircraft with one rank)
+  const unsigned *L = c->lpos_h.data();
+  auto put = [&](auto *dst, const auto *src) {
+    if (dst)
+      for (int64_t r = 0; r < nr; ++r) dst[L[r]] = src[r];
+  };
   const double *f64 = (const double *)((const char *)c->feed_host + 64);
   double *dst[kFeedF64] = {o->lat, o->lon, o->alt, o->tas, o->cas, o->gs, o->trk, o->vs, o->tcpamax};
-  for (int f = 0; f < kFeedF64; ++f)
-    if (dst[f]) memcpy(dst[f], f64 + f * nr, (size_t)nr * 8);
+  for (int f = 0; f < kFeedF64; ++f) put(dst[f], f64 + f * nr);
   const float *f32 = (const float *)(f64 + kFeedF64 * nr);
-  if (o->asasn) memcpy(o->asasn, f32, (size_t)nr * 4);
-  if (o->asase) memcpy(o->asase, f32 + nr, (size_t)nr * 4);
-  if (o->inconf) memcpy(o->inconf, f32 + 2 * nr, (size_t)nr);
+  put(o->asasn, f32);
+  put(o->asase, f32 + nr);
+  put(o->inconf, (const uint8_t *)(f32 + 2 * nr));
   return 0;
 }
 

@@ -210,7 +210,17 @@ struct Ctx {
   DevBuf red;  // small reduction scratch
   DevBuf pg_send, pg_recv;  // C2 pair gather staging (bsa_gather_pairs)
 
-  // GPU-resident sim (bsa_sim.hip)
+  // GPU-resident sim (bsa_sim.hip).  Its state lives in HOME order: home
+  // position h holds aircraft h2id[h] (id2h is the inverse), fixed at init as
+  // the spatial order of the initial traffic, so a rank's rows are a
+  // contiguous, spatially compact home range [sim_rb, sim_re) (512-aligned)
+  // and the detect reads its columns without a gather or a re-sort.  lpos[r]:
+  // position of home sim_rb + r among the rank's rows sorted by aircraft index.
+  bool home = false;                  // own[] and the sim arrays are in home order
+  bool det_home = false;              // detect_enqueue: home-ordered state (set by sim_cd)
+  bool last_home = false;             // the last detect's ci / li are home rows (fetch translates)
+  DevBuf h2id, id2h;                  // u32, device
+  std::vector<unsigned> h2id_h, id2h_h, lpos_h;  // host copies
   bool sim_ready = false;
   bsa_sim_params simp{};
   int64_t sim_steps = 0, sim_cd_calls = 0, sim_rb = 0, sim_re = 0, sim_rpr = 0;
@@ -296,7 +306,8 @@ WindField wind_field(const Ctx *c);  // device view of the context's 2-D field (
 // all-reduce and MVP (may raise the gate's bit 1 on resopairs overflow),
 // bk_apply after MVP.  State arrays are full-N device arrays.
 struct BkDev {
-  const double *lat, *lon, *gse, *gsn, *trk;
+  const double *lat, *lon, *gse, *gsn, *trk;  // home order
+  const unsigned *h2id, *id2h;                // home <-> aircraft index
   uint8_t *active;
   unsigned long long *gate;
   unsigned *sticky;
@@ -309,6 +320,20 @@ void bk_release(Ctx *c);
 
 // exclusive prefix sum of n words, one launch (bsa_cd.hip)
 int scan_excl(Ctx *c, const unsigned *in, unsigned *out, int n);
+// spatial (home) order of the n aircraft in own[] (bsa_cd.hip): home -> aircraft index
+int home_order(Ctx *c, double tla, std::vector<unsigned> &h2id);
+// the last detect's pair lists and per-row outputs in aircraft-index terms
+// (bsa_ctx.hip): home rows -> indices, rows in ascending index order
+struct HostPairs {
+  std::vector<int32_t> ci, cj, li, lj;
+  std::vector<double> pay;  // 5 x P (qdr dist tcpa tinconf dcpa)
+  std::vector<uint8_t> inconf;
+  std::vector<double> tcpamax;
+};
+int download_pairs(Ctx *c, HostPairs &h);
+void home_pairs_to_ids(const Ctx *c, int64_t rb, HostPairs &h);
+// resident sim (bsa_sim.hip): the maps of Ctx::h2id_h (host + device, lpos of this rank's rows)
+int set_home_maps(Ctx *c);
 
 // error helpers
 int fail(Ctx *c, const char *fmt, ...);

@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_mvp_pair(int rb, bsa_mvp_params p, MvpI
   for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < P; k += stride) {
     double4 dv;
     uint8_t fl;
-    mvp_pair(p, MvpPairIn{in.gseast, in.gsnorth, in.vs, in.alt, p.swnoreso ? in.noreso : nullptr}, in.ci[k],
+    mvp_pair(p, MvpPairIn{in.gseast, in.gsnorth, in.vs, in.alt, p.swnoreso ? in.noreso : nullptr, nullptr}, in.ci[k],
              in.cj[k], in.pay[k], in.pay[(size_t)1 * P + k], in.pay[(size_t)2 * P + k],
              in.pay[(size_t)3 * P + k], dv, fl);
     in.pdv[k] = dv;
@@ -267,6 +267,7 @@ extern "C" int bsa_mvp(bsa_ctx *cc, const bsa_mvp_params *p, const double *gseas
     return bsa::fail(c, "bsa_mvp: NULL array argument");
   BSA_HIP(c, hipSetDevice(c->device));
   if (!c->have_pairs) return bsa::fail(c, "bsa_mvp: no detect results (call bsa_detect first)");
+  if (c->home) return bsa::fail(c, "bsa_mvp on a context holding a resident sim (home order): use another context");
   const int64_t n = c->n, nrows = c->last_re - c->last_rb;
   // staging: 6 full-N fp64 inputs + flags + per-row in/out
   const size_t need = (size_t)n * 8 * 4 + (size_t)n * 2 + (size_t)nrows * (8 * 4 + 4 * 2) + 256;

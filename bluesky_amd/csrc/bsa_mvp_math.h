@@ -13,12 +13,15 @@ namespace bsa {
 struct MvpPairIn {
   const double *gseast, *gsnorth, *vs, *alt;
   const uint8_t *noreso;  // NULL = empty NORESO list
+  const unsigned *id2h;   // resident step (home order): the intruder's home position; NULL = identity
 };
 
-// dv = (dv1, dv2, dv3, tsolV); fl: bit 0 subtract from dv[id1], bit 1 add back (NORESO)
+// dv = (dv1, dv2, dv3, tsolV); fl: bit 0 subtract from dv[id1], bit 1 add back (NORESO).
+// id1 indexes the arrays; id2 is the intruder's aircraft index (mapped by id2h)
 __device__ __forceinline__ void mvp_pair(const bsa_mvp_params &p, const MvpPairIn &in, int id1, int id2,
                                          double qdr_deg, double dist, double tcpa, double tLOS, double4 &dv,
                                          uint8_t &fl) {
+  if (in.id2h) id2 = (int)in.id2h[id2];
   const double gse1 = in.gseast[id1], gsn1 = in.gsnorth[id1], vs1 = in.vs[id1], alt1 = in.alt[id1];
   // ---- MVP.MVP (MVP.py:149-231)
   const double qdr = qdr_deg * kD2R;

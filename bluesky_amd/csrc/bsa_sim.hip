@@ -18,6 +18,9 @@
 // every later kernel that writes persistent state (K3, K4') becomes a no-op,
 // so the state stays exactly as before the failed step; the host then grows
 // the buffers and re-runs the batch from that step.
+#include <algorithm>
+#include <type_traits>
+
 #include "bsa_kin_math.h"
 
 #pragma clang fp contract(off)
@@ -242,6 +245,77 @@ void sim_release(Ctx *c) {
   comm_release(c);
 }
 
+// ---- home order (host side): arrays cross the ABI in aircraft-index order
+// and live on the device in home order (Ctx::h2id_h)
+template <typename F>
+static void by_size(size_t esz, F f) {
+  if (esz == 8) f((const uint64_t *)nullptr);
+  else if (esz == 4) f((const uint32_t *)nullptr);
+  else f((const uint8_t *)nullptr);
+}
+
+// dst[h] (device) = src[h2id[h]] (host), h in [0, n)
+static int put_home(Ctx *c, void *dst, const void *src, size_t esz, std::vector<char> &tmp) {
+  const int64_t n = c->n;
+  tmp.resize((size_t)n * esz + 8);
+  const unsigned *H = c->h2id_h.data();
+  by_size(esz, [&](auto tag) {
+    using T = std::remove_const_t<std::remove_pointer_t<decltype(tag)>>;
+    T *t = (T *)tmp.data();
+    const T *q = (const T *)src;
+    for (int64_t h = 0; h < n; ++h) t[h] = q[H[h]];
+  });
+  BSA_HIP(c, hipMemcpyAsync(dst, tmp.data(), (size_t)n * esz, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// out[h2id[h]] (host) = src[h] (device), h in [hb, he)
+static int get_home(Ctx *c, void *out, const void *src, size_t esz, int64_t hb, int64_t he,
+                    std::vector<char> &tmp) {
+  if (he <= hb) return 0;
+  tmp.resize((size_t)(he - hb) * esz + 8);
+  BSA_HIP(c, hipMemcpyAsync(tmp.data(), (const char *)src + (size_t)hb * esz, (size_t)(he - hb) * esz,
+                            hipMemcpyDeviceToHost, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  const unsigned *H = c->h2id_h.data();
+  by_size(esz, [&](auto tag) {
+    using T = std::remove_const_t<std::remove_pointer_t<decltype(tag)>>;
+    const T *t = (const T *)tmp.data();
+    T *o = (T *)out;
+    for (int64_t h = hb; h < he; ++h) o[H[h]] = t[h - hb];
+  });
+  return 0;
+}
+
+// the maps of a home order h2id_h (host + device) and this rank's lpos
+int set_home_maps(Ctx *c) {
+  const int64_t n = c->n;
+  c->id2h_h.assign((size_t)n, 0u);
+  for (int64_t h = 0; h < n; ++h) c->id2h_h[c->h2id_h[(size_t)h]] = (unsigned)h;
+  const int64_t rb = c->sim_rb, nr = c->sim_re - c->sim_rb;
+  std::vector<unsigned> ord((size_t)nr);
+  for (int64_t r = 0; r < nr; ++r) ord[(size_t)r] = (unsigned)r;
+  std::sort(ord.begin(), ord.end(), [&](unsigned a, unsigned b) { return c->h2id_h[rb + a] < c->h2id_h[rb + b]; });
+  c->lpos_h.assign((size_t)nr, 0u);
+  for (int64_t k = 0; k < nr; ++k) c->lpos_h[ord[(size_t)k]] = (unsigned)k;
+  if (!ensure(c, c->h2id, (size_t)n * 4, "home -> index") || !ensure(c, c->id2h, (size_t)n * 4, "index -> home"))
+    return -1;
+  BSA_HIP(c, hipMemcpyAsync(c->h2id.p, c->h2id_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipMemcpyAsync(c->id2h.p, c->id2h_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// rows of `rank`: a 512-aligned home range (the detect's row tiles are then
+// column tiles)
+void set_rank_rows(Ctx *c) {
+  const int64_t n = c->n, R = c->nranks;
+  c->sim_rpr = ((n + R - 1) / R + kTile - 1) / kTile * kTile;
+  c->sim_rb = std::min<int64_t>(n, (int64_t)c->rank * c->sim_rpr);
+  c->sim_re = std::min<int64_t>(n, c->sim_rb + c->sim_rpr);
+}
+
 // one CD step of the batch (enqueue only)
 static int sim_cd(Ctx *c) {
   const bsa_sim_params &p = c->simp;
@@ -256,7 +330,9 @@ static int sim_cd(Ctx *c) {
     c->fuse_vs = (const double *)c->own[5].p;
     c->fuse_alt = (const double *)c->own[4].p;
   }
+  c->det_home = true;
   const int de = detect_enqueue(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, gate);
+  c->det_home = false;
   c->fuse_mvp = nullptr;
   if (de) return -1;
   c->sim_cd_calls++;
@@ -267,6 +343,8 @@ static int sim_cd(Ctx *c) {
   bk.gse = (const double *)c->s_gse.p;
   bk.gsn = (const double *)c->s_gsn.p;
   bk.trk = (const double *)c->own[2].p;
+  bk.h2id = (const unsigned *)c->h2id.p;
+  bk.id2h = (const unsigned *)c->id2h.p;
   bk.active = (uint8_t *)c->s_active.p;
   bk.gate = gate;
   bk.sticky = sticky;
@@ -329,7 +407,15 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
                          s->eps, s->accel, s->asas_alt};
   for (auto q : src)
     if (!q) return bsa::fail(c, "bsa_sim_init: NULL array");
+  // aircraft-index order first: the home order is the spatial order of this state
   if (bsa_set_state(cc, n, s->lat, s->lon, s->trk, s->gs, s->alt, s->vs)) return -1;
+  if (bsa::home_order(c, p->tla, c->h2id_h)) return -1;
+  bsa::set_rank_rows(c);
+  if (bsa::set_home_maps(c)) return -1;
+  std::vector<char> tmp;
+  const double *st6[6] = {s->lat, s->lon, s->trk, s->gs, s->alt, s->vs};
+  for (int k = 0; k < 6; ++k)
+    if (bsa::put_home(c, c->own[k].p, st6[k], 8, tmp)) return -1;
   bsa::DevBuf *dst[] = {&c->s_tas, &c->s_hdg, &c->s_gse, &c->s_gsn, &c->s_aptrk, &c->s_aptas,
                         &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                         &c->s_aalt};
@@ -338,7 +424,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   const size_t N8 = (size_t)n * 8;
   for (int k = 0; k < 13; ++k) {
     if (!bsa::ensure(c, *dst[k], N8, "sim state")) return -1;
-    BSA_HIP(c, hipMemcpyAsync(dst[k]->p, hs[k], N8, hipMemcpyHostToDevice, c->stream));
+    if (bsa::put_home(c, dst[k]->p, hs[k], 8, tmp)) return -1;
   }
   // ASAS arrays: asas.trk/tas start at traf.trk/tas (asas.py:405-409), vs 0, inactive
   if (!bsa::ensure(c, c->s_atrk, N8, "asas trk") || !bsa::ensure(c, c->s_atas, N8, "asas tas") ||
@@ -349,8 +435,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   BSA_HIP(c, hipMemsetAsync(c->s_ax.p, 0, N8, c->stream));   // traf.ax: 0 at create
   c->sim_limits = false;
   c->sim_perf = false;
-  BSA_HIP(c, hipMemcpyAsync(c->s_atrk.p, s->trk, N8, hipMemcpyHostToDevice, c->stream));
-  BSA_HIP(c, hipMemcpyAsync(c->s_atas.p, s->tas, N8, hipMemcpyHostToDevice, c->stream));
+  if (bsa::put_home(c, c->s_atrk.p, s->trk, 8, tmp) || bsa::put_home(c, c->s_atas.p, s->tas, 8, tmp)) return -1;
   BSA_HIP(c, hipMemsetAsync(c->s_avs.p, 0, N8, c->stream));
   BSA_HIP(c, hipMemsetAsync(c->s_ase.p, 0, (size_t)n * 4, c->stream));
   BSA_HIP(c, hipMemsetAsync(c->s_asn.p, 0, (size_t)n * 4, c->stream));
@@ -361,15 +446,13 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   c->simp = *p;
   c->bk_ready = false;  // empty resopairs / previous pair sets
-  c->sim_rpr = (n + c->nranks - 1) / c->nranks;
-  c->sim_rb = std::min<int64_t>(n, (int64_t)c->rank * c->sim_rpr);
-  c->sim_re = std::min<int64_t>(n, c->sim_rb + c->sim_rpr);
   c->sim_steps = c->sim_cd_calls = c->sim_last_conf = c->sim_last_los = 0;
   c->sim_gathered = true;
   if (c->feed_pending) {  // a snapshot of the previous sim is dropped
     BSA_HIP(c, hipEventSynchronize(c->feed_ev));
     c->feed_pending = false;
   }
+  c->home = true;
   c->sim_ready = true;
   return 0;
 }
@@ -447,9 +530,9 @@ int bsa_sim_set_limits(bsa_ctx *cc, const double *hmax, const double *vmin, cons
     if (!q) return bsa::fail(c, "bsa_sim_set_limits: NULL envelope array");
   const size_t N8 = (size_t)c->n * 8;
   if (!bsa::ensure(c, c->s_env, 6 * N8, "OpenAP envelope")) return -1;
+  std::vector<char> tmp;
   for (int k = 0; k < 6; ++k)
-    BSA_HIP(c, hipMemcpyAsync((char *)c->s_env.p + k * N8, src[k], N8, hipMemcpyHostToDevice, c->stream));
-  BSA_HIP(c, hipStreamSynchronize(c->stream));
+    if (bsa::put_home(c, (char *)c->s_env.p + k * N8, src[k], 8, tmp)) return -1;
   c->sim_limits = true;
   return 0;
 }
@@ -478,7 +561,8 @@ int bsa_sim_set_perf(bsa_ctx *cc, int64_t ntypes, const double *table, const int
       !bsa::ensure(c, c->s_phase, (size_t)n, "flight phase"))
     return -1;
   BSA_HIP(c, hipMemcpyAsync(c->s_ptab.p, table, tb, hipMemcpyHostToDevice, c->stream));
-  BSA_HIP(c, hipMemcpyAsync(c->s_ptype.p, type_idx, (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  std::vector<char> tmp;
+  if (bsa::put_home(c, c->s_ptype.p, type_idx, 4, tmp)) return -1;
   BSA_HIP(c, hipMemsetAsync(c->s_phase.p, 0, (size_t)n, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   c->sim_perf = true;
@@ -491,14 +575,12 @@ int bsa_sim_read_perf(bsa_ctx *cc, uint8_t *phase, double *ax) {
   if (!c) return -1;
   if (!c->sim_ready) return bsa::fail(c, "bsa_sim_read_perf before bsa_sim_init");
   BSA_HIP(c, hipSetDevice(c->device));
-  const int64_t rb = c->sim_rb, nr = c->sim_re - c->sim_rb;
+  std::vector<char> tmp;
   if (phase) {
     if (!c->sim_perf) return bsa::fail(c, "no flight phase: bsa_sim_set_perf is off");
-    if (nr > 0) BSA_HIP(c, hipMemcpyAsync(phase + rb, (uint8_t *)c->s_phase.p + rb, nr, hipMemcpyDeviceToHost, c->stream));
+    if (bsa::get_home(c, phase, c->s_phase.p, 1, c->sim_rb, c->sim_re, tmp)) return -1;
   }
-  if (ax && nr > 0)
-    BSA_HIP(c, hipMemcpyAsync(ax + rb, (double *)c->s_ax.p + rb, (size_t)nr * 8, hipMemcpyDeviceToHost, c->stream));
-  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  if (ax && bsa::get_home(c, ax, c->s_ax.p, 8, c->sim_rb, c->sim_re, tmp)) return -1;
   return 0;
 }
 
@@ -508,7 +590,6 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
   if (!s) return bsa::fail(c, "NULL sim state");
   if (!c->sim_ready) return bsa::fail(c, "bsa_sim_update before bsa_sim_init");
   BSA_HIP(c, hipSetDevice(c->device));
-  const size_t N8 = (size_t)c->n * 8;
   struct {
     const double *src;
     void *dst;
@@ -519,14 +600,14 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
             {s->ap_alt, c->s_apalt.p}, {s->ap_vs, c->s_apvs.p},   {s->selalt, c->s_selalt.p},
             {s->bank, c->s_bank.p},    {s->eps, c->s_eps.p},      {s->accel, c->s_accel.p},
             {s->asas_alt, c->s_aalt.p}};
-  // the replicated CD inputs are rewritten on every rank
+  // the replicated CD inputs are rewritten on every rank (in the sim's home order)
   bool any_cd = false;
+  std::vector<char> tmp;
   for (int k = 0; k < 19; ++k) {
     if (!cp[k].src) continue;
     if (k < 10) any_cd = true;
-    BSA_HIP(c, hipMemcpyAsync(cp[k].dst, cp[k].src, N8, hipMemcpyHostToDevice, c->stream));
+    if (bsa::put_home(c, cp[k].dst, cp[k].src, 8, tmp)) return -1;
   }
-  BSA_HIP(c, hipStreamSynchronize(c->stream));
   if (any_cd) {
     c->sim_gathered = true;     // every rank passed the same full arrays
     c->reuse_valid = false;     // a state jump rebuilds any reused candidate list
@@ -540,20 +621,19 @@ int bsa_sim_read(bsa_ctx *cc, bsa_sim_out *o) {
   if (!c->sim_ready) return bsa::fail(c, "bsa_sim_read before bsa_sim_init");
   BSA_HIP(c, hipSetDevice(c->device));
   if (bsa::sim_gather(c) || bsa::sim_gather_asas(c)) return -1;
-  const size_t N8 = (size_t)c->n * 8;
   struct {
     void *dst;
     const void *src;
-    size_t bytes;
-  } cp[] = {{o->lat, c->own[0].p, N8},      {o->lon, c->own[1].p, N8},      {o->alt, c->own[4].p, N8},
-            {o->tas, c->s_tas.p, N8},       {o->hdg, c->s_hdg.p, N8},       {o->vs, c->own[5].p, N8},
-            {o->gs, c->own[3].p, N8},       {o->trk, c->own[2].p, N8},      {o->gseast, c->s_gse.p, N8},
-            {o->gsnorth, c->s_gsn.p, N8},   {o->asas_trk, c->s_atrk.p, N8}, {o->asas_tas, c->s_atas.p, N8},
-            {o->asas_vs, c->s_avs.p, N8},   {o->asas_alt, c->s_aalt.p, N8},
-            {o->active, c->s_active.p, (size_t)c->n}};
+    size_t esz;
+  } cp[] = {{o->lat, c->own[0].p, 8},      {o->lon, c->own[1].p, 8},      {o->alt, c->own[4].p, 8},
+            {o->tas, c->s_tas.p, 8},       {o->hdg, c->s_hdg.p, 8},       {o->vs, c->own[5].p, 8},
+            {o->gs, c->own[3].p, 8},       {o->trk, c->own[2].p, 8},      {o->gseast, c->s_gse.p, 8},
+            {o->gsnorth, c->s_gsn.p, 8},   {o->asas_trk, c->s_atrk.p, 8}, {o->asas_tas, c->s_atas.p, 8},
+            {o->asas_vs, c->s_avs.p, 8},   {o->asas_alt, c->s_aalt.p, 8},
+            {o->active, c->s_active.p, 1}};
+  std::vector<char> tmp;
   for (auto &e : cp)
-    if (e.dst) BSA_HIP(c, hipMemcpyAsync(e.dst, e.src, e.bytes, hipMemcpyDeviceToHost, c->stream));
-  BSA_HIP(c, hipStreamSynchronize(c->stream));
+    if (e.dst && bsa::get_home(c, e.dst, e.src, e.esz, 0, c->n, tmp)) return -1;
   return 0;
 }
 
@@ -574,6 +654,28 @@ int bsa_sim_stats(bsa_ctx *cc, int64_t *out6) {
   out6[3] = c->sim_last_los;
   out6[4] = c->sim_rb;
   out6[5] = c->sim_re;
+  return 0;
+}
+
+int bsa_sim_detect_rows(bsa_ctx *cc, int64_t row_begin, int64_t row_end, int64_t *n_conf, int64_t *n_los) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !n_conf || !n_los) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_detect_rows before bsa_sim_init");
+  if (row_begin % bsa::kTile != 0) return bsa::fail(c, "row_begin must be a multiple of %d", bsa::kTile);
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (bsa::sim_gather(c)) return -1;
+  c->det_home = true;
+  const int r = bsa::detect(c, c->simp.rpz, c->simp.hpz, c->simp.tla, 0, row_begin, row_end, n_conf, n_los);
+  c->det_home = false;
+  return r;
+}
+
+int bsa_sim_row_ids(bsa_ctx *cc, int32_t *ids) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !ids) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_row_ids before bsa_sim_init");
+  const int64_t rb = c->sim_rb, nr = c->sim_re - c->sim_rb;
+  for (int64_t r = 0; r < nr; ++r) ids[c->lpos_h[(size_t)r]] = (int32_t)c->h2id_h[(size_t)(rb + r)];
   return 0;
 }
 
@@ -616,10 +718,17 @@ int bsa_sim_resopairs(bsa_ctx *cc, int32_t *idx1, int32_t *idx2, int64_t cap, in
   std::vector<unsigned> col((size_t)total);
   BSA_HIP(c, hipMemcpyAsync(col.data(), c->bk_rcol.p, (size_t)total * 4, hipMemcpyDeviceToHost, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
-  for (int64_t r = 0; r < nr; ++r)
-    for (unsigned k = ptr[(size_t)r]; k < ptr[(size_t)r + 1]; ++k) {
-      idx1[k] = (int32_t)(c->last_rb + r);
-      idx2[k] = (int32_t)col[k];
+  // rows in ascending aircraft index (each row's columns are ascending, a
+  // deleted intruder's marker last)
+  std::vector<unsigned> ord((size_t)nr);
+  for (int64_t r = 0; r < nr; ++r) ord[(size_t)r] = (unsigned)r;
+  const unsigned *H = c->h2id_h.data() + c->last_rb;
+  std::sort(ord.begin(), ord.end(), [&](unsigned a, unsigned b) { return H[a] < H[b]; });
+  int64_t at = 0;
+  for (unsigned r : ord)
+    for (unsigned k = ptr[r]; k < ptr[r + 1]; ++k, ++at) {
+      idx1[at] = (int32_t)H[r];
+      idx2[at] = (int32_t)col[k];
     }
   return 0;
 }

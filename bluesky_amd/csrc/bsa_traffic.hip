@@ -83,6 +83,10 @@ static std::vector<PerAc> per_aircraft(Ctx *c) {
 
 static int check_sim(Ctx *c, const char *what) {
   if (!c->sim_ready) return fail(c, "%s before bsa_sim_init", what);
+  if (c->feed_pending) {  // a requested ACDATA snapshot is dropped: its rows are re-laid out
+    BSA_HIP(c, hipEventSynchronize(c->feed_ev));
+    c->feed_pending = false;
+  }
   if (c->nranks > 1) return fail(c, "%s with several ranks: re-init the sim (rows would move between GPUs)", what);
   if (c->bk_ready && (c->last_rb != 0 || c->last_re != c->n))
     return fail(c, "%s: the last detect on this context did not cover the sim's rows", what);
@@ -160,9 +164,21 @@ int bsa_sim_delete(bsa_ctx *cc, int64_t k, const int64_t *idx) {
     }
   }
   const int64_t nn = n - (int64_t)d.size();
+  // the arrays are in home order: old home -> new home (the kept homes keep
+  // their order), and the new home -> index map
+  std::vector<int> nh((size_t)n);
+  std::vector<unsigned> h2id_new((size_t)nn);
+  {
+    int run = 0;
+    for (int64_t h = 0; h < n; ++h) {
+      const int id = nid[c->h2id_h[(size_t)h]];
+      nh[(size_t)h] = id < 0 ? -1 : run;
+      if (id >= 0) h2id_new[(size_t)run++] = (unsigned)id;
+    }
+  }
   bsa::DevBuf map;
   if (!bsa::ensure(c, map, (size_t)n * 4, "delete map")) return -1;
-  BSA_HIP(c, hipMemcpyAsync(map.p, nid.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  BSA_HIP(c, hipMemcpyAsync(map.p, nh.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
   // gather every per-aircraft array into a fresh buffer, then swap
   std::vector<bsa::PerAc> arrs = bsa::per_aircraft(c);
   struct Fresh {  // released unless swapped in (error paths)
@@ -206,7 +222,8 @@ int bsa_sim_delete(bsa_ctx *cc, int64_t k, const int64_t *idx) {
     fresh[a] = bsa::DevBuf{};
   }
   // ASAS bookkeeping (asas.py:409-504): remap the CSRs of the resopairs and
-  // of the previous call's conflict / LoS pairs (rows = all n on one rank)
+  // of the previous call's conflict / LoS pairs (rows = all n homes on one
+  // rank, columns = aircraft indices)
   if (c->bk_ready) {
     std::vector<unsigned> p, q, np, nq;
     auto remap = [&](bsa::DevBuf &ptr, bsa::DevBuf &col, bool dangling, size_t colcap, const char *what) -> int {
@@ -214,7 +231,7 @@ int bsa_sim_delete(bsa_ctx *cc, int64_t k, const int64_t *idx) {
       np.assign(1, 0u);
       nq.clear();
       for (int64_t o = 0; o < n; ++o) {
-        if (nid[(size_t)o] < 0) continue;  // ownship deleted: its pairs go (asas.py:421-423)
+        if (nh[(size_t)o] < 0) continue;  // ownship deleted: its pairs go (asas.py:421-423)
         bool dang = false;
         for (unsigned e = p[(size_t)o]; e < p[(size_t)o + 1]; ++e) {
           const unsigned j = q[e];
@@ -235,7 +252,8 @@ int bsa_sim_delete(bsa_ctx *cc, int64_t k, const int64_t *idx) {
       return -1;
   }
   bsa::set_n(c, nn);
-  return 0;
+  c->h2id_h = h2id_new;
+  return bsa::set_home_maps(c);
 }
 
 int bsa_sim_create(bsa_ctx *cc, int64_t m, const bsa_sim_state *s) {
@@ -292,7 +310,9 @@ int bsa_sim_create(bsa_ctx *cc, int64_t m, const bsa_sim_state *s) {
     }
   }
   bsa::set_n(c, nn);
-  return 0;
+  // the new aircraft take the homes after the existing ones, in index order
+  for (int64_t k = n; k < nn; ++k) c->h2id_h.push_back((unsigned)k);
+  return bsa::set_home_maps(c);
 }
 
 }  // extern "C"

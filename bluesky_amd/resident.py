@@ -5,8 +5,10 @@ CD + MVP every ``cd_every`` steps (asas.update, asas.py:473-504, with
 ``asas.active = inconf`` standing in for ResumeNav, or with ``resume_nav`` the
 device-side resopairs bookkeeping + ResumeNav), then Pilot.APorASAS
 (no wind) fused with the kinematic update (traffic.py:397-409).
-With several ranks (one process per GPU) each rank owns a contiguous row
-block and the replicated state is all-gathered over RCCL before each CD.
+State is kept on the device in home order (the spatial order of the initial
+traffic); arrays cross the API in aircraft-index order.  With several ranks
+(one process per GPU) each rank owns a contiguous, spatially compact range of
+home rows and the replicated state is all-gathered over RCCL before each CD.
 """
 import numpy as np
 
@@ -125,6 +127,10 @@ class ResidentSim:
 
     def resopairs(self):
         return self.ctx.sim_resopairs()
+
+    def row_ids(self):
+        """Aircraft indices of this rank's rows (ascending)."""
+        return self.ctx.sim_row_ids()
 
     def gather_pairs(self, root=0):
         """C2: the last CD call's pairs of all ranks, on ``root`` (collective)."""

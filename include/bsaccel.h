@@ -320,7 +320,13 @@ int bsa_gather_pairs(bsa_ctx *ctx, int root, const bsa_pairs_out *out);
  *                         bookkeeping + ResumeNav (asas.py:409-504) on the device
  *   every step:           Pilot.APorASAS (pilot.py:28-63, winddim 0/1) fused with
  *                         UpdateAirSpeed/GroundSpeed/Position (traffic.py:425-483)
- * AP targets, selalt, bank, eps and perf.acceleration() are frozen inputs. */
+ * AP targets, selalt, bank, eps and perf.acceleration() are frozen inputs.
+ * Every array crosses this ABI in aircraft-index order.  On the device the
+ * sim keeps them in HOME order (the spatial order of the state at
+ * bsa_sim_init): rank r owns the home range [row_begin, row_end) of
+ * bsa_sim_stats (512-aligned, spatially compact), whose aircraft indices
+ * bsa_sim_row_ids lists; "this rank's rows" below are those aircraft, in
+ * ascending index (all of 0..n-1 with one rank). */
 typedef struct bsa_sim_params {
   double simdt, rpz, hpz, tla;
   int32_t cd_every; /* >= 1: CD + MVP every k steps (1 = DTNOLOOK=simdt, 20 = asas_dt/simdt) */
@@ -378,7 +384,7 @@ int bsa_sim_set_limits(bsa_ctx *ctx, const double *hmax, const double *vmin, con
  * (validated).  Takes precedence over bsa_sim_set_limits; table == NULL
  * switches it off (the default after bsa_sim_init). */
 int bsa_sim_set_perf(bsa_ctx *ctx, int64_t ntypes, const double *table, const int32_t *type_idx);
-/* This rank's rows [row_begin, row_end) of the flight phase of the last step
+/* This rank's rows of the flight phase of the last step
  * (0..8, phase.py:4-12; needs bsa_sim_set_perf) and of traf.ax, written into
  * full-n host arrays; either pointer may be NULL. */
 int bsa_sim_read_perf(bsa_ctx *ctx, uint8_t *phase, double *ax);
@@ -409,8 +415,18 @@ int bsa_sim_delete(bsa_ctx *ctx, int64_t k, const int64_t *idx);
  * Any pointer may be NULL. */
 int bsa_sim_read(bsa_ctx *ctx, bsa_sim_out *o);
 /* [0] steps done, [1] CD calls, [2] conflicts and [3] LoS pairs of the last
- * CD call (this rank's rows), [4] this rank's row_begin, [5] row_end. */
+ * CD call (this rank's rows), [4] this rank's row_begin, [5] row_end (its home
+ * range: row_end - row_begin rows; (0, n) with one rank). */
 int bsa_sim_stats(bsa_ctx *ctx, int64_t *out6);
+/* The aircraft indices of this rank's rows, ascending (row_end - row_begin
+ * entries): the rows of bsa_sim_acdata_poll's arrays, of bsa_fetch_pairs'
+ * inconf / tcpamax after resident steps, and of bsa_sim_read_perf. */
+int bsa_sim_row_ids(bsa_ctx *ctx, int32_t *ids);
+/* Measurement aid: the sim's detect (home order, its rpz / hpz / tla) of the
+ * home rows [row_begin, row_end) (row_begin a multiple of 512) against all
+ * columns -- one rank's share of a CD step, on one GPU.  The pairs are
+ * fetchable like a bsa_detect's; the sim's own state is not changed. */
+int bsa_sim_detect_rows(bsa_ctx *ctx, int64_t row_begin, int64_t row_end, int64_t *n_conf, int64_t *n_los);
 /* ASAS bookkeeping after the last CD call (resume_nav = 1; replaces
  * ASAS.update's Python sets, asas.py:490-502):
  * [0] |resopairs| of this rank's rows, [1] |confpairs_unique|,
@@ -419,7 +435,7 @@ int bsa_sim_stats(bsa_ctx *ctx, int64_t *out6);
  * the global pair sets (every rank gathers all ranks' pair keys; the same
  * values on every rank). */
 int bsa_sim_asas_stats(bsa_ctx *ctx, int64_t *out6);
-/* This rank's resopairs (idx1 ascending, then idx2; idx2 = -1, last in its
+/* This rank's resopairs (aircraft indices; idx1 ascending, then idx2; idx2 = -1, last in its
  * row, for an intruder deleted since the last CD call), at most cap pairs;
  * *count = total (call again with a larger buffer when *count > cap). */
 int bsa_sim_resopairs(bsa_ctx *ctx, int32_t *idx1, int32_t *idx2, int64_t cap, int64_t *count);

@@ -1,0 +1,45 @@
+"""Per-rank detect cost of a row-sharded CD step, probed on one GPU: the stage
+times of the resident sim's detect of each rank's home rows (a 512-aligned,
+spatially compact slice, bsa_sim_detect_rows) against all N columns, for
+R = 1, 2, 4, 8, on the box100k and global1m workloads.  Reports the slowest
+rank's stages (the step waits for it).
+Usage: python tools/rowslice_probe.py [workload ...]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bluesky_amd import _lib, resident, synth  # noqa: E402
+
+
+def main():
+    names = sys.argv[1:] or ['box100k', 'global1m']
+    ctx = _lib.Context(0)
+    ctx.set_timing_sample(1)
+    for name in names:
+        t = synth.workload(name)
+        n = t.ntraf
+        sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
+        for R in (1, 2, 4, 8):
+            rpr = ((n + R - 1) // R + 511) // 512 * 512
+            worst = None
+            for r in range(R):
+                rb, re = min(n, r * rpr), min(n, (r + 1) * rpr)
+                if re <= rb:
+                    continue
+                for _ in range(2):
+                    ctx.sim_detect_rows(rb, re)
+                ctx.timing_reset()
+                for _ in range(6):
+                    ctx.sim_detect_rows(rb, re)
+                tm, ts = ctx.timing_summary()
+                d = max(ts['detects'], 1)
+                row = dict(rank=r, rows=re - rb, ms={k: round(v, 4) for k, v in tm.items()},
+                           tiles=ts['tiles'] / d, groups=ts['groups'] / d, candidates=ts['candidates'] / d)
+                if worst is None or tm['total'] > worst['ms']['total']:
+                    worst = row
+            print(name, 'R=%d' % R, json.dumps(worst), flush=True)
+
+
+if __name__ == '__main__':
+    main()
