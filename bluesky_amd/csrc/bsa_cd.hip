@@ -789,6 +789,15 @@ __global__ __launch_bounds__(256) void k_items(int nrows, int ncols, const TileB
   }
 }
 
+// Diagnostic item timeline (build with -DBSA_PF_TRACE; `make trace`,
+// tools/pf_trace.py): per work item {item, wave << 8 | sub-groups, start,
+// end} (s_memrealtime, 100 MHz) into a per-wave region of pf_trace (no
+// atomics), dumped by detect_finish to $BSA_PF_TRACE_FILE.
+#ifdef BSA_PF_TRACE
+__device__ unsigned long long *pf_trace;
+constexpr unsigned long long kTraceRecs = 1ull << 21;
+constexpr unsigned kTraceWave = 256;
+#endif
 // Diagnostic phase timers (build with -DBSA_PF_STAMPS; `make stamps`):
 // cycles per wave spent in 0 dequeue/setup, 1 stage 1, 2 refine drains,
 // 3 flushes, summed over waves into Counters::stamp.
@@ -927,6 +936,9 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef BSA_PF_TRACE
+  unsigned tr_n = 0;
+#endif
   for (;;) {
     unsigned long long item;
     {
@@ -935,6 +947,10 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       item = wave_bcast_u64(m0) * kn.shards + shard;
     }
     if (item >= nitems) break;
+#ifdef BSA_PF_TRACE
+    const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
+    unsigned tr_subs = 0;
+#endif
     do {  // one item; `break` ends it
 #ifndef PF_XCD_ITEMS
 #define PF_XCD_ITEMS 1
@@ -950,6 +966,9 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     unsigned long long gm = masks[tp * PF_ITEMS_PER_TILE + slice];
     if (!gm) break;
     subs += (unsigned)__popcll(gm);
+#ifdef BSA_PF_TRACE
+    tr_subs = (unsigned)__popcll(gm);
+#endif
 
     // the next batch = the first kSubsPerBatch remaining sub-groups (ascending):
     // lane b holding the r-th set bit of m (r < 8, r = set bits below b) posts
@@ -1190,6 +1209,18 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 #endif
     if (PF_ITEM_FLUSH && n2) flush2();
     } while (0);
+#ifdef BSA_PF_TRACE
+    if (lane == 0 && pf_trace) {  // per-wave record region (no atomics)
+      const unsigned long long slot = ((unsigned long long)blockIdx.x * PF_WAVES + w) * kTraceWave + tr_n++;
+      if (tr_n <= kTraceWave && slot < kTraceRecs) {
+        unsigned long long *t = pf_trace + 4 * slot;
+        t[0] = item;
+        t[1] = ((unsigned long long)blockIdx.x << 2 | w) << 8 | tr_subs;
+        t[2] = tr0;
+        t[3] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+#endif
   }
   PF_STAMP(0);
   if (n2) flush2();
@@ -1916,6 +1947,18 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     if (z.shards < 1 || z.shards > kWorkShards || (z.shards & (z.shards - 1))) z.shards = kWorkShards;
     return z;
   }();
+#ifdef BSA_PF_TRACE
+  {
+    static DevBuf tb;
+    const size_t need = (size_t)kTraceRecs * 32;
+    if (!ensure(c, tb, need, "prefilter trace")) return -1;
+    BSA_HIP(c, hipMemsetAsync(tb.p, 0, need, c->stream));
+    void *pt = tb.p;
+    BSA_HIP(c, hipMemcpyToSymbolAsync(HIP_SYMBOL(pf_trace), &pt, sizeof pt, 0, hipMemcpyHostToDevice, c->stream));
+    c->trace_buf = tb.p;
+    c->trace_bytes = need;
+  }
+#endif
   const unsigned pf_grid = (unsigned)std::max<long long>(
       kWorkShards, std::min<long long>(ntp * PF_ITEMS_PER_TILE / PF_WAVES + 1, 256 * PF_BLOCKS_PER_CU));
   if (noprune)
@@ -2007,6 +2050,18 @@ int detect_finish(Ctx *c, bool *retry) {
   c->last_conf = (int64_t)h.conf;
   c->last_los = (int64_t)h.los;
   c->have_pairs = true;
+#ifdef BSA_PF_TRACE
+  if (const char *fn = getenv("BSA_PF_TRACE_FILE")) {
+    std::vector<unsigned long long> t(kTraceRecs * 4);
+    BSA_HIP(c, hipMemcpy(t.data(), c->trace_buf, t.size() * 8, hipMemcpyDeviceToHost));
+    if (FILE *f = fopen(fn, "ab")) {
+      const unsigned long long hdr[4] = {0xfeedull, (unsigned long long)(t.size() / 4), h.groups, h.tiles};
+      fwrite(hdr, 8, 4, f);
+      fwrite(t.data(), 8, t.size(), f);
+      fclose(f);
+    }
+  }
+#endif
 #ifdef BSA_PF_STAMPS
   fprintf(stderr, "[bsa stamps] prefilter wave-cycles: setup %.4g stage1 %.4g drain %.4g flush %.4g | "
           "stage-1 survivors %.4g refine rounds %.4g batches %.4g enqueue trips %.4g\n",

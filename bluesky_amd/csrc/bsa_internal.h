@@ -198,6 +198,8 @@ struct Ctx {
   bool ev_valid = false;
   bool empty_detect = false;
   DevBuf stats;  // accumulated per-detect statistics {groups, candidates, tiles, detects, list builds}
+  void *trace_buf = nullptr;  // diagnostic builds (-DBSA_PF_TRACE): prefilter item timeline
+  size_t trace_bytes = 0;
 
   // MVP / kinematics staging (host-buffer entry points)
   DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl;

@@ -1,0 +1,74 @@
+"""Prefilter item timeline (diagnostic build `make trace`, libbsaccel_trace.so).
+
+run:     BSACCEL_LIB=.../libbsaccel_trace.so BSA_PF_TRACE_FILE=f python tools/pf_trace.py run WORKLOAD [ROWS_DIV]
+analyse: python tools/pf_trace.py show f
+
+`run` steps the resident sim (home order) a few times and, with ROWS_DIV = R,
+also detects rank 0's home slice of R ranks; every detect appends one record
+set.  `show` prints, per detect: the kernel span (first item start -> last
+item end), the item-duration distribution, when the waves ran dry (the tail),
+and the busiest waves."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(name, div):
+    from bluesky_amd import _lib, resident, synth
+    t = synth.workload(name)
+    ctx = _lib.Context(0)
+    sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
+    sim.step(3)
+    n = t.ntraf
+    rpr = ((n + div - 1) // div + 511) // 512 * 512
+    for _ in range(2):
+        ctx.sim_detect_rows(0, min(n, rpr))
+    ctx.sync()
+
+
+def show(fn):
+    raw = np.fromfile(fn, dtype=np.uint64)
+    k = 0
+    det = 0
+    while k < len(raw):
+        assert raw[k] == 0xfeed
+        m, groups, tiles = int(raw[k + 1]), int(raw[k + 2]), int(raw[k + 3])
+        rec = raw[k + 4:k + 4 + 4 * m].reshape(m, 4)
+        k += 4 + 4 * m
+        rec = rec[rec[:, 3] > 0]
+        t0 = rec[:, 2].min()
+        st = (rec[:, 2] - t0) / 100.0     # us (100 MHz)
+        en = (rec[:, 3] - t0) / 100.0
+        dur = en - st
+        subs = (rec[:, 1] & 0xff).astype(np.int64)
+        wave = (rec[:, 1] >> 8).astype(np.int64)
+        span = en.max()
+        print('detect %d: %d items (%d with work), groups %d, tiles %d, span %.1f us' %
+              (det, len(rec), int((subs > 0).sum()), groups, tiles, span))
+        q = np.percentile(dur, [50, 90, 99, 100])
+        print('  item us  p50 %.2f p90 %.2f p99 %.2f max %.2f   (sub-groups of the max item: %d)' %
+              (q[0], q[1], q[2], q[3], subs[np.argmax(dur)]))
+        # per wave: busy time and last end
+        uw, inv = np.unique(wave, return_inverse=True)
+        busy = np.bincount(inv, weights=dur)
+        last = np.zeros(len(uw))
+        np.maximum.at(last, inv, en)
+        print('  waves %d: busy us p50 %.1f max %.1f; last end p10 %.1f p50 %.1f p90 %.1f max %.1f' %
+              (len(uw), np.median(busy), busy.max(), *np.percentile(last, [10, 50, 90, 100])))
+        for frac in (0.5, 0.9, 0.99):
+            print('  %.0f%% of item-time done by %.1f us' %
+                  (frac * 100, np.interp(frac, np.cumsum(np.sort(dur)[::-1]) / dur.sum(), np.sort(en)) if False else
+                   en[np.argsort(en)][np.searchsorted(np.cumsum(dur[np.argsort(en)]) / dur.sum(), frac)]))
+        starts = np.sort(st)
+        print('  item starts: first %.1f, 50%% by %.1f, last %.1f us' % (starts[0], starts[len(starts) // 2], starts[-1]))
+        det += 1
+
+
+if __name__ == '__main__':
+    if sys.argv[1] == 'run':
+        run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+    else:
+        show(sys.argv[2])
