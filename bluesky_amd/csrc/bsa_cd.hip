@@ -300,11 +300,37 @@ struct FusedBoxes {
   TileBox *sbox, *gbox, *tbox;  // gbox == nullptr: not fused (k_boxes runs)
 };
 
+// fp64 column record of aircraft o: intruder[o] geometry, own[o] velocity /
+// altitude (the per-aircraft factors of StateBasedCD.py's broadcasts)
+__device__ __forceinline__ ColRec col_record(const SoA6 &own, const SoA6 &intr, int o) {
+  const double la = intr.lat[o], lo = intr.lon[o];
+  const double rad = la * kD2R;
+  const double trk = own.trk[o] * kD2R;
+  const double gs = own.gs[o];
+  const double olat = own.lat[o];
+  ColRec c;
+  c.lat = la;
+  c.lon = lo;
+  c.sinlat = sin(rad);
+  c.coslat = cos(rad);
+  c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);  // geo.py:127
+  c.u = gs * sin(trk);                          // StateBasedCD.py:31-32
+  c.v = gs * cos(trk);
+  c.alt = own.alt[o];
+  c.vs = own.vs[o];
+  c.eps = (olat == 0.0) ? 0.000001 : 0.0;      // geo.py:128 (column-indexed)
+  c.olat = olat;
+  for (int q = 0; q < 5; ++q) c.pad[q] = 0.0;
+  return c;
+}
+
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
-// Workgroup = kTile lanes (one tile of sorted records).
+// Workgroup = kTile lanes (one tile of sorted records).  rec = 0 (the
+// resident sim's home order): the fp64 records are not stored -- K1b builds
+// the few it needs from the state arrays with col_record itself.
 // presorted: the state arrays are already in sorted (home) order, perm only
 // names the aircraft (the resident sim): record k reads index k, coalesced.
-__global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__restrict__ perm, int presorted,
+__global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__restrict__ perm, int presorted, int rec,
                                                      SoA6 own, SoA6 intr, int distinct, int shared,
                                                      double rpz, double hpz, double tla,
                                                      ColRec *__restrict__ C, PFRec *__restrict__ PC,
@@ -318,26 +344,9 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
   if (k < cnt) {
     const int o = presorted ? k : (int)perm[k];
     const double tlap = tla > 0.0 ? tla : 0.0;
-    const double la = intr.lat[o], lo = intr.lon[o];
-    const double rad = la * kD2R;
-    const double sinl = sin(rad), cosl = cos(rad);
-    const double trk = own.trk[o] * kD2R;
-    const double gs = own.gs[o];
-    const double olat = own.lat[o];
-    ColRec c;
-    c.lat = la;
-    c.lon = lo;
-    c.sinlat = sinl;
-    c.coslat = cosl;
-    c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);
-    c.u = gs * sin(trk);                           // StateBasedCD.py:31-32
-    c.v = gs * cos(trk);
-    c.alt = own.alt[o];
-    c.vs = own.vs[o];
-    c.eps = (olat == 0.0) ? 0.000001 : 0.0;       // geo.py:128 (column-indexed)
-    c.olat = olat;
-    for (int q = 0; q < 5; ++q) c.pad[q] = 0.0;
-    C[k] = c;
+    const ColRec c = col_record(own, intr, o);
+    if (rec) C[k] = c;
+    const double lo = c.lon, sinl = c.sinlat, cosl = c.coslat, gs = own.gs[o], olat = c.olat;
     const double lor = lo * kD2R;
     // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
     // when own != intruder (geo.py:128): never prune such a column horizontally
@@ -582,12 +591,18 @@ __device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileB
 // ("near": a row tile against itself and its neighbours, the costly items)
 // from the front of the list, the others from its back (cap - 1 - k), so the
 // sweep dequeues the near pairs first -- longest items first keeps the tail of
-// the dynamic schedule short (measured -5 us at box100k).  Each thread
-// classifies kTPPer consecutive candidate pairs; one returning atomic per
-// class and 1024-thread workgroup (a returning atomic on one word saturates
-// at ~88 per us, MI355X_MICROARCH 'dequeue').
+// the dynamic schedule short (measured -5 us at box100k).
+// Two-level: a workgroup takes one SUPER row (kSuper row tiles), tests its
+// union box against every super column's (kSuper column tiles) and only
+// expands the kept super pairs into tile pairs: at 1M aircraft ~1 % of the
+// (N/512)^2 tile pairs survive, so testing them all (3.8 M box pairs) cost
+// 42 us.  A union box is a superset of its tiles' boxes and
+// boxes_may_interact is monotone in the extents, so no kept tile pair is
+// lost.  One returning atomic per class and expansion round of the
+// workgroup (a returning atomic on one word saturates at ~88 per us,
+// MI355X_MICROARCH 'dequeue').
 constexpr int kTPThreads = 1024;
-constexpr int kTPPerMax = 8;  // candidate pairs per thread (fewer when there are few: parallelism)
+constexpr int kSuper = 8;  // tiles per super tile (each side)
 __device__ __forceinline__ uint2 tile_at(const uint2 *__restrict__ list, unsigned long long k,
                                          unsigned long long near, unsigned long long cap) {
   return list[k < near ? k : cap - 1 - (k - near)];
@@ -595,52 +610,85 @@ __device__ __forceinline__ uint2 tile_at(const uint2 *__restrict__ list, unsigne
 __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, const TileBox *__restrict__ rb,
                                                           const TileBox *__restrict__ cb, int noprune,
                                                           uint2 *__restrict__ out, unsigned long long cap,
-                                                          Counters *__restrict__ cnt, int kTPPer,
+                                                          Counters *__restrict__ cnt,
                                                           const unsigned *__restrict__ build) {
   if (build && !build[0]) return;
-  __shared__ unsigned wpre[2][kTPThreads / 64];
+  __shared__ TileBox srt[kSuper];            // this super row's tile boxes
+  __shared__ unsigned keep[kTPThreads];      // kept super columns of the chunk
+  __shared__ unsigned wpre[3][kTPThreads / 64];
   __shared__ unsigned long long bbase[2];
-  const long long total = (long long)nrt * nct;
-  const long long id0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * kTPPer;
-  unsigned kn = 0, kf = 0;  // bit q: candidate id0 + q kept as near / far
-  for (int q = 0; q < kTPPer; ++q) {
-    const long long id = id0 + q;
-    if (id >= total) break;
-    const int rt = (int)(id / nct), ct = (int)(id % nct);
-    const TileBox a = rb[rt], b = cb[ct];
-    if (!(noprune || boxes_may_interact(a, b))) continue;
-    const bool near = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]) == 0.f &&
-                      gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]) == 0.f &&
-                      gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]) == 0.f;
-    if (near) kn |= 1u << q; else kf |= 1u << q;
-  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned cn = (unsigned)__popc(kn), cf = (unsigned)__popc(kf);
-  const unsigned xn = wave_incl_scan(cn), xf = wave_incl_scan(cf);
-  if (lane == 63) {
-    wpre[0][w] = xn;
-    wpre[1][w] = xf;
-  }
+  const int rt0 = blockIdx.x * kSuper, nr = min(kSuper, nrt - rt0);
+  if (threadIdx.x < nr) srt[threadIdx.x] = rb[rt0 + threadIdx.x];
   __syncthreads();
-  if (threadIdx.x < 2) {
-    unsigned run = 0;
-    for (int q = 0; q < kTPThreads / 64; ++q) {
-      const unsigned v = wpre[threadIdx.x][q];
-      wpre[threadIdx.x][q] = run;
-      run += v;
+  TileBox sr = srt[0];
+  for (int i = 1; i < nr; ++i) sr = box_union(sr, srt[i]);
+  const int nsc = (nct + kSuper - 1) / kSuper;
+  for (int c0 = 0; c0 < nsc; c0 += kTPThreads) {
+    // super columns c0 + threadIdx.x: union box, tested against the super row
+    const int sc = c0 + threadIdx.x;
+    bool kp = false;
+    if (sc < nsc) {
+      const int ct0 = sc * kSuper, nc = min(kSuper, nct - ct0);
+      TileBox u = cb[ct0];
+      for (int j = 1; j < nc; ++j) u = box_union(u, cb[ct0 + j]);
+      kp = noprune || boxes_may_interact(sr, u);
     }
-    unsigned long long *ctr = threadIdx.x == 0 ? &cnt->tiles_near : &cnt->pad[0];
-    bbase[threadIdx.x] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
-    if (run) atomicAdd(&cnt->tiles, (unsigned long long)run);
-  }
-  __syncthreads();
-  unsigned pn = (unsigned)bbase[0] + wpre[0][w] + xn - cn;
-  unsigned pf = (unsigned)bbase[1] + wpre[1][w] + xf - cf;
-  for (int q = 0; q < kTPPer; ++q) {
-    const long long id = id0 + q;
-    const uint2 v = make_uint2((unsigned)(id / nct), (unsigned)(id % nct));
-    if (kn >> q & 1u) out[pn++] = v;
-    if (kf >> q & 1u) out[cap - 1 - pf++] = v;
+    const unsigned x = wave_incl_scan(kp ? 1u : 0u);
+    if (lane == 63) wpre[2][w] = x;
+    __syncthreads();
+    unsigned before = 0, K = 0;
+    for (int q = 0; q < kTPThreads / 64; ++q) {
+      before += q < w ? wpre[2][q] : 0u;
+      K += wpre[2][q];
+    }
+    if (kp) keep[before + x - 1] = (unsigned)sc;
+    __syncthreads();
+    // expansion: K super columns x (nr row tiles x kSuper column tiles)
+    const unsigned ne = K * kSuper * kSuper;
+    for (unsigned e0 = 0; e0 < ne; e0 += kTPThreads) {
+      const unsigned e = e0 + threadIdx.x;
+      bool kn = false, kf = false;
+      int rt = 0, ct = 0;
+      if (e < ne) {
+        const unsigned sc2 = keep[e / (kSuper * kSuper)], r = e % (kSuper * kSuper);
+        const int i = (int)(r / kSuper);
+        rt = rt0 + i;
+        ct = (int)sc2 * kSuper + (int)(r % kSuper);
+        if (i < nr && ct < nct) {
+          const TileBox a = srt[i], b = cb[ct];
+          if (noprune || boxes_may_interact(a, b)) {
+            const bool near = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]) == 0.f &&
+                              gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]) == 0.f &&
+                              gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]) == 0.f;
+            kn = near;
+            kf = !near;
+          }
+        }
+      }
+      const unsigned xn = wave_incl_scan(kn ? 1u : 0u), xf = wave_incl_scan(kf ? 1u : 0u);
+      if (lane == 63) {
+        wpre[0][w] = xn;
+        wpre[1][w] = xf;
+      }
+      __syncthreads();
+      if (threadIdx.x < 2) {
+        unsigned run = 0;
+        for (int q = 0; q < kTPThreads / 64; ++q) {
+          const unsigned v = wpre[threadIdx.x][q];
+          wpre[threadIdx.x][q] = run;
+          run += v;
+        }
+        unsigned long long *ctr = threadIdx.x == 0 ? &cnt->tiles_near : &cnt->pad[0];
+        bbase[threadIdx.x] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
+        if (run) atomicAdd(&cnt->tiles, (unsigned long long)run);
+      }
+      __syncthreads();
+      const uint2 v = make_uint2((unsigned)rt, (unsigned)ct);
+      if (kn) out[bbase[0] + wpre[0][w] + xn - 1] = v;
+      if (kf) out[cap - 1 - (bbase[1] + wpre[1][w] + xf - 1)] = v;
+      __syncthreads();  // wpre / bbase are rewritten by the next round
+    }
   }
 }
 
@@ -1431,7 +1479,7 @@ constexpr int kPayStride = 6;  // doubles per candidate record (cpay): key, qdr,
 __global__ __launch_bounds__(256) void k_exact(
     const RowRec *__restrict__ R, const ColRec *__restrict__ C,
     const unsigned *__restrict__ perm_r, const unsigned *__restrict__ perm_c,
-    const uint2 *__restrict__ cand, const Counters *__restrict__ cnt,
+    const uint2 *__restrict__ cand, const Counters *__restrict__ cnt, SoA6 hs, int recs,
     unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
     unsigned char *__restrict__ cflag, double *__restrict__ cpay, unsigned char *__restrict__ inconf,
     unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int kwik,
@@ -1460,8 +1508,13 @@ __global__ __launch_bounds__(256) void k_exact(
     const unsigned oi = perm_r ? perm_r[p.x] : (unsigned)rb + p.x, oj = perm_c[p.y];
     unsigned char flag = 0;
     if (perm_r ? oi != oj : oi != p.y) {
-      const PairResult o = kwik ? eval_pair<true>(R[p.x], C[p.y], rpz, hpz, tla)
-                                : eval_pair<false>(R[p.x], C[p.y], rpz, hpz, tla);
+      PairResult o;
+      if (!recs) {  // home mode: the records from the state arrays (rows = columns' slice)
+        const ColRec ri = col_record(hs, hs, (int)oi), cj = col_record(hs, hs, (int)p.y);
+        o = eval_pair<false>(reinterpret_cast<const RowRec &>(ri), cj, rpz, hpz, tla);
+      } else {
+        o = kwik ? eval_pair<true>(R[p.x], C[p.y], rpz, hpz, tla) : eval_pair<false>(R[p.x], C[p.y], rpz, hpz, tla);
+      }
       flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
       const int row = (int)oi - rb;
       // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
@@ -1728,6 +1781,10 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // slice [rb, re) of the columns (no re-sort, no gather)
   const bool home = c->det_home;
   c->last_home = home;
+  // home mode: K1b builds its fp64 records from the state arrays (no 128-B
+  // record per aircraft written by K0b) -- BSA_HOME_REC=1 forces the records
+  static const int home_rec_env = getenv("BSA_HOME_REC") ? atoi(getenv("BSA_HOME_REC")) : -1;
+  const bool recs = !home || home_rec_env == 1;
   if (home && (distinct || rb % kTile != 0 || (flags & BSA_FLAG_KWIK)))
     return fail(c, "home-order detect needs own == intruder, a %d-aligned row slice, no KWIK", kTile);
   const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;
@@ -1905,7 +1962,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                   (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p};
   }
   hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, kTile)), dim3(kTile), 0, c->stream, (int)n, perm_c,
-                     home ? 1 : 0, own,
+                     home ? 1 : 0, recs ? 1 : 0, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs);
   BSA_HIP(c, hipGetLastError());
@@ -1923,10 +1980,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
                        (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
   // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
-  const int tpper = (int)std::min<long long>(kTPPerMax, std::max<long long>(1, ntp / (1024LL * kTPThreads)));
-  hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((ntp + (long long)kTPThreads * tpper - 1) / ((long long)kTPThreads * tpper))),
-                     dim3(kTPThreads), 0, c->stream, nrt, nct, tbox_r, (const TileBox *)c->tbox_c.p, noprune,
-                     (uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt, tpper, build);
+  hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
+                     nrt, nct, tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
+                     (unsigned long long)ntp, dcnt, build);
   BSA_HIP(c, hipGetLastError());
   // K0e: per (tile pair, 64-row slice) the mask of interacting column sub-groups
   hipLaunchKernelGGL(k_items, dim3((unsigned)std::min<long long>(2048, (ntp + 3) / 4)), dim3(256), 0,
@@ -1978,7 +2034,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // ---- K1b exact evaluation: grid-stride over the device-side count, one
   // resident round (4 workgroups per CU at its register budget)
   hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
-                     perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, cap, rpz, hpz, tla, (int)rb, (int)nrows,
+                     perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, own, recs ? 1 : 0, cap, rpz, hpz, tla, (int)rb,
+                     (int)nrows,
                      (unsigned char *)c->cflag.p, (double *)c->cpay.p,
                      (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
                      (unsigned *)c->rowcnt.p, kwik, reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
