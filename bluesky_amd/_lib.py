@@ -157,6 +157,7 @@ SIGNATURES.update({
     'bsa_sim_read': (ctypes.c_int, [_vp, ctypes.POINTER(SimOut)]),
     'bsa_sim_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_row_ids': (ctypes.c_int, [_vp, _c_i32p]),
+    'bsa_set_row_bucket': (ctypes.c_int, [_vp, ctypes.c_int]),
     'bsa_sim_detect_rows': (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int64, _c_i64p, _c_i64p]),
     'bsa_sim_asas_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_resopairs': (ctypes.c_int, [_vp, _c_i32p, _c_i32p, ctypes.c_int64, _c_i64p]),
@@ -599,6 +600,10 @@ class Context:
         return dict(steps=int(v[0]), cd_calls=int(v[1]), n_conf=int(v[2]), n_los=int(v[3]),
                     row_begin=int(v[4]), row_end=int(v[5]))
 
+    def set_row_bucket(self, width):
+        """bsa_set_row_bucket: K2's per-row bucket width (0 = scatter into segments)."""
+        self.check(self.lib.bsa_set_row_bucket(self.h, int(width)), 'bsa_set_row_bucket')
+
     def sim_row_ids(self):
         """Aircraft indices of this rank's rows, ascending (bsa_sim_row_ids): the
         rows of acdata / fetch_pairs' inconf and tcpamax after resident steps."""
@@ -614,6 +619,7 @@ class Context:
         self.check(self.lib.bsa_sim_detect_rows(self.h, int(row_begin), int(row_end), ctypes.byref(nc),
                                                 ctypes.byref(nl)), 'bsa_sim_detect_rows')
         self.gen += 1
+        self._rows = (int(row_begin), int(row_end))
         return nc.value, nl.value
 
     def sim_asas_stats(self):

@@ -1400,7 +1400,7 @@ __device__ __forceinline__ unsigned long long cand_prefix(const Counters *cnt, u
 }
 __device__ __forceinline__ bool cand_overflow(const Counters *cnt, unsigned long long cap) {
   const unsigned long long ccap = cap / kCandShards;
-  bool o = false;
+  bool o = cnt->k2_demand != 0;  // a K2 row bucket was full: retried with wider buckets
 #pragma unroll
   for (int q = 0; q < kCandShards; ++q) o |= cnt->cshard[q][0] > ccap;
   return o;
@@ -1479,10 +1479,11 @@ constexpr int kPayStride = 6;  // doubles per candidate record (cpay): key, qdr,
 __global__ __launch_bounds__(256) void k_exact(
     const RowRec *__restrict__ R, const ColRec *__restrict__ C,
     const unsigned *__restrict__ perm_r, const unsigned *__restrict__ perm_c,
-    const uint2 *__restrict__ cand, const Counters *__restrict__ cnt, SoA6 hs, int recs,
+    const uint2 *__restrict__ cand, Counters *__restrict__ cnt, SoA6 hs, int recs,
     unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
     unsigned char *__restrict__ cflag, double *__restrict__ cpay, unsigned char *__restrict__ inconf,
-    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, int kwik,
+    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, unsigned *__restrict__ kb,
+    int B, int kwik,
     unsigned *__restrict__ rctl, const Snap *__restrict__ snap_cur, Snap *__restrict__ snap_build, int nsnap) {
   if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
   if (rctl) {  // reuse: after a build this detect's state becomes the snapshot
@@ -1531,9 +1532,23 @@ __global__ __launch_bounds__(256) void k_exact(
         // positive tcpa can raise it, and positive doubles order as integers.
         if (o.tcpa > 0.0)
           atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
-        atomicAdd(&rowcnt[row], 1u);
+        if (B) {  // row bucket: the pair's column at the slot its count returned
+          const unsigned s = atomicAdd(&rowcnt[row], 1u);
+          if (s < (unsigned)B) kb[(size_t)row * B + s] = oj;
+          else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
+        } else {
+          atomicAdd(&rowcnt[row], 1u);
+        }
       }
-      if (o.los) atomicAdd(&rowcnt[nrows + 1 + row], 1u);
+      if (o.los) {
+        if (B) {
+          const unsigned s = atomicAdd(&rowcnt[nrows + 1 + row], 1u);
+          if (s < (unsigned)B) kb[((size_t)nrows + row) * B + s] = oj;
+          else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
+        } else {
+          atomicAdd(&rowcnt[nrows + 1 + row], 1u);
+        }
+      }
     }
     cflag[idx] = flag;
   }
@@ -1606,7 +1621,10 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
                                               int *__restrict__ li, int *__restrict__ lj,
                                               unsigned long long *__restrict__ stats,
                                               unsigned long long *__restrict__ gate,
-                                              const unsigned *__restrict__ build, MvpFuse mf) {
+                                              const unsigned *__restrict__ build, MvpFuse mf,
+                                              const unsigned char *__restrict__ cflag,
+                                              const unsigned *__restrict__ rowcnt, const unsigned *__restrict__ kb,
+                                              int B) {
   const bool ovf = cand_overflow(cnt, cap);
   const unsigned P = rowoff[nrows], L = rowoff[2 * nrows + 1] - P;
   const unsigned t0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1617,13 +1635,20 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
     cnt->los = ovf ? 0 : L;
     cnt->cand = ncand;
     const bool built = !build || build[0];  // a reused list swept nothing this detect
-    if (built) {
+    // an overflowed detect is retried and counted once, when it completes; a
+    // list built by a detect whose K2 row buckets overflowed is complete and
+    // reused by the retry, so that build counts
+    bool list_ovf = false;
+    for (int q = 0; q < kCandShards; ++q) list_ovf |= cnt->cshard[q][0] > cap / kCandShards;
+    if (built && !list_ovf) {
       stats[0] += cnt->groups;
       stats[2] += cnt->tiles;
       stats[4] += 1;
     }
-    stats[1] += ncand;
-    stats[3] += 1;
+    if (!ovf) {
+      stats[1] += ncand;
+      stats[3] += 1;
+    }
     if (gate) {
       gate[0] = ovf ? 1 : 0;
       gate[1] = ovf ? 0 : P;
@@ -1631,6 +1656,51 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
   }
   if (ovf) return;
   const unsigned stride = gridDim.x * blockDim.x;
+  if (B) {
+    // row buckets (K1b): one lane per candidate; a pair's rank among its row's
+    // bucket (the row's columns, in any order) is its place in the segment
+    unsigned long long pre[kCandShards + 1];
+    const unsigned long long ncand = cand_prefix(cnt, cap, pre);
+    for (unsigned long long k = t0; k < ncand; k += stride) {
+      const unsigned char f = cflag[k];
+      if (!f) continue;
+      const unsigned long long kk = (unsigned long long)__double_as_longlong(cpay[k * kPayStride]);
+      const int row = (int)(kk >> 32) - rb;
+      const unsigned col = (unsigned)kk;
+      if (f & 1) {
+        const unsigned *b = kb + (size_t)row * B;
+        const unsigned c = rowcnt[row];
+        unsigned rank = 0;
+        for (unsigned y = 0; y < c; ++y) rank += (b[y] < col) ? 1u : 0u;
+        const unsigned pos = rowoff[row] + rank;
+        ci[pos] = (int)(kk >> 32);
+        cj[pos] = (int)col;
+        double pay[5];
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          pay[q] = cpay[k * kPayStride + 1 + q];
+          out[(size_t)q * P + pos] = pay[q];
+        }
+        if (mf.pdv) {
+          double4 dv;
+          uint8_t fl;
+          mvp_pair(mf.p, mf.in, (int)(kk >> 32), (int)col, pay[0], pay[1], pay[2], pay[3], dv, fl);
+          mf.pdv[pos] = dv;
+          mf.pfl[pos] = fl;
+        }
+      }
+      if (f & 2) {
+        const unsigned *b = kb + ((size_t)nrows + row) * B;
+        const unsigned c = rowcnt[nrows + 1 + row];
+        unsigned rank = 0;
+        for (unsigned y = 0; y < c; ++y) rank += (b[y] < col) ? 1u : 0u;
+        const unsigned pos = rowoff[nrows + 1 + row] - P + rank;
+        li[pos] = (int)(kk >> 32);
+        lj[pos] = (int)col;
+      }
+    }
+    return;
+  }
   for (unsigned x = t0; x < P + L; x += stride) {
     const bool conf = x < P;
     const unsigned long long *keys = conf ? skey : lkey;
@@ -2033,24 +2103,30 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count, one
   // resident round (4 workgroups per CU at its register budget)
+  // K2 row buckets (B pairs per row per list; a fuller row retries wider, then without)
+  const int B = c->k2_bucket;
+  if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * 4, "K2 row buckets")) return -1;
   hipLaunchKernelGGL(k_exact, dim3(256 * 4), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
                      perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, own, recs ? 1 : 0, cap, rpz, hpz, tla, (int)rb,
                      (int)nrows,
                      (unsigned char *)c->cflag.p, (double *)c->cpay.p,
                      (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
-                     (unsigned *)c->rowcnt.p, kwik, reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
+                     (unsigned *)c->rowcnt.p, (unsigned *)c->kbuck.p, B, kwik,
+                     reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
                      (const Snap *)c->snap_cur.p, (Snap *)c->snap_build.p, (int)n);
   BSA_HIP(c, hipGetLastError());
   if (mark(3)) return -1;
   // ---- K2: row offsets, scatter into row segments, per-row rank + gather
   const int nscan = (int)(2 * (nrows + 1));
   if (scan_excl(c, (const unsigned *)c->rowcnt.p, (unsigned *)c->rowoff.p, nscan)) return -1;
-  hipLaunchKernelGGL(k_scatter, dim3(256 * 4), dim3(256), 0, c->stream, (const Counters *)dcnt, cap, (int)rb,
-                     (int)nrows, (const unsigned char *)c->cflag.p, (const double *)c->cpay.p,
-                     (const unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
-                     (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
-                     (unsigned long long *)c->lkey2.p);
-  BSA_HIP(c, hipGetLastError());
+  if (!B) {  // (row buckets: k_rank reads K1b's buckets, no scatter)
+    hipLaunchKernelGGL(k_scatter, dim3(256 * 4), dim3(256), 0, c->stream, (const Counters *)dcnt, cap, (int)rb,
+                       (int)nrows, (const unsigned char *)c->cflag.p, (const double *)c->cpay.p,
+                       (const unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
+                       (unsigned long long *)c->ckey2.p, (unsigned *)c->cval2.p,
+                       (unsigned long long *)c->lkey2.p);
+    BSA_HIP(c, hipGetLastError());
+  }
   MvpFuse mf{};
   c->fuse_done = false;
   if (c->fuse_mvp) {
@@ -2069,11 +2145,20 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      (const unsigned *)c->cval2.p, (const double *)c->cpay.p,
                      (const unsigned long long *)c->lkey2.p, (int)rb, (int *)c->out_ci.p, (int *)c->out_cj.p,
                      (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
-                     (unsigned long long *)c->stats.p, gate, build, mf);
+                     (unsigned long long *)c->stats.p, gate, build, mf, (const unsigned char *)c->cflag.p,
+                     (const unsigned *)c->rowcnt.p, (const unsigned *)c->kbuck.p, B);
   BSA_HIP(c, hipGetLastError());
   if (mark(4)) return -1;
   c->ev_valid = c->ev_valid || timed;
   return 0;
+}
+
+// K2 row buckets too narrow for a row with `demand` pairs: the next power of
+// two, or (beyond 64) the scatter into row segments
+void grow_k2_bucket(Ctx *c, unsigned long long demand) {
+  int b = std::max(c->k2_bucket, 1);
+  while ((unsigned long long)b < demand && b <= 64) b *= 2;
+  c->k2_bucket = b > 64 ? 0 : b;
 }
 
 // Wait for the enqueued detect and read its totals.  *retry is set (and the
@@ -2086,6 +2171,11 @@ int detect_finish(Ctx *c, bool *retry) {
   if (c->empty_detect) {
     c->last_conf = c->last_los = c->last_cand = c->last_tiles = c->last_groups = 0;
     c->have_pairs = true;
+    return 0;
+  }
+  if (h.k2_demand) {  // a K2 row bucket was full: nothing was written (the
+    grow_k2_bucket(c, h.k2_demand);  // candidate list itself is complete: a reusable one stays valid)
+    *retry = true;
     return 0;
   }
   unsigned long long worst = 0, total = 0;

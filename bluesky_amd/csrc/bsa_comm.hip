@@ -125,6 +125,37 @@ int comm_allgather(Ctx *c, const void *send, void *recv, size_t bytes) {
   return retire(c);
 }
 
+// In-place all-gather of nf fp64 arrays, each at least nranks * rpr long:
+// rank q's block [q rpr, (q + 1) rpr) of every array reaches every rank (the
+// resident sim's home ranges are contiguous, so nothing is packed or
+// unpacked).  RCCL: nf in-place ncclAllGather fused in one group.
+int comm_allgather_inplace(Ctx *c, double *const *f, int nf, size_t rpr) {
+  if (!comm_multi(c) || rpr == 0 || nf <= 0) return 0;
+  if (c->comm) {
+    BSA_NCCL(c, ncclGroupStart());
+    for (int k = 0; k < nf; ++k)
+      BSA_NCCL(c, ncclAllGather(f[k] + (size_t)c->rank * rpr, f[k], rpr, ncclDouble, (ncclComm_t)c->comm, c->stream));
+    BSA_NCCL(c, ncclGroupEnd());
+    return 0;
+  }
+  // in-process group: this rank's blocks into its slot, then every peer's
+  // blocks out of theirs
+  Group *g = c->group;
+  const size_t blk = rpr * 8;
+  if (!ensure(c, c->g_send, blk * nf, "gather send")) return -1;
+  for (int k = 0; k < nf; ++k)
+    BSA_HIP(c, hipMemcpyAsync((char *)c->g_send.p + k * blk, f[k] + (size_t)c->rank * rpr, blk,
+                              hipMemcpyDeviceToDevice, c->stream));
+  if (publish(c, c->g_send.p, blk * nf)) return -1;
+  for (int q = 0; q < g->n; ++q) {
+    if (q == c->rank) continue;
+    for (int k = 0; k < nf; ++k)
+      BSA_HIP(c, hipMemcpyAsync(f[k] + (size_t)q * rpr, (const char *)g->slot[q].p + k * blk, blk,
+                                hipMemcpyDeviceToDevice, c->stream));
+  }
+  return retire(c);
+}
+
 int comm_allreduce_max_u64(Ctx *c, unsigned long long *buf, int count) {
   if (!comm_multi(c) || count <= 0) return 0;
   if (count > 256) return fail(c, "device max all-reduce of %d words", count);

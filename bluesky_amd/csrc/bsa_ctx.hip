@@ -335,6 +335,13 @@ int bsa_set_candidate_capacity(bsa_ctx *c, int64_t capacity) {
   return 0;
 }
 
+int bsa_set_row_bucket(bsa_ctx *c, int width) {
+  if (!c) return -1;
+  if (width < 0 || width > 64) return bsa::fail(c, "row bucket width must be in [0, 64]");
+  c->k2_bucket = width;
+  return 0;
+}
+
 int bsa_set_candidate_reuse(bsa_ctx *c, int on, double sigma_h, double sigma_v) {
   if (!c) return -1;
   if (on && !(sigma_h > 0.0 && sigma_h < 1e6 && sigma_v > 0.0 && sigma_v < 1e5))

@@ -117,7 +117,8 @@ struct Counters {
   unsigned long long tiles;
   unsigned long long groups;  // (64-row x 8-column) blocks swept by the prefilter
   unsigned long long tiles_near;  // of `tiles`: pairs whose boxes overlap (listed first, swept first)
-  unsigned long long pad[2];
+  unsigned long long pad[1];      // (far tile pairs, counted from the list's end)
+  unsigned long long k2_demand;   // K2 row buckets: the largest row count beyond Ctx::k2_bucket (0: fit)
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];
   unsigned long long cshard[kCandShards][16];  // candidates per shard (word 0 of each line)
@@ -149,6 +150,8 @@ struct Ctx {
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
   DevBuf tbox_r, tbox_c, gbox_r, gbox_c, sbox_c, tilepairs, itemmask, workq;
   DevBuf rowcnt, rowoff, lslot;  // K2 counting sort
+  DevBuf kbuck, kslot;           // K2 row buckets (column indices) and each candidate's slots
+  int k2_bucket = 8;             // bucket width (pairs per row); 0 = scatter into row segments
   DevBuf scan_ws;                // single-pass scan: [0] ticket counter, then tile status words
   bool scan_ready = false;
   unsigned long long scan_tickets = 0;
@@ -352,6 +355,7 @@ int fail(Ctx *c, const char *fmt, ...);
 bool comm_multi(const Ctx *c);
 int comm_allgather(Ctx *c, const void *send, void *recv, size_t bytes);  // recv: nranks x bytes
 int comm_allreduce_max_u64(Ctx *c, unsigned long long *buf, int count); // device words, in place
+int comm_allgather_inplace(Ctx *c, double *const *f, int nf, size_t rpr); // rank blocks of nf arrays
 int comm_allreduce_host(Ctx *c, double *v, int count, bool max);         // host values (synchronises)
 int comm_gatherv(Ctx *c, int root, const void *send, size_t bytes, void *recv, const size_t *off,
                  const size_t *len);                                     // rank-order blocks to root
@@ -368,5 +372,6 @@ int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, in
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
                    unsigned long long *gate);
 int detect_finish(Ctx *c, bool *retry);
+void grow_k2_bucket(Ctx *c, unsigned long long demand);
 
 }  // namespace bsa

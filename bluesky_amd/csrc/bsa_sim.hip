@@ -201,8 +201,9 @@ static int sim_gather(Ctx *c) {
     return 0;
   }
   SimDev d = sim_dev(c);
-  Fields fl{{d.lat, d.lon, d.trk, d.gs, d.alt, d.vs, d.gse, d.gsn}, 8, nullptr};
-  if (gather_fields(c, fl)) return -1;
+  // in place: the home ranges are contiguous and the arrays padded to nranks x rpr
+  double *const f[8] = {d.lat, d.lon, d.trk, d.gs, d.alt, d.vs, d.gse, d.gsn};
+  if (comm_allgather_inplace(c, f, 8, (size_t)c->sim_rpr)) return -1;
   c->sim_gathered = true;
   return 0;
 }
@@ -412,6 +413,10 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   if (bsa::home_order(c, p->tla, c->h2id_h)) return -1;
   bsa::set_rank_rows(c);
   if (bsa::set_home_maps(c)) return -1;
+  // the all-gathered arrays hold nranks x rpr entries (in-place all-gather)
+  const size_t NG = (size_t)std::max<int64_t>(n, c->sim_rpr * c->nranks) * 8;
+  for (int k = 0; k < 6; ++k)
+    if (!bsa::ensure_keep(c, c->own[k], NG, "gathered state")) return -1;
   std::vector<char> tmp;
   const double *st6[6] = {s->lat, s->lon, s->trk, s->gs, s->alt, s->vs};
   for (int k = 0; k < 6; ++k)
@@ -423,7 +428,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
                         s->ap_vs, s->selalt, s->bank, s->eps, s->accel, s->asas_alt};
   const size_t N8 = (size_t)n * 8;
   for (int k = 0; k < 13; ++k) {
-    if (!bsa::ensure(c, *dst[k], N8, "sim state")) return -1;
+    if (!bsa::ensure(c, *dst[k], k < 4 ? NG : N8, "sim state")) return -1;
     if (bsa::put_home(c, dst[k]->p, hs[k], 8, tmp)) return -1;
   }
   // ASAS arrays: asas.trk/tas start at traf.trk/tas (asas.py:405-409), vs 0, inactive
@@ -507,6 +512,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     // abort ran on the same, unchanged state)
     bsa::Counters h;
     BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
+    if (h.k2_demand) bsa::grow_k2_bucket(c, h.k2_demand);  // a K2 row bucket was full on this rank
     unsigned long long worst = 0;
     for (int q = 0; q < bsa::kCandShards; ++q) worst = std::max(worst, h.cshard[q][0]);
     if (worst > c->cand_cap / bsa::kCandShards)

@@ -126,6 +126,12 @@ int bsa_last_candidates(bsa_ctx *ctx, int64_t *n_candidates);
  * capacity (grown the same way). */
 int bsa_set_candidate_capacity(bsa_ctx *ctx, int64_t capacity);
 
+/* K2 (canonical order) row buckets: width w (1..64) pairs per row are
+ * placed by K1b directly, K2 ranks each pair inside its row's bucket; a row
+ * with more pairs makes the detect retry with a wider bucket (beyond 64: the
+ * scatter into row segments, width 0).  Default 8.  Results never depend on
+ * it (tests set it to exercise every path). */
+int bsa_set_row_bucket(bsa_ctx *ctx, int width);
 /* Candidate-list reuse across detects (own == intruder, whole row range, not
  * KWIK / NOPRUNE).  A detect that builds the list inflates
  * every aircraft's reach by a horizontal budget sigma_h [m] and a vertical

@@ -162,3 +162,27 @@ def test_kwik_random_box_vs_oracle(ctx):
     got = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx, kwik=True)
     exp = ocd.detect_arrays(t, t, RPZ, HPZ, TLA, kwik=True)
     util.assert_detect_equal(got, exp, RPZ, TLA)
+
+
+def test_row_bucket_widths_are_identical(ctx):
+    """K2 row buckets (bsa_set_row_bucket): width 1 and 2 overflow on dense rows
+    and retry wider, 0 scatters into row segments -- every width gives the
+    default width's results bitwise, on a dense cluster and on a golden case
+    with stacked identical aircraft."""
+    t = synth.box(2500, 40.0, seed=47)        # ~30 conflicts per aircraft
+    cases = [(t, t, RPZ, HPZ, TLA)]
+    own, intr, z = util.load_cd(util.golden('cd_edge*.npz')[0])
+    cases.append((own, intr, float(z['rpz']), float(z['hpz']), float(z['tla'])))
+    try:
+        for own, intr, rpz, hpz, tla in cases:
+            ctx.set_row_bucket(8)
+            exp = statebased.detect_indices(own, intr, rpz, hpz, tla, ctx=ctx, with_dcpa=True)
+            for w in (0, 1, 2, 64):
+                ctx.set_row_bucket(w)
+                got = statebased.detect_indices(own, intr, rpz, hpz, tla, ctx=ctx, with_dcpa=True)
+                for k in exp:
+                    if exp[k] is not None:
+                        assert np.array_equal(np.asarray(got[k]), np.asarray(exp[k])), (w, k)
+        assert len(exp['ci']) > 0
+    finally:
+        ctx.set_row_bucket(8)

@@ -198,3 +198,45 @@ def test_sharded_standalone_detect_gather(ctx):
     assert res[0] is None and res[2] is None
     for k in full:
         assert np.array_equal(res[1][k], full[k]), k
+
+
+def test_home_ranges_and_row_ids(ctx):
+    """Home order: the ranks' home ranges are 512-aligned and
+    tile 0..n, their aircraft (bsa_sim_row_ids) partition the indices, and each
+    rank's share of a CD step (bsa_sim_detect_rows on one GPU) gives exactly
+    the rows of the whole detect."""
+    t = synth.box(3001, 100.0, seed=67)
+    init = resident.initial_state(t)
+    p = resident.params(cd_every=1)
+    world = 3
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=world, group=g)
+        return sim.stats(), sim.row_ids()
+
+    res = run_ranks(world, rank)
+    edges = [(st['row_begin'], st['row_end']) for st, _ in res]
+    assert edges[0][0] == 0 and edges[-1][1] == t.ntraf
+    assert all(a[1] == b[0] for a, b in zip(edges, edges[1:]))
+    assert all(rb % 512 == 0 for rb, _ in edges)
+    ids = np.concatenate([i for _, i in res])
+    assert np.array_equal(np.sort(ids), np.arange(t.ntraf))
+    assert all(np.all(np.diff(i) > 0) for _, i in res)
+    # one GPU: the sim's detect of each rank's home slice vs the full detect
+    full = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx)
+    c = _lib.Context(0)
+    try:
+        sim = resident.ResidentSim(init, p, ctx=c)
+        for (rb, re), (_, rid) in zip(edges, res):
+            nc, nl = c.sim_detect_rows(rb, re)
+            got = c.fetch_pairs(nc, nl)
+            sel = np.isin(full['ci'], rid)
+            assert np.array_equal(got['ci'], full['ci'][sel]) and np.array_equal(got['cj'], full['cj'][sel])
+            assert np.array_equal(got['qdr'], full['qdr'][sel])
+            lsel = np.isin(full['li'], rid)
+            assert np.array_equal(got['li'], full['li'][lsel])
+            assert np.array_equal(got['inconf'], full['inconf'][rid])
+            assert np.array_equal(got['tcpamax'], full['tcpamax'][rid])
+        assert sim.stats()['steps'] == 0
+    finally:
+        c.close()

@@ -425,3 +425,27 @@ def test_resident_openap_phase_matches_oracle(ctx):
     sim.set_perf(None)
     with pytest.raises(RuntimeError):
         sim.set_perf(table, np.full(n, len(table), np.int32))   # index outside the table
+
+
+def test_resident_row_bucket_overflow_retry_is_exact(ctx):
+    """K2 row buckets one pair wide overflow on the first dense row: the
+    resident step aborts, widens them and re-runs (bsa_sim_step's retry) --
+    the state after several MVP steps equals the default run's bitwise."""
+    from bluesky_amd import _lib
+    t = synth.box(1500, 60.0, seed=53)
+    init = resident.initial_state(t)
+    p = resident.params(cd_every=1)
+    ref = resident.ResidentSim(init, p, ctx=ctx)
+    ref.step(4)
+    exp = ref.read()
+    c = _lib.Context(0)
+    try:
+        c.set_row_bucket(1)
+        sim = resident.ResidentSim(init, p, ctx=c)
+        sim.step(4)
+        got = sim.read()
+        for k in exp:
+            assert np.array_equal(got[k], exp[k]), k
+        assert sim.stats()['n_conf'] == ref.stats()['n_conf'] > 0
+    finally:
+        c.close()
