@@ -1851,10 +1851,14 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // slice [rb, re) of the columns (no re-sort, no gather)
   const bool home = c->det_home;
   c->last_home = home;
-  // home mode: K1b builds its fp64 records from the state arrays (no 128-B
-  // record per aircraft written by K0b) -- BSA_HOME_REC=1 forces the records
+  // home mode: K1b builds its fp64 records from the state arrays instead of
+  // reading 128-B records K0b wrote for EVERY column: cheaper when K0b's
+  // record writes dominate -- at 1M (0.165 -> 0.084 ms of K0) or for one rank's
+  // slice of several; with one rank below 2^18 aircraft the stored records
+  // win (each aircraft is in ~5 candidates there: K1b 27 -> 18 us at 100k).
+  // BSA_HOME_REC=0/1 overrides.
   static const int home_rec_env = getenv("BSA_HOME_REC") ? atoi(getenv("BSA_HOME_REC")) : -1;
-  const bool recs = !home || home_rec_env == 1;
+  const bool recs = !home || (home_rec_env >= 0 ? home_rec_env == 1 : (n < (1 << 18) && c->nranks == 1));
   if (home && (distinct || rb % kTile != 0 || (flags & BSA_FLAG_KWIK)))
     return fail(c, "home-order detect needs own == intruder, a %d-aligned row slice, no KWIK", kTile);
   const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;

@@ -227,6 +227,8 @@ struct Ctx {
   DevBuf h2id, id2h;                  // u32, device
   std::vector<unsigned> h2id_h, id2h_h, lpos_h;  // host copies
   bool sim_ready = false;
+  bool mvp_deferred = false;            // this step's K3 rows run inside K4' (sim_cd -> bsa_sim_step)
+  std::vector<unsigned char> mvp_defer;  // the deferred K3 arguments (MvpIn, bsa_mvp_row.h)
   bsa_sim_params simp{};
   int64_t sim_steps = 0, sim_cd_calls = 0, sim_rb = 0, sim_re = 0, sim_rpr = 0;
   int64_t sim_last_conf = 0, sim_last_los = 0;
@@ -292,9 +294,12 @@ struct MvpDev {
   float *o_asase, *o_asasn;
   double *o_tsolv;
 };
+struct MvpIn;
+// defer != NULL (resident step): the per-row kernel is not launched; its
+// arguments go to *defer for the fused MVP + pilot + kinematics kernel
 int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned *seg,
                const unsigned long long *gate, unsigned *sticky, const uint8_t *inconf, uint8_t *active,
-               bool resolve, bool pairs_done = false);
+               bool resolve, bool pairs_done = false, MvpIn *defer = nullptr);
 
 // device pointers for the fused kinematics kernel
 struct KinDev {

@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "bsa_kin_math.h"
+#include "bsa_mvp_row.h"
 
 #pragma clang fp contract(off)
 
@@ -45,13 +46,26 @@ struct SimDev {
 };
 
 // Pilot.APorASAS (pilot.py:28-63; no wind, constant wind or a 2-D field) +
-// UpdateAirSpeed/GroundSpeed/Position, rows [rb, re)
+// UpdateAirSpeed/GroundSpeed/Position, rows [rb, re).  FUSE (a CD step without
+// the ASAS bookkeeping): K3's per-row part (bsa_mvp_row.h: the dv fold, the
+// finalize, asas.active = inconf, or DoNothing) runs first in the same lane --
+// the row's new ASAS targets are what its pilot reads next (traffic.py:397),
+// one launch and one pass over the row state fewer.  The gate check of
+// k_mvp_row is made by every lane, so the whole grid agrees on an abort.
+template <bool FUSE>
 __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, int winddim, double vwn,
-                                                       double vwe, WindField wf, SimDev d) {
-  if (*d.sticky) return;
+                                                       double vwe, WindField wf, SimDev d, MvpIn mv,
+                                                       bsa_mvp_params mp) {
+  if (FUSE) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && mv.gate[0] != 0) mv.sticky[0] = 1u;
+    if (*d.sticky || mv.gate[0] != 0) return;
+  } else if (*d.sticky) {
+    return;
+  }
   const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
   if (k >= re) return;
+  if (FUSE) mvp_row(rb, k - rb, mp, mv);
   if (winddim == 2) {  // pilot.py:32 and traffic.py:463 read the field at the same pre-step position
     kin::windfield_2d(wf, d.lat[k], d.lon[k], vwn, vwe);
     winddim = 1;
@@ -377,10 +391,19 @@ static int sim_cd(Ctx *c) {
   d.o_asasn = (float *)c->s_asn.p + rb;
   d.o_tsolv = nullptr;
   // K3 (+ gate, + asas.active = inconf unless ResumeNav runs) on the detect's own row offsets
+  // without the bookkeeping (which runs between K3 and K4') K3's rows are
+  // deferred into K4' of this step (k_sim_pilot_kin<true>)
+  const bool defer = !p.resume_nav && c->sim_re > c->sim_rb;
+  MvpIn din{};
   if (mvp_device(c, p.mvp, d, (const unsigned *)c->rowoff.p, gate, sticky,
                  p.resume_nav ? nullptr : (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p, p.reso != 0,
-                 c->fuse_done))
+                 c->fuse_done, defer ? &din : nullptr))
     return -1;
+  if (defer) {
+    c->mvp_defer.resize(sizeof(MvpIn));
+    memcpy(c->mvp_defer.data(), &din, sizeof(MvpIn));
+    c->mvp_deferred = true;
+  }
   // second half: resopairs rewrite, ResumeNav's asas.active, unique / cumulative counts
   return p.resume_nav ? bk_apply(c, bk) : 0;
 }
@@ -480,9 +503,17 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
       if (c->sim_steps % c->simp.cd_every == 0)
         if (bsa::sim_cd(c)) return -1;
       const int64_t nb = std::max<int64_t>(1, (re - rb + 255) / 256);
-      hipLaunchKernelGGL(bsa::k_sim_pilot_kin, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb, (int)re,
-                         c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
-                         bsa::wind_field(c), bsa::sim_dev(c));
+      bsa::MvpIn mv{};
+      if (c->mvp_deferred) memcpy(&mv, c->mvp_defer.data(), sizeof(mv));
+      if (c->mvp_deferred)
+        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<true>, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb,
+                           (int)re, c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
+                           bsa::wind_field(c), bsa::sim_dev(c), mv, c->simp.mvp);
+      else
+        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<false>, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb,
+                           (int)re, c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
+                           bsa::wind_field(c), bsa::sim_dev(c), mv, c->simp.mvp);
+      c->mvp_deferred = false;
       BSA_HIP(c, hipGetLastError());
       c->sim_gathered = c->nranks == 1;
       c->sim_steps++;
