@@ -165,10 +165,33 @@ struct BkUniq {
   unsigned long long *uniq, *all;
 };
 
+// per-workgroup sums of two counts, then ONE atomic each per workgroup (a
+// per-wave atomic on one word serialises at ~12 ns each)
+__device__ __forceinline__ void block_add2(unsigned long long a, unsigned long long b, unsigned long long *pa,
+                                           unsigned long long *pb) {
+  __shared__ unsigned long long s[2][4];
+  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    s[0][w] = a;
+    s[1][w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long ta = 0, tb = 0;
+    for (unsigned q = 0; q < blockDim.x / 64; ++q) {
+      ta += s[0][q];
+      tb += s[1][q];
+    }
+    if (ta) atomicAdd(pa, ta);
+    if (tb) atomicAdd(pb, tb);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_bk_unique(BkUniq u, const unsigned long long *gate, const unsigned *sticky) {
   if (bk_aborted(gate, sticky)) return;
   const unsigned P = *u.np;
   const unsigned lane = threadIdx.x & 63;
+  unsigned long long nrep = 0, nfresh = 0;  // this wave's counts (lane 0)
   for (unsigned x = blockIdx.x * blockDim.x + threadIdx.x; x - lane < P; x += gridDim.x * blockDim.x) {
     bool rep = false, fresh = false;
     if (x < P) {
@@ -179,11 +202,10 @@ __global__ __launch_bounds__(256) void k_bk_unique(BkUniq u, const unsigned long
       if (rep) fresh = !(csr_has(u.pptr, u.pcol, i, j) || csr_has(u.pptr, u.pcol, jh, ii));
     }
     const unsigned long long mr = __ballot(rep), mf = __ballot(fresh);
-    if (lane == 0) {
-      if (mr) atomicAdd(u.uniq, (unsigned long long)__popcll(mr));
-      if (mf) atomicAdd(u.all, (unsigned long long)__popcll(mf));
-    }
+    nrep += (unsigned long long)__popcll(mr);
+    nfresh += (unsigned long long)__popcll(mf);
   }
+  block_add2(nrep, nfresh, u.uniq, u.all);
 }
 
 // LoS row pointers from K2's offsets: lptr[r] = rowoff[nrows + 1 + r] - P
@@ -285,6 +307,7 @@ __global__ __launch_bounds__(256) void k_bk_unique_g(KeyBlocks kb, unsigned long
   const unsigned long long P = los ? b[1] : b[0];
   const unsigned long long *keys = b + 2 + (los ? b[0] : 0);
   const unsigned lane = threadIdx.x & 63;
+  unsigned long long nrep = 0, nfresh = 0;
   for (unsigned long long x = blockIdx.x * blockDim.x + threadIdx.x; x - lane < P;
        x += (unsigned long long)gridDim.x * blockDim.x) {
     bool rep = false, fresh = false;
@@ -296,11 +319,10 @@ __global__ __launch_bounds__(256) void k_bk_unique_g(KeyBlocks kb, unsigned long
       if (rep) fresh = !(key_has(kb.prev, kb.W, kb.rpr, los, i, j) || key_has(kb.prev, kb.W, kb.rpr, los, jh, ii));
     }
     const unsigned long long mr = __ballot(rep), mf = __ballot(fresh);
-    if (lane == 0) {
-      if (mr) atomicAdd(st + 1 + los, (unsigned long long)__popcll(mr));
-      if (mf) atomicAdd(st + 3 + los, (unsigned long long)__popcll(mf));
-    }
+    nrep += (unsigned long long)__popcll(mr);
+    nfresh += (unsigned long long)__popcll(mf);
   }
+  block_add2(nrep, nfresh, st + 1 + los, st + 3 + los);
 }
 
 __global__ __launch_bounds__(256) void k_bk_copy_keys(unsigned long long words, const unsigned long long *src,

@@ -781,6 +781,7 @@ constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 // measurements; results never depend on it)
 struct PfKnobs {
   int shards;  // dequeue counters in use (power of two <= kWorkShards)
+  int pieces;  // work items per (tile pair, 64-row slice): 1, 2 or 4
 };
 #ifndef BSA_PF_WAVES_PER_EU
 #define BSA_PF_WAVES_PER_EU 4
@@ -950,7 +951,11 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // so ONE XCD sweeps all 8 slices of a tile pair, close together in time: the
   // column tile is fetched into that XCD's L2 once instead of into all eight.
   static_assert(PF_ITEMS_PER_TILE == 8, "item id layout: 3 bits of slice");
-  const unsigned long long nitems = ((ntiles + 7) / 8) * 64;
+  // pieces > 1: an item's column mask is split into that many pieces, each a
+  // work item of its own -- when there are fewer items than waves (one rank's
+  // share of a multi-GPU step) the densest items, ~60 us each, set the sweep's
+  // span otherwise (tools/pf_trace.py); empty pieces are skipped like empty items
+  const unsigned long long nitems = ((ntiles + 7) / 8) * 64 * (unsigned)kn.pieces;
   const unsigned shard = blockIdx.x & (kn.shards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
@@ -1003,8 +1008,10 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 #ifndef PF_XCD_ITEMS
 #define PF_XCD_ITEMS 1
 #endif
-    const unsigned long long tp = PF_XCD_ITEMS ? (item & 7ull) + ((item >> 6) << 3) : item >> 3;
-    const unsigned slice = PF_XCD_ITEMS ? (unsigned)(item >> 3) & 7u : (unsigned)item & 7u;
+    const unsigned piece = (unsigned)((item >> 3) % (unsigned)kn.pieces);
+    const unsigned long long it = (item & 7ull) | ((item >> 3) / (unsigned)kn.pieces) << 3;
+    const unsigned long long tp = PF_XCD_ITEMS ? (it & 7ull) + ((it >> 6) << 3) : it >> 3;
+    const unsigned slice = PF_XCD_ITEMS ? (unsigned)(it >> 3) & 7u : (unsigned)it & 7u;
     if (tp >= ntiles) break;
     const uint2 rc = tile_at(tiles, tp, near, tcap);
     const int rbase = (int)rc.x * kTile + (int)slice * PF_WROWS;
@@ -1012,6 +1019,10 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const int cbase = (int)rc.y * kTile;
     // column sub-groups of this tile that may interact with the wave's row box (K0e)
     unsigned long long gm = masks[tp * PF_ITEMS_PER_TILE + slice];
+    if (kn.pieces > 1) {
+      const unsigned w = 64u / (unsigned)kn.pieces;
+      gm &= ((1ull << w) - 1ull) << (w * piece);
+    }
     if (!gm) break;
     subs += (unsigned)__popcll(gm);
 #ifdef BSA_PF_TRACE
@@ -1273,7 +1284,17 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   PF_STAMP(0);
   if (n2) flush2();
   write_pending();
-  if (lane == 0 && subs) atomicAdd(&cnt->groups, (unsigned long long)subs);
+  // the roofline's sub-group count: one atomic per workgroup, spread over 32
+  // lines (4096 waves adding to one word serialised at ~12 ns each, ~50 us of
+  // the sweep's tail when the waves finish together)
+  __shared__ unsigned wsubs[PF_WAVES];
+  if (lane == 0) wsubs[w] = subs;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned t = 0;
+    for (int q = 0; q < PF_WAVES; ++q) t += wsubs[q];
+    if (t) atomicAdd(&cnt->gpart[blockIdx.x & 31][0], (unsigned long long)t);
+  }
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
   if (lane == 0)
@@ -1634,6 +1655,9 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
     cnt->conf = ovf ? 0 : P;
     cnt->los = ovf ? 0 : L;
     cnt->cand = ncand;
+    unsigned long long g = 0;
+    for (int q = 0; q < 32; ++q) g += cnt->gpart[q][0];
+    cnt->groups = g;
     const bool built = !build || build[0];  // a reused list swept nothing this detect
     // an overflowed detect is retried and counted once, when it completes; a
     // list built by a detect whose K2 row buckets overflowed is complete and
@@ -2071,12 +2095,18 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : lim * lim};
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
-  static const PfKnobs kn = [] {
+  static const PfKnobs kn0 = [] {
     const char *v = getenv("BSA_PF_SHARDS");
-    PfKnobs z{v ? atoi(v) : kWorkShards};
+    PfKnobs z{v ? atoi(v) : kWorkShards, 1};
     if (z.shards < 1 || z.shards > kWorkShards || (z.shards & (z.shards - 1))) z.shards = kWorkShards;
     return z;
   }();
+  // pieces: ~8 items per row tile, a few hundred row tiles fill the waves;
+  // fewer rows split the items (BSA_PF_PIECES overrides)
+  static const int pieces_env = getenv("BSA_PF_PIECES") ? atoi(getenv("BSA_PF_PIECES")) : 0;
+  PfKnobs kn = kn0;
+  kn.pieces = nrows >= (1 << 16) ? 1 : (nrows >= (1 << 14) ? 2 : 4);
+  if (pieces_env == 1 || pieces_env == 2 || pieces_env == 4) kn.pieces = pieces_env;
 #ifdef BSA_PF_TRACE
   {
     static DevBuf tb;

@@ -106,7 +106,10 @@ constexpr int kResortEvery = 8;  // detect calls between spatial re-sorts
 constexpr int kResortEveryReuse = 64;  // ... with a reusable candidate list (a re-sort rebuilds it)
 constexpr int kEvSets = 4096;    // detect timing event sets kept between resets
 
-constexpr int kCandShards = 8;  // candidate list shards (one counter each, 128 B apart)
+#ifndef BSA_CAND_SHARDS
+#define BSA_CAND_SHARDS 8
+#endif
+constexpr int kCandShards = BSA_CAND_SHARDS;  // candidate list shards (one counter each, 128 B apart)
 constexpr unsigned kDangling = 0xffffffffu;  // resopairs column of a deleted intruder (sorts last in a row)
 
 // counters block on the device
@@ -122,6 +125,7 @@ struct Counters {
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];
   unsigned long long cshard[kCandShards][16];  // candidates per shard (word 0 of each line)
+  unsigned long long gpart[32][16];  // sub-groups swept, per prefilter workgroup shard (summed into groups by K2)
 };
 
 // ---------------------------------------------------------------- buffers
