@@ -237,6 +237,7 @@ struct Ctx {
   int64_t sim_steps = 0, sim_cd_calls = 0, sim_rb = 0, sim_re = 0, sim_rpr = 0;
   int64_t sim_last_conf = 0, sim_last_los = 0;
   bool sim_gathered = true;  // replicas consistent with every rank's rows
+  bool sim_gs_derivable = false;  // gseast / gsnorth of every row follow from gs / trk (K4' without wind ran)
   DevBuf s_tas, s_hdg, s_gse, s_gsn;                        // traffic state besides own[]
   DevBuf s_aptrk, s_aptas, s_apalt, s_apvs, s_selalt, s_bank, s_eps, s_accel;  // frozen
   DevBuf s_atrk, s_atas, s_avs, s_aalt, s_ase, s_asn, s_active;  // ASAS (full n)

@@ -208,6 +208,19 @@ static int gather_fields(Ctx *c, const Fields &fl) {
   return 0;
 }
 
+// Without wind, K4' sets gs = tas, trk = hdg and gseast / gsnorth =
+// tas sin / cos(hdg) (traffic.py:455-460, bsa_kin_math.h): every rank derives
+// the other ranks' gseast / gsnorth from their gathered gs / trk with the same
+// expressions, bitwise, instead of receiving them (6 arrays over xGMI, not 8)
+__global__ __launch_bounds__(256) void k_derive_gs(int n, int rb, int re, const double *__restrict__ gs,
+                                                   const double *__restrict__ trk, double *__restrict__ gse,
+                                                   double *__restrict__ gsn) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n || (k >= rb && k < re)) return;
+  gsn[k] = gs[k] * cos(trk[k] * kD2R);
+  gse[k] = gs[k] * sin(trk[k] * kD2R);
+}
+
 // C1: replicate every rank's rows of the 8 arrays CD and MVP read for any row
 static int sim_gather(Ctx *c) {
   if (c->nranks == 1 || c->sim_gathered) {
@@ -215,9 +228,16 @@ static int sim_gather(Ctx *c) {
     return 0;
   }
   SimDev d = sim_dev(c);
-  // in place: the home ranges are contiguous and the arrays padded to nranks x rpr
+  // in place: the home ranges are contiguous and the arrays padded to nranks x rpr;
+  // gseast / gsnorth are derived when every rank's came from K4' without wind
   double *const f[8] = {d.lat, d.lon, d.trk, d.gs, d.alt, d.vs, d.gse, d.gsn};
-  if (comm_allgather_inplace(c, f, 8, (size_t)c->sim_rpr)) return -1;
+  const bool derive = c->simp.winddim == 0 && c->sim_gs_derivable;
+  if (comm_allgather_inplace(c, f, derive ? 6 : 8, (size_t)c->sim_rpr)) return -1;
+  if (derive) {
+    hipLaunchKernelGGL(k_derive_gs, dim3((unsigned)((c->n + 255) / 256)), dim3(256), 0, c->stream, (int)c->n,
+                       (int)c->sim_rb, (int)c->sim_re, (const double *)d.gs, (const double *)d.trk, d.gse, d.gsn);
+    BSA_HIP(c, hipGetLastError());
+  }
   c->sim_gathered = true;
   return 0;
 }
@@ -476,6 +496,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   c->bk_ready = false;  // empty resopairs / previous pair sets
   c->sim_steps = c->sim_cd_calls = c->sim_last_conf = c->sim_last_los = 0;
   c->sim_gathered = true;
+  c->sim_gs_derivable = false;  // gseast / gsnorth are the host's until K4' runs
   if (c->feed_pending) {  // a snapshot of the previous sim is dropped
     BSA_HIP(c, hipEventSynchronize(c->feed_ev));
     c->feed_pending = false;
@@ -498,6 +519,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
   for (int attempt = 0; c->sim_steps < target; ++attempt) {
     if (attempt > 6) return bsa::fail(c, "candidate buffer overflow in the resident step (retries exhausted)");
     const int64_t base = c->sim_steps, base_cd = c->sim_cd_calls;
+    const bool derivable0 = c->sim_gs_derivable;
     BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 32, c->stream));  // sticky, steps_done, demands
     while (c->sim_steps < target) {
       if (c->sim_steps % c->simp.cd_every == 0)
@@ -515,6 +537,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
                            bsa::wind_field(c), bsa::sim_dev(c), mv, c->simp.mvp);
       c->mvp_deferred = false;
       BSA_HIP(c, hipGetLastError());
+      c->sim_gs_derivable = true;  // every rank's rows now hold K4's gs / trk / gse / gsn
       c->sim_gathered = c->nranks == 1;
       c->sim_steps++;
     }
@@ -530,6 +553,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
     const int64_t done = (int64_t)ctl[1];
     c->sim_steps = base + done;
+    c->sim_gs_derivable = derivable0 || done > 0;  // K4' ran for the completed steps only
     int64_t cds = 0;
     for (int64_t k = base; k < base + done; ++k) cds += (k % c->simp.cd_every == 0) ? 1 : 0;
     c->sim_cd_calls = base_cd + cds;
@@ -647,6 +671,7 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
   }
   if (any_cd) {
     c->sim_gathered = true;     // every rank passed the same full arrays
+    c->sim_gs_derivable = false;  // (gseast / gsnorth may be the host's)
     c->reuse_valid = false;     // a state jump rebuilds any reused candidate list
   }
   return 0;
