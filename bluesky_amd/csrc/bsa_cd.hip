@@ -1311,7 +1311,13 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 // that already started.  Tile status words carry the launch's epoch, so they
 // need no zeroing between launches: {epoch:30 | flag:2 | value:32}, flag 1 =
 // the tile's own total, 2 = inclusive prefix through the tile.
-constexpr int kScanThreads = 1024, kScanItems = 8, kScanTile = kScanThreads * kScanItems;
+#ifndef BSA_SCAN_THREADS
+#define BSA_SCAN_THREADS 512
+#endif
+#ifndef BSA_SCAN_ITEMS
+#define BSA_SCAN_ITEMS 4
+#endif
+constexpr int kScanThreads = BSA_SCAN_THREADS, kScanItems = BSA_SCAN_ITEMS, kScanTile = kScanThreads * kScanItems;
 __device__ __forceinline__ unsigned long long scan_word(unsigned epoch, unsigned flag, unsigned v) {
   return ((unsigned long long)(epoch & 0x3fffffffu) << 34) | ((unsigned long long)flag << 32) | v;
 }
