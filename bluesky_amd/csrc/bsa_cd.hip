@@ -899,7 +899,8 @@ template <bool NOPRUNE>
 __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, const float4 *__restrict__ pprow, int nrows,
     const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, const float4 *__restrict__ ppcol, int ncols,
-    const unsigned long long *__restrict__ masks, const uint2 *__restrict__ tiles, unsigned long long tcap,
+    const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ sbox_c, int noprune,
+    const uint2 *__restrict__ tiles, unsigned long long tcap,
     Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
     uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn) {
@@ -1017,8 +1018,18 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const int rbase = (int)rc.x * kTile + (int)slice * PF_WROWS;
     if (rbase >= nrows) break;
     const int cbase = (int)rc.y * kTile;
-    // column sub-groups of this tile that may interact with the wave's row box (K0e)
-    unsigned long long gm = masks[tp * PF_ITEMS_PER_TILE + slice];
+    // column sub-groups of this tile that may interact with the wave's row box:
+    // the stage-1 test on box gaps (one sub-group box per lane), evaluated as
+    // the item starts -- its two box loads are as deep as the mask load of a
+    // separate K0e launch was, and the launch is saved
+    unsigned long long gm;
+    {
+      const int nsub = min(kSubsPerTile, (ncols - cbase + kSub - 1) / kSub);
+      const int sg = min(lane, nsub - 1);
+      const TileBox sb = sbox_c[cbase / kSub + sg];
+      const TileBox rg = gbox_r[((int)rc.x * kTile) / kGroup + (int)slice];
+      gm = __ballot(lane < nsub && (noprune || boxes_may_interact(rg, sb)));
+    }
     if (kn.pieces > 1) {
       const unsigned w = 64u / (unsigned)kn.pieces;
       gm &= ((1ull << w) - 1ull) << (w * piece);
@@ -1311,20 +1322,19 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 // that already started.  Tile status words carry the launch's epoch, so they
 // need no zeroing between launches: {epoch:30 | flag:2 | value:32}, flag 1 =
 // the tile's own total, 2 = inclusive prefix through the tile.
-#ifndef BSA_SCAN_THREADS
-#define BSA_SCAN_THREADS 512
-#endif
-#ifndef BSA_SCAN_ITEMS
-#define BSA_SCAN_ITEMS 4
-#endif
-constexpr int kScanThreads = BSA_SCAN_THREADS, kScanItems = BSA_SCAN_ITEMS, kScanTile = kScanThreads * kScanItems;
+// Tiles of kScanThreads x kScanItems words: 2048 below 2^19 words (more tiles
+// in flight: K2 26.3 -> 24.6 us at 100k, 19.9 -> 14.6 us for one rank of 8),
+// 8192 above (at 1M a 2048-word tiling's ~1000 tiles lengthened the ticket
+// queue and the look-back: 62 -> 139 us)
 __device__ __forceinline__ unsigned long long scan_word(unsigned epoch, unsigned flag, unsigned v) {
   return ((unsigned long long)(epoch & 0x3fffffffu) << 34) | ((unsigned long long)flag << 32) | v;
 }
+template <int kScanThreads, int kScanItems>
 __global__ __launch_bounds__(kScanThreads) void k_scan_excl(const unsigned *__restrict__ in, unsigned *__restrict__ out,
                                                             int n, unsigned long long *__restrict__ ticket,
                                                             unsigned long long base,
                                                             unsigned long long *__restrict__ status, unsigned epoch) {
+  constexpr int kScanTile = kScanThreads * kScanItems;
   __shared__ unsigned wsum[kScanThreads / 64];
   __shared__ unsigned s_tile, s_excl;
   if (threadIdx.x == 0) s_tile = (unsigned)(atomicAdd(ticket, 1ull) - base);
@@ -1395,6 +1405,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_excl(const unsigned *__re
 
 int scan_excl(Ctx *c, const unsigned *in, unsigned *out, int n) {
   if (n <= 0) return 0;
+  const bool small = n <= (1 << 19);
+  const int kScanTile = small ? 512 * 4 : 1024 * 8;
   const unsigned tiles = (unsigned)((n + kScanTile - 1) / kScanTile);
   const size_t had = c->scan_ws.bytes;
   if (!ensure_keep(c, c->scan_ws, 8 * (size_t)(1 + tiles), "scan tile status")) return -1;
@@ -1407,8 +1419,12 @@ int scan_excl(Ctx *c, const unsigned *in, unsigned *out, int n) {
   }
   const unsigned epoch = ++c->scan_epoch;  // never 0: fresh (zeroed) status words are never ready
   unsigned long long *ws = (unsigned long long *)c->scan_ws.p;
-  hipLaunchKernelGGL(k_scan_excl, dim3(tiles), dim3(kScanThreads), 0, c->stream, in, out, n, ws, c->scan_tickets,
-                     ws + 1, epoch);
+  if (small)
+    hipLaunchKernelGGL((k_scan_excl<512, 4>), dim3(tiles), dim3(512), 0, c->stream, in, out, n, ws, c->scan_tickets,
+                       ws + 1, epoch);
+  else
+    hipLaunchKernelGGL((k_scan_excl<1024, 8>), dim3(tiles), dim3(1024), 0, c->stream, in, out, n, ws,
+                       c->scan_tickets, ws + 1, epoch);
   BSA_HIP(c, hipGetLastError());
   c->scan_tickets += tiles;
   return 0;
@@ -2088,12 +2104,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      nrt, nct, tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
                      (unsigned long long)ntp, dcnt, build);
   BSA_HIP(c, hipGetLastError());
-  // K0e: per (tile pair, 64-row slice) the mask of interacting column sub-groups
-  hipLaunchKernelGGL(k_items, dim3((unsigned)std::min<long long>(2048, (ntp + 3) / 4)), dim3(256), 0,
-                     c->stream, (int)nrows, (int)n, gbox_r, (const TileBox *)c->sbox_c.p,
-                     (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, (const Counters *)dcnt, noprune,
-                     (unsigned long long *)c->itemmask.p, build);
-  BSA_HIP(c, hipGetLastError());
+  // (K0e, an item's column sub-group mask, is evaluated by K1a as the item starts)
   if (mark(1)) return -1;
 
   const float T = (float)(tla > 0.0 ? tla : 0.0);
@@ -2130,13 +2141,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (noprune)
     hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
-                       (const float4 *)c->pfpcol.p, (int)n, (const unsigned long long *)c->itemmask.p,
+                       (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
-                       (const float4 *)c->pfpcol.p, (int)n, (const unsigned long long *)c->itemmask.p,
+                       (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
   BSA_HIP(c, hipGetLastError());
