@@ -1527,8 +1527,11 @@ constexpr int kExactRec = 0, kExactKwik = 1, kExactHome = 2;
 #ifndef BSA_EXACT_WAVES
 #define BSA_EXACT_WAVES 4
 #endif
+#ifndef BSA_EXACT_HOME_WAVES
+#define BSA_EXACT_HOME_WAVES 2
+#endif
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kExactHome ? 2 : BSA_EXACT_WAVES, 8))) void k_exact(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kExactHome ? BSA_EXACT_HOME_WAVES : BSA_EXACT_WAVES, 8))) void k_exact(
     const RowRec *__restrict__ R, const ColRec *__restrict__ C,
     const unsigned *__restrict__ perm_r, const unsigned *__restrict__ perm_c,
     const uint2 *__restrict__ cand, Counters *__restrict__ cnt, SoA6 hs,
