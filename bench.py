@@ -38,7 +38,8 @@ PF_FLOPS_PER_PAIR = 9        # prefilter stage-1 fp32 flops per tested pair (DES
 KIN_BYTES_PER_AC = 234       # K4 algorithmic HBM bytes per aircraft-step
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E (spec)
 PMC_JSON = os.path.join(REPO, 'profiles', 'pmc_latest.json')
-TIMING_SAMPLE = 4            # detects per HIP-event-timed detect (bsa_set_timing_sample)
+TIMING_SAMPLE = 8            # detects per HIP-event-timed detect (bsa_set_timing_sample; each timed one
+                             # costs ~24 us of event bubbles, profiles/r02 kernel trace)
 
 
 def pmc_figures():

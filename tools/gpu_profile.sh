@@ -3,7 +3,7 @@
 # bench line (with the CPU baseline).  Counter passes are separate runs with
 # --kernel-trace only (no sys/runtime trace), each under its own time limit.
 set -u
-TAG=${TAG:-r02b}
+TAG=${TAG:-r02c}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
