@@ -781,7 +781,7 @@ constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 // measurements; results never depend on it)
 struct PfKnobs {
   int shards;  // dequeue counters in use (power of two <= kWorkShards)
-  int pieces;  // work items per (tile pair, 64-row slice): 1, 2 or 4
+  int pieces;  // work items per (tile pair, 64-row slice): 1, 2, 4 (or 8, BSA_PF_PIECES)
 };
 #ifndef BSA_PF_WAVES_PER_EU
 #define BSA_PF_WAVES_PER_EU 4
@@ -953,9 +953,11 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // column tile is fetched into that XCD's L2 once instead of into all eight.
   static_assert(PF_ITEMS_PER_TILE == 8, "item id layout: 3 bits of slice");
   // pieces > 1: an item's column mask is split into that many pieces, each a
-  // work item of its own -- when there are fewer items than waves (one rank's
-  // share of a multi-GPU step) the densest items, ~60 us each, set the sweep's
-  // span otherwise (tools/pf_trace.py); empty pieces are skipped like empty items
+  // work item of its own, piece p taking the set bits of rank p mod pieces (an
+  // equal share of the sub-groups; contiguous quarters of the mask were uneven
+  // where the dense columns bunch) -- the densest items, 60-85 us each, set the
+  // sweep's span otherwise (tools/pf_trace.py: at the 100k box the last item
+  // starts at 67 us of 97); empty pieces are skipped like empty items
   const unsigned long long nitems = ((ntiles + 7) / 8) * 64 * (unsigned)kn.pieces;
   const unsigned shard = blockIdx.x & (kn.shards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
@@ -1030,10 +1032,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       const TileBox rg = gbox_r[((int)rc.x * kTile) / kGroup + (int)slice];
       gm = __ballot(lane < nsub && (noprune || boxes_may_interact(rg, sb)));
     }
-    if (kn.pieces > 1) {
-      const unsigned w = 64u / (unsigned)kn.pieces;
-      gm &= ((1ull << w) - 1ull) << (w * piece);
-    }
+    if (kn.pieces > 1)  // piece p: the set bits of rank p, p + pieces, ... (equal shares of a dense mask)
+      gm = __ballot(((gm >> lane) & 1ull) && (lane_prefix(gm) & (unsigned)(kn.pieces - 1)) == piece);
     if (!gm) break;
     subs += (unsigned)__popcll(gm);
 #ifdef BSA_PF_TRACE
@@ -2134,8 +2134,11 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // fewer rows split the items (BSA_PF_PIECES overrides)
   static const int pieces_env = getenv("BSA_PF_PIECES") ? atoi(getenv("BSA_PF_PIECES")) : 0;
   PfKnobs kn = kn0;
-  kn.pieces = nrows >= (1 << 16) ? 1 : (nrows >= (1 << 14) ? 2 : 4);
-  if (pieces_env == 1 || pieces_env == 2 || pieces_env == 4) kn.pieces = pieces_env;
+  // (measured, tools/gpu_pieces.sh: 2 pieces at the 100k box, 102 -> 97 us; 4 for
+  // one rank of 8 there, 36 -> 29 us; 2 at 125k rows of 1M, 65 -> 53 us; 1
+  // from 250k rows up, where 2 cost +15 us)
+  kn.pieces = nrows >= 3 * (1 << 16) ? 1 : (nrows >= (1 << 15) ? 2 : 4);
+  if (pieces_env == 1 || pieces_env == 2 || pieces_env == 4 || pieces_env == 8) kn.pieces = pieces_env;
 #ifdef BSA_PF_TRACE
   {
     static DevBuf tb;

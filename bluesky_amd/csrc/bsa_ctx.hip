@@ -196,7 +196,7 @@ void bsa_destroy(bsa_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   bsa::DevBuf *all[] = {&c->rowrec, &c->colrec, &c->pfrow, &c->pfcol, &c->counters, &c->cand,
-                        &c->ckey, &c->cval, &c->ckey2, &c->cval2, &c->cpay, &c->lkey, &c->lkey2,
+                        &c->ckey, &c->cval, &c->ckey2, &c->cval2, &c->cpay, &c->kbuck, &c->lkey, &c->lkey2,
                         &c->out_ci, &c->out_cj, &c->out_li, &c->out_lj, &c->out_pay, &c->inconf,
                         &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage, &c->mvp_pdv, &c->mvp_pfl,
                         &c->pfvrow, &c->pfvcol, &c->pfprow, &c->pfpcol, &c->key_r, &c->idx_r, &c->key_r2, &c->perm_r,
