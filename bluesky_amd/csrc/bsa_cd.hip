@@ -792,52 +792,6 @@ static_assert(kSubsPerTile == 64, "one sub-group box per lane");
 constexpr int kSubsPerBatch = 64 / kSub;  // sub-groups per 64-column batch
 static_assert(PF_Q1 >= 64 * 8, "one 8-column chunk of survivors fits the stage-1 queue");
 
-// K0e: for every work item (tile pair, 64-row slice) the 64-bit mask of the
-// column tile's 8-column sub-groups whose boxes may interact with the slice's
-// row box (boxes_may_interact: the stage-1 test applied to box gaps), so the
-// sweep starts an item with one scalar load instead of a chain of dependent
-// loads (tile pair -> row box -> 64 sub-group boxes, 3 KB per item).  One wave
-// per tile pair: its 64 sub-group boxes are loaded once (one per lane) and
-// tested against the 8 row-slice boxes (lanes 0..7, all loads up front).
-__global__ __launch_bounds__(256) void k_items(int nrows, int ncols, const TileBox *__restrict__ gbox_r,
-                                               const TileBox *__restrict__ sbox_c, const uint2 *__restrict__ tiles,
-                                               unsigned long long tcap, const Counters *__restrict__ cnt, int noprune,
-                                               unsigned long long *__restrict__ masks,
-                                               const unsigned *__restrict__ build) {
-  if (build && !build[0]) return;
-  const unsigned long long ntiles = cnt->tiles, near = cnt->tiles_near;
-  const int lane = threadIdx.x & 63;
-  const unsigned long long nw = ((unsigned long long)gridDim.x * blockDim.x) >> 6;
-  for (unsigned long long tp = ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; tp < ntiles;
-       tp += nw) {
-    const uint2 rc = tile_at(tiles, tp, near, tcap);
-    const int cbase = (int)rc.y * kTile;
-    const int nsub = min(kSubsPerTile, (ncols - cbase + kSub - 1) / kSub);
-    const bool have = lane < nsub;
-    TileBox sb, rbl;
-    if (have) sb = sbox_c[cbase / kSub + lane];
-    const int nslice = min(PF_ITEMS_PER_TILE, (nrows - (int)rc.x * kTile + PF_WROWS - 1) / PF_WROWS);
-    if (lane < nslice) rbl = gbox_r[((int)rc.x * kTile) / kGroup + lane];
-    for (int sl = 0; sl < PF_ITEMS_PER_TILE; ++sl) {
-      bool gk = false;
-      if (sl < nslice) {
-        TileBox a;
-        auto bc = [&](float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), sl)); };
-        for (int q = 0; q < 3; ++q) {
-          a.lo[q] = bc(rbl.lo[q]);
-          a.hi[q] = bc(rbl.hi[q]);
-        }
-        a.vlo = bc(rbl.vlo);
-        a.vhi = bc(rbl.vhi);
-        a.smax = bc(rbl.smax);
-        gk = have && (noprune || boxes_may_interact(a, sb));
-      }
-      const unsigned long long m = __ballot(gk);
-      if (lane == 0) masks[tp * PF_ITEMS_PER_TILE + sl] = m;
-    }
-  }
-}
-
 // Diagnostic item timeline (build with -DBSA_PF_TRACE; `make trace`,
 // tools/pf_trace.py): per work item {item, wave << 8 | sub-groups, start,
 // end} (s_memrealtime, 100 MHz) into a per-wave region of pf_trace (no
@@ -937,8 +891,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // wave dequeues items from the counter of its shard (blockIdx % shards,
   // 128 B apart; a returning atomic on one word saturates at ~88 per us).
   // Near tile pairs (the costly ones) come first in the list.  An item's
-  // sub-group mask comes from K0e (k_items): one scalar load, no dependent
-  // box loads.  (Measured slower: claiming the next item ahead (+20 us, also
+  // sub-group mask is formed as it starts (below).  (Measured slower: claiming the next item ahead (+20 us, also
   // without spills: a returning atomic in flight joins every later in-order
   // vmcnt wait, so its latency is moved, not hidden); several items per
   // dequeue, or PF_GROUP consecutive tile pairs of one slice per item sharing
@@ -2083,8 +2036,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (!ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
       !ensure(c, c->gbox_c, ngc * sizeof(TileBox), "column group boxes") ||
       !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
-      !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs") ||
-      !ensure(c, c->itemmask, (size_t)ntp * PF_ITEMS_PER_TILE * 8, "item masks"))
+      !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
     return -1;
   FusedBoxes fb{nullptr, nullptr, nullptr};
   ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};

@@ -152,9 +152,9 @@ struct Ctx {
   DevBuf rowrec, colrec, pfrow, pfcol, pfvrow, pfvcol, pfprow, pfpcol;
   // spatial order: Morton keys and the sorted-position -> original-index maps
   DevBuf key_r, idx_r, key_r2, perm_r, key_c, idx_c, key_c2, perm_c;
-  DevBuf tbox_r, tbox_c, gbox_r, gbox_c, sbox_c, tilepairs, itemmask, workq;
-  DevBuf rowcnt, rowoff, lslot;  // K2 counting sort
-  DevBuf kbuck, kslot;           // K2 row buckets (column indices) and each candidate's slots
+  DevBuf tbox_r, tbox_c, gbox_r, gbox_c, sbox_c, tilepairs, workq;
+  DevBuf rowcnt, rowoff;         // K2 counting sort
+  DevBuf kbuck;                  // K2 row buckets (column indices)
   int k2_bucket = 8;             // bucket width (pairs per row); 0 = scatter into row segments
   DevBuf scan_ws;                // single-pass scan: [0] ticket counter, then tile status words
   bool scan_ready = false;
