@@ -731,8 +731,13 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // any NaN keeps the pair.
 __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, const float4 &cp,
                                           const float4 &cv, const RefineParams &prm) {
+  // Branch-free: every lane evaluates every test and the decision is one
+  // select at the end -- the same values and the same keep / reject outcome as
+  // testing them in order with early returns (far or clamped pairs are kept
+  // whatever the rest says), without the exec-mask bookkeeping and the
+  // per-branch LDS waits of the early-exit form.
   const float dx = cp.x - rp.x, dy = cp.y - rp.y, dz = cp.z - rp.z;
-  if (dx * dx + dy * dy + dz * dz > (float)(kRefineChord * kRefineChord)) return true;  // > ~190 km: keep
+  const bool far = dx * dx + dy * dy + dz * dz > (float)(kRefineChord * kRefineChord);  // > ~190 km: keep
   // chord projected on the row's local east / north basis
   //   e = (-y, x, 0) / rho,  n = (-z x / rho, -z y / rho, rho),  rho = cos(lat)
   // (from the fp32 unit vector; |lat| > ~89.4 deg rows are flagged)
@@ -743,32 +748,30 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
   const float pn = (dz * rho - rp.z * (dx * rp.x + dy * rp.y) * irho) * kRS;
   const float ve = cv.x - rv.x, vn = cv.y - rv.y;          // own.u[j] - int.u[i]
   const float vv = ve * ve + vn * vn;
-  if (!(vv >= 4e-6f)) return true;                         // reference may clamp dv2; NaN
+  const bool clamp = !(vv >= 4e-6f);                       // reference may clamp dv2; NaN
   const float dalt = cv.w - rv.w;                          // own.alt[j] - int.alt[i]
   const float H = prm.H + (rp.w + cp.w);                   // + vertical budgets (reuse; else 0)
   const float dvs = cv.z - rv.z;
   const float adv = __builtin_fabsf(dvs);
-  float t0 = 0.f, t1 = prm.T;
   // reciprocals by v_rcp_f32 (1 ulp): every division here only places a
   // window edge or the closest-approach time, and the margins below are
   // many orders of magnitude wider than 1 ulp
-  if (adv < 1e-3f) {
-    if (__builtin_fabsf(dalt) >= H + 1e-3f * prm.T + 2.f + 1e-5f * __builtin_fabsf(dalt)) return false;
-  } else {
-    const float inv = __builtin_amdgcn_rcpf(dvs);
-    const float ta = (-H - dalt) * inv, tb = (H - dalt) * inv;
-    const float lo = fminf(ta, tb), hi = fmaxf(ta, tb);
-    const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + H)) * __builtin_fabsf(inv) +
-                    1e-4f * fmaxf(__builtin_fabsf(lo), __builtin_fabsf(hi));
-    t0 = fmaxf(lo - d, 0.f);
-    t1 = fminf(hi + d, prm.T);
-    if (t0 > t1) return false;
-  }
+  const bool level = adv < 1e-3f;
+  const bool level_out = __builtin_fabsf(dalt) >= H + 1e-3f * prm.T + 2.f + 1e-5f * __builtin_fabsf(dalt);
+  const float inv = __builtin_amdgcn_rcpf(dvs);
+  const float ta = (-H - dalt) * inv, tb = (H - dalt) * inv;
+  const float lo = fminf(ta, tb), hi = fmaxf(ta, tb);
+  const float d = (2.f + 1e-5f * (__builtin_fabsf(dalt) + H)) * __builtin_fabsf(inv) +
+                  1e-4f * fmaxf(__builtin_fabsf(lo), __builtin_fabsf(hi));
+  const float w0 = fmaxf(lo - d, 0.f), w1 = fminf(hi + d, prm.T);
+  const bool vout = level ? level_out : (w0 > w1);
+  const float t0 = level ? 0.f : w0, t1 = level ? prm.T : w1;
   const float tl = t0 * (1.f - kE1), th = t1 * (1.f + 2.f * kE1);
   float ts = -(pe * ve + pn * vn) * __builtin_amdgcn_rcpf(vv);
   ts = fminf(fmaxf(ts, tl), th);
   const float qe = pe + ve * ts, qn = pn + vn * ts;
-  return !(qe * qe + qn * qn > prm.lim2);
+  const bool hout = qe * qe + qn * qn > prm.lim2;
+  return far | clamp | !(vout | hout);
 }
 
 #ifndef PF_Q1
