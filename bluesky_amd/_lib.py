@@ -172,6 +172,22 @@ SIGNATURES.update({
     'bsa_sim_acdata_poll': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(AcData)]),
 })
 
+
+
+class AsasOut(ctypes.Structure):
+    """bsa_asas_out (include/bsaccel.h)."""
+    _fields_ = [(k, _c_dp) for k in ('trk', 'tas', 'vs', 'alt')] + [('asase', _c_fp), ('asasn', _c_fp),
+                                                                   ('active', _c_u8p), ('dropped', _c_u8p)]
+
+
+SIGNATURES.update({
+    'bsa_sim_cd': (ctypes.c_int, [_vp]),
+    'bsa_sim_set_params': (ctypes.c_int, [_vp, ctypes.POINTER(SimParams)]),
+    'bsa_sim_set_reso_lists': (ctypes.c_int, [_vp, _c_u8p, _c_u8p]),
+    'bsa_sim_read_asas': (ctypes.c_int, [_vp, ctypes.POINTER(AsasOut)]),
+    'bsa_sim_halo_stats': (ctypes.c_int, [_vp, _c_i64p]),
+})
+
 UNIQUE_ID_BYTES = 128
 
 _lib = None
@@ -585,6 +601,38 @@ class Context:
         self.gen += 1
         self.check(self.lib.bsa_sim_step(self.h, int(nsteps)), 'bsa_sim_step')
 
+    def sim_cd(self):
+        """bsa_sim_cd: one CD call (detect -> resolver -> bookkeeping) without kinematics."""
+        self.gen += 1
+        self.check(self.lib.bsa_sim_cd(self.h), 'bsa_sim_cd')
+
+    def sim_set_params(self, params):
+        """bsa_sim_set_params: new rpz / hpz / tla / MVP switches for a running sim."""
+        self.check(self.lib.bsa_sim_set_params(self.h, ctypes.byref(params)), 'bsa_sim_set_params')
+
+    def sim_set_reso_lists(self, noreso=None, resooff=None):
+        """bsa_sim_set_reso_lists: NORESO / RESOOFF membership (full-n bool-like arrays, None = empty)."""
+        keep = [None if a is None else np.ascontiguousarray(a, dtype=np.uint8).ravel() for a in (noreso, resooff)]
+        for a in keep:
+            if a is not None and len(a) != self.n:
+                raise ValueError('membership array has length %d != %d' % (len(a), self.n))
+        self.check(self.lib.bsa_sim_set_reso_lists(self.h, ptr(keep[0], _c_u8p), ptr(keep[1], _c_u8p)),
+                   'bsa_sim_set_reso_lists')
+
+    def sim_read_asas(self):
+        """bsa_sim_read_asas: asas trk / tas / vs / alt, asase / asasn, active and the
+        ResumeNav drops of this rank's rows (full-n arrays, other rows 0)."""
+        n = self.n
+        o = {k: np.zeros(n) for k in ('trk', 'tas', 'vs', 'alt')}
+        o.update(asase=np.zeros(n, np.float32), asasn=np.zeros(n, np.float32), active=np.zeros(n, np.uint8),
+                 dropped=np.zeros(n, np.uint8))
+        ao = AsasOut(**{k: ptr(o[k]) for k in ('trk', 'tas', 'vs', 'alt')}, asase=ptr(o['asase'], _c_fp),
+                     asasn=ptr(o['asasn'], _c_fp), active=ptr(o['active'], _c_u8p), dropped=ptr(o['dropped'], _c_u8p))
+        self.check(self.lib.bsa_sim_read_asas(self.h, ctypes.byref(ao)), 'bsa_sim_read_asas')
+        o['active'] = o['active'].astype(bool)
+        o['dropped'] = o['dropped'].astype(bool)
+        return o
+
     def sim_read(self):
         n = self.n
         o = {k: np.empty(n) for k in SIM_OUT_FIELDS}
@@ -621,6 +669,13 @@ class Context:
         self.gen += 1
         self._rows = (int(row_begin), int(row_end))
         return nc.value, nl.value
+
+    def sim_halo_stats(self):
+        """bsa_sim_halo_stats: bytes received / sent per CD call, tiles received at the
+        last CD call (or needed by the last bsa_sim_detect_rows share), regrowths."""
+        v = np.zeros(4, np.int64)
+        self.check(self.lib.bsa_sim_halo_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_halo_stats')
+        return dict(rx_bytes=int(v[0]), tx_bytes=int(v[1]), tiles=int(v[2]), regrowths=int(v[3]))
 
     def sim_asas_stats(self):
         """ASAS bookkeeping counts after the last CD call (resume_nav on); the

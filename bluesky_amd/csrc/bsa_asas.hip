@@ -57,6 +57,7 @@ struct BkIn {
   const unsigned *nptr;    // next CSR pointers (write pass)
   unsigned *ncol;
   uint8_t *active;         // full-N
+  uint8_t *dropped;        // full-N (home order) or NULL: the row dropped a pair this call
   unsigned long long *stats;
 };
 
@@ -133,15 +134,18 @@ __global__ __launch_bounds__(256) void k_bk_write(BkIn in) {
   if (r >= in.nrows) return;
   const int i = in.rb + r;
   unsigned pos = in.nptr[r];
-  bool any = false, seen = false;
+  bool any = false, seen = false, drop = false;
   bk_merge(in, r, [&](unsigned j) {
     seen = true;
     if (bk_keep(in, i, (int)j)) {
       in.ncol[pos++] = j;
       any = true;
+    } else {
+      drop = true;  // asas.py:454-468: ASAS off, waypoint recovery (route.direct) for the ownship
     }
   });
   if (seen) in.active[i] = any ? 1 : 0;
+  if (in.dropped) in.dropped[i] = drop ? 1 : 0;
 }
 
 // is (r, c) in the CSR (ptr over rows 0.., ascending cols)?
@@ -356,6 +360,7 @@ static BkIn bk_in(Ctx *c, const BkDev &d) {
   in.nptr = (const unsigned *)c->bk_nptr.p;
   in.ncol = (unsigned *)c->bk_ncol.p;
   in.active = d.active;
+  in.dropped = d.dropped;
   in.stats = (unsigned long long *)c->bk_stats.p;
   return in;
 }

@@ -25,6 +25,7 @@
 // of separation, and K1b evaluates the survivors exactly.
 #include <hipcub/hipcub.hpp>
 
+#include "bsa_box.h"
 #include "bsa_geo_math.h"
 #include "bsa_internal.h"
 #include "bsa_mvp_math.h"
@@ -330,15 +331,21 @@ __device__ __forceinline__ ColRec col_record(const SoA6 &own, const SoA6 &intr, 
 // the few it needs from the state arrays with col_record itself.
 // presorted: the state arrays are already in sorted (home) order, perm only
 // names the aircraft (the resident sim): record k reads index k, coalesced.
+// Tiles: workgroup b prepares tile tile_base + b, or tile_list[b] (a halo
+// tile list of the row-sharded step, -1 = unused slot).
 __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__restrict__ perm, int presorted, int rec,
                                                      SoA6 own, SoA6 intr, int distinct, int shared,
                                                      double rpz, double hpz, double tla,
                                                      ColRec *__restrict__ C, PFRec *__restrict__ PC,
                                                      PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
-                                                     ReuseParams rz, FusedBoxes fb, ZeroArgs zs) {
+                                                     ReuseParams rz, FusedBoxes fb, ZeroArgs zs, int tile_base,
+                                                     const int *__restrict__ tile_list) {
   __shared__ TileBox fgb[kTile / 64];
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (zs.cnt) zero_state(zs, k, gridDim.x * blockDim.x);  // K0z (fused): nothing here reads that state
+  // K0z (fused): nothing here reads that state
+  if (zs.cnt) zero_state(zs, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+  const int tile = tile_list ? tile_list[blockIdx.x] : tile_base + (int)blockIdx.x;
+  if (tile < 0) return;  // (the whole workgroup: no barrier is skipped by part of it)
+  const int k = tile * kTile + (int)threadIdx.x;
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
   if (k < cnt) {
@@ -420,7 +427,7 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
     }
   }
   // K0c (fused): this thread wrote PC[k] above, every thread reaches the barrier
-  if (fb.gbox) tile_boxes(cnt, blockIdx.x, PC, fgb, fb.sbox, fb.gbox, fb.tbox);
+  if (fb.gbox) tile_boxes(cnt, tile, PC, fgb, fb.sbox, fb.gbox, fb.tbox);
 }
 
 // ------------------------------------------------------------------ K0c tile boxes
@@ -443,20 +450,6 @@ constexpr int kGroupsPerTile = kTile / kGroup;
 constexpr int kSub = 8;  // column sub-group (culling granularity; one stage-1 chunk)
 static_assert(kGroup % kSub == 0 && (kSub & (kSub - 1)) == 0, "sub-groups tile a group");
 
-__device__ __forceinline__ TileBox box_union(const TileBox &a, const TileBox &b) {
-  TileBox u;
-  for (int q = 0; q < 3; ++q) {
-    u.lo[q] = fminf(a.lo[q], b.lo[q]);
-    u.hi[q] = fmaxf(a.hi[q], b.hi[q]);
-  }
-  u.vlo = fminf(a.vlo, b.vlo);
-  u.vhi = fmaxf(a.vhi, b.vhi);
-  u.smax = fmaxf(a.smax, b.smax);
-  u.pad0 = 0.f;
-  u.count = a.count + b.count;
-  u.pad1 = 0;
-  return u;
-}
 
 // Counters words that belong to the candidate list (kept across detects by reuse)
 __device__ __forceinline__ bool list_word(int k) {
@@ -571,21 +564,6 @@ __device__ __forceinline__ unsigned wave_incl_scan(unsigned x) {
 }
 
 // ------------------------------------------------------------------ K0d tile pairs
-__device__ __forceinline__ float gap(float alo, float ahi, float blo, float bhi) {
-  return fmaxf(0.f, fmaxf(alo - bhi, blo - ahi));
-}
-
-// Can any pair of the two boxes pass stage 1?  Horizontally the gaps bound the
-// chord from below and s_i + s_j <= smax_a + smax_b; vertically stage 1 needs
-// lo_j < hi_i and hi_j > lo_i, so the [vlo, vhi] intervals must overlap.
-__device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileBox &b) {
-  const float gx = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]);
-  const float gy = gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]);
-  const float gz = gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]);
-  const float d2 = gx * gx + gy * gy + gz * gz;
-  const float st = (a.smax + b.smax) * 1.00001f + 1e-5f;
-  return !(d2 >= st * st) && (b.vlo < a.vhi) && (b.vhi > a.vlo);
-}
 
 // K0d: the kept tile pairs, listed in two classes: pairs whose boxes overlap
 // ("near": a row tile against itself and its neighbours, the costly items)
@@ -607,11 +585,17 @@ __device__ __forceinline__ uint2 tile_at(const uint2 *__restrict__ list, unsigne
                                          unsigned long long near, unsigned long long cap) {
   return list[k < near ? k : cap - 1 - (k - near)];
 }
+// present (halo mode, nullable): column tiles whose data this rank holds --
+// its own [p0, p1) and the halo tiles it received.  A kept pair with any
+// other column tile means the halo plan disagreed with this test (it cannot:
+// the plan runs the same boxes_may_interact on the same boxes): it is flagged
+// (cnt->halo_miss, the step fails loudly), never silently dropped or swept.
 __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, const TileBox *__restrict__ rb,
                                                           const TileBox *__restrict__ cb, int noprune,
                                                           uint2 *__restrict__ out, unsigned long long cap,
                                                           Counters *__restrict__ cnt,
-                                                          const unsigned *__restrict__ build) {
+                                                          const unsigned *__restrict__ build,
+                                                          const uint8_t *__restrict__ present, int p0, int p1) {
   if (build && !build[0]) return;
   __shared__ TileBox srt[kSuper];            // this super row's tile boxes
   __shared__ unsigned keep[kTPThreads];      // kept super columns of the chunk
@@ -657,7 +641,9 @@ __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, cons
         ct = (int)sc2 * kSuper + (int)(r % kSuper);
         if (i < nr && ct < nct) {
           const TileBox a = srt[i], b = cb[ct];
-          if (noprune || boxes_may_interact(a, b)) {
+          if ((noprune || boxes_may_interact(a, b)) && present && !(ct >= p0 && ct < p1) && !present[ct]) {
+            cnt->halo_miss = 1;
+          } else if (noprune || boxes_may_interact(a, b)) {
             const bool near = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]) == 0.f &&
                               gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]) == 0.f &&
                               gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]) == 0.f;
@@ -1400,6 +1386,7 @@ __device__ __forceinline__ unsigned long long cand_prefix(const Counters *cnt, u
 __device__ __forceinline__ bool cand_overflow(const Counters *cnt, unsigned long long cap) {
   const unsigned long long ccap = cap / kCandShards;
   bool o = cnt->k2_demand != 0;  // a K2 row bucket was full: retried with wider buckets
+  o |= cnt->halo_ovf != 0 || cnt->halo_miss != 0;  // halo tiles missing: the step is re-run
 #pragma unroll
   for (int q = 0; q < kCandShards; ++q) o |= cnt->cshard[q][0] > ccap;
   return o;
@@ -1835,6 +1822,41 @@ static int next_events(Ctx *c, hipEvent_t **ev) {
   return 0;
 }
 
+// stage 1 at the look-ahead midpoints unless KWIK, candidate
+// reuse, BSA_FLAG_STAGE1_T0 or the BSA_STAGE1_T0 environment variable
+static int stage1_mid(int flags, bool reuse, int kwik) {
+  static const bool t0_env = getenv("BSA_STAGE1_T0") && atoi(getenv("BSA_STAGE1_T0")) != 0;
+  return (!reuse && !kwik && !(flags & BSA_FLAG_STAGE1_T0) && !t0_env) ? 1 : 0;
+}
+
+static SoA6 soa(const DevBuf *a) {
+  return SoA6{(const double *)a[0].p, (const double *)a[1].p, (const double *)a[2].p,
+              (const double *)a[3].p, (const double *)a[4].p, (const double *)a[5].p};
+}
+
+int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla) {
+  const int64_t n = c->n;
+  if (n <= 0) return 0;
+  const int nct = (int)((n + kTile - 1) / kTile);
+  if (!ensure(c, c->colrec, n * sizeof(ColRec), "column records") ||
+      !ensure(c, c->pfcol, n * sizeof(PFRec), "prefilter columns") ||
+      !ensure(c, c->pfvcol, n * sizeof(PFVel), "prefilter column velocities") ||
+      !ensure(c, c->pfpcol, n * sizeof(float4), "prefilter column positions") ||
+      !ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
+      !ensure(c, c->gbox_c, ((n + kGroup - 1) / kGroup) * sizeof(TileBox), "column group boxes") ||
+      !ensure(c, c->sbox_c, ((n + kSub - 1) / kSub) * sizeof(TileBox), "column sub-group boxes"))
+    return -1;
+  const SoA6 own = soa(c->own);
+  const FusedBoxes fb{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p};
+  const ZeroArgs zs{0, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)nct), dim3(kTile), 0, c->stream, (int)n,
+                     (const unsigned *)c->h2id.p, 1, 0, own, own, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
+                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, stage1_mid(0, false, 0),
+                     ReuseParams{}, fb, zs, 0, (const int *)nullptr);
+  BSA_HIP(c, hipGetLastError());
+  return 0;
+}
+
 // Enqueue one complete detect on the stream (K0-K2), no host synchronisation.
 // gate (device, nullable): receives {overflow, P} for the resident sim step.
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
@@ -1865,6 +1887,11 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // slice [rb, re) of the columns (no re-sort, no gather)
   const bool home = c->det_home;
   c->last_home = home;
+  // halo mode (home mode of the row-sharded step, or its one-GPU probe): K0
+  // prepares the rank's own column tiles [a0, a1), halo_mid plans / exchanges
+  // the tiles its rows can reach, K0 prepares those from the list
+  const bool halo = home && c->halo_mode != 0;
+  const int a0 = (int)(rb / kTile), a1 = (int)((re + kTile - 1) / kTile);
   // home mode: K1b builds its fp64 records from the state arrays instead of
   // reading 128-B records K0b wrote for EVERY column: cheaper when K0b's
   // record writes dominate -- at 1M (0.165 -> 0.084 ms of K0) or for one rank's
@@ -1885,14 +1912,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // whole range is detected; only then can the candidate list be reused
   const bool shared = home || (!distinct && rb == 0 && re == n);
   const int64_t roff = home ? rb : 0;  // the rows' offset in the shared records
-  const bool reuse = c->reuse_on && shared && rb == 0 && re == n && !noprune && !kwik && n > 0;
+  const bool reuse = c->reuse_on && shared && rb == 0 && re == n && !noprune && !kwik && n > 0 && !halo;
   if (!reuse) c->reuse_valid = false;
   // stage 1 at the look-ahead midpoints: its bound is derived
   // for the great-circle geometry and fixed reaches, so not with KWIK nor with
   // the reuse budgets (whose drift checks assume t = 0 points); the
   // BSA_STAGE1_T0 environment variable selects t = 0 for A/B measurements
-  static const bool t0_env = getenv("BSA_STAGE1_T0") && atoi(getenv("BSA_STAGE1_T0")) != 0;
-  const int mid = (!reuse && !kwik && !(flags & BSA_FLAG_STAGE1_T0) && !t0_env) ? 1 : 0;
+  const int mid = stage1_mid(flags, reuse, kwik);
   // stage events of this detect: only one detect in ev_every is timed (each
   // record costs a ~5 us bubble before the next kernel, bsa_set_timing_sample)
   hipEvent_t *ev = nullptr;
@@ -1916,6 +1942,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   };
   if (n == 0 || nrows == 0) {
     if (zero(false, nullptr, 0)) return -1;
+    if (halo && halo_mid(c, rb, re)) return -1;  // a rank without rows still takes part in the exchange
     if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
     for (int e = 1; e < 5; ++e)
       if (mark(e)) return -1;
@@ -2048,11 +2075,23 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     zs = ZeroArgs{(int)nrows, 1, 0, dcnt, (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
                   (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p};
   }
-  hipLaunchKernelGGL(k_prep_cols, dim3(blocks_for(n, kTile)), dim3(kTile), 0, c->stream, (int)n, perm_c,
-                     home ? 1 : 0, recs ? 1 : 0, own,
+  hipLaunchKernelGGL(k_prep_cols, dim3(halo ? (unsigned)(a1 - a0) : blocks_for(n, kTile)), dim3(kTile), 0,
+                     c->stream, (int)n, perm_c, home ? 1 : 0, recs ? 1 : 0, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
-                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs);
+                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs,
+                     halo ? a0 : 0, (const int *)nullptr);
   BSA_HIP(c, hipGetLastError());
+  if (halo) {
+    if (halo_mid(c, rb, re)) return -1;
+    if (c->halo_hl > 0) {  // the received tiles' records and boxes (no per-detect zeroing here)
+      const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+      hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)c->halo_hl), dim3(kTile), 0, c->stream, (int)n, perm_c, 1,
+                         recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
+                         (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs2, 0,
+                         (const int *)c->h_hl.p);
+      BSA_HIP(c, hipGetLastError());
+    }
+  }
 
   // ---- K0c/K0d group / tile boxes (rows; columns when reused) and the tile-pair work list
   if (!shared && (!ensure(c, c->tbox_r, nrt * sizeof(TileBox), "row tile boxes") ||
@@ -2069,7 +2108,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
                      nrt, nct, tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
-                     (unsigned long long)ntp, dcnt, build);
+                     (unsigned long long)ntp, dcnt, build, halo ? halo_present(c) : nullptr, a0, a1);
   BSA_HIP(c, hipGetLastError());
   // (K0e, an item's column sub-group mask, is evaluated by K1a as the item starts)
   if (mark(1)) return -1;
@@ -2158,7 +2197,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
         !ensure(c, c->mvp_pfl, std::max<unsigned long long>(cap, 1), "mvp pair flags"))
       return -1;
     mf.p = *c->fuse_mvp;
-    mf.in = MvpPairIn{c->fuse_gse, c->fuse_gsn, c->fuse_vs, c->fuse_alt, nullptr,
+    mf.in = MvpPairIn{c->fuse_gse, c->fuse_gsn, c->fuse_vs, c->fuse_alt, c->fuse_noreso,
                       c->det_home ? (const unsigned *)c->id2h.p : nullptr};
     mf.pdv = (double4 *)c->mvp_pdv.p;
     mf.pfl = (uint8_t *)c->mvp_pfl.p;

@@ -42,6 +42,7 @@ struct Group {
   int arrived = 0;
   unsigned long long phase = 0;
   bool broken = false;
+  bool destroy_pending = false;           // bsa_group_destroy while members were still joined
   Ctx *ctx[kMaxGroup] = {};
   DevBuf slot[kMaxGroup];                 // each rank's published copy (its own device)
   hipEvent_t pub[kMaxGroup] = {}, done[kMaxGroup] = {};
@@ -165,8 +166,15 @@ int comm_allreduce_max_u64(Ctx *c, unsigned long long *buf, int count) {
   }
   Group *g = c->group;
   if (publish(c, buf, (size_t)count * 8)) return -1;
+  // stage every peer's slot into this rank's scratch with copies (the group
+  // may span devices without peer access), then reduce locally
+  const size_t b = (size_t)count * 8;
+  if (!ensure(c, c->red, b * g->n, "reduction scratch")) return -1;
   SlotPtrs s{};
-  for (int q = 0; q < g->n; ++q) s.p[q] = (const unsigned long long *)g->slot[q].p;
+  for (int q = 0; q < g->n; ++q) {
+    BSA_HIP(c, hipMemcpyAsync((char *)c->red.p + q * b, g->slot[q].p, b, hipMemcpyDeviceToDevice, c->stream));
+    s.p[q] = (const unsigned long long *)((const char *)c->red.p + q * b);
+  }
   hipLaunchKernelGGL(k_max_u64_slots, dim3(1), dim3(256), 0, c->stream, buf, count, g->n, s);
   BSA_HIP(c, hipGetLastError());
   return retire(c);
@@ -231,6 +239,39 @@ int comm_gatherv(Ctx *c, int root, const void *send, size_t bytes, void *recv, c
   return retire(c);
 }
 
+// Halo exchange (bsa_halo.hip): this rank's region for rank q is
+// send[soff[q], + slen[q]), rank q's region for this rank lands at
+// recv[roff[q], + rlen[q]); peer[q] = where that region starts in rank q's
+// send buffer (in-process group).  The lengths are agreed by all ranks (the
+// capacity matrix), so every send has its matching receive.
+int comm_halo(Ctx *c, const void *send, const size_t *soff, const size_t *slen, size_t stot, void *recv,
+              const size_t *roff, const size_t *rlen, const size_t *peer) {
+  if (!comm_multi(c)) return 0;
+  const int R = c->nranks, me = c->rank;
+  if (c->comm) {
+    bool any = false;
+    for (int q = 0; q < R; ++q) any = any || (q != me && (slen[q] || rlen[q]));
+    if (!any) return 0;
+    BSA_NCCL(c, ncclGroupStart());
+    for (int q = 0; q < R; ++q) {
+      if (q == me) continue;
+      if (slen[q])
+        BSA_NCCL(c, ncclSend((const char *)send + soff[q], slen[q], ncclUint8, q, (ncclComm_t)c->comm, c->stream));
+      if (rlen[q])
+        BSA_NCCL(c, ncclRecv((char *)recv + roff[q], rlen[q], ncclUint8, q, (ncclComm_t)c->comm, c->stream));
+    }
+    BSA_NCCL(c, ncclGroupEnd());
+    return 0;
+  }
+  Group *g = c->group;
+  if (publish(c, send, stot)) return -1;
+  for (int q = 0; q < R; ++q)
+    if (q != me && rlen[q])
+      BSA_HIP(c, hipMemcpyAsync((char *)recv + roff[q], (const char *)g->slot[q].p + peer[q], rlen[q],
+                                hipMemcpyDeviceToDevice, c->stream));
+  return retire(c);
+}
+
 void comm_release(Ctx *c) {
   if (c->comm) {
     ncclCommDestroy((ncclComm_t)c->comm);
@@ -238,16 +279,22 @@ void comm_release(Ctx *c) {
   }
   if (c->group) {
     Group *g = c->group;
-    std::lock_guard<std::mutex> lk(g->m);
-    if (g->ctx[c->rank] == c) {
-      (void)hipStreamSynchronize(c->stream);
-      release(g->slot[c->rank]);
-      if (g->pub[c->rank]) (void)hipEventDestroy(g->pub[c->rank]);
-      if (g->done[c->rank]) (void)hipEventDestroy(g->done[c->rank]);
-      g->pub[c->rank] = g->done[c->rank] = nullptr;
-      g->ctx[c->rank] = nullptr;
+    bool last = false;
+    {
+      std::lock_guard<std::mutex> lk(g->m);
+      if (g->ctx[c->rank] == c) {
+        (void)hipStreamSynchronize(c->stream);
+        release(g->slot[c->rank]);
+        if (g->pub[c->rank]) (void)hipEventDestroy(g->pub[c->rank]);
+        if (g->done[c->rank]) (void)hipEventDestroy(g->done[c->rank]);
+        g->pub[c->rank] = g->done[c->rank] = nullptr;
+        g->ctx[c->rank] = nullptr;
+      }
+      last = g->destroy_pending;
+      for (int q = 0; q < g->n; ++q) last = last && !g->ctx[q];
     }
     c->group = nullptr;
+    if (last) delete g;  // the group was destroyed while this context was its last member
   }
   c->nranks = 1;
   c->rank = 0;
@@ -293,7 +340,21 @@ bsa_group *bsa_group_create(int nranks) {
   return g;
 }
 
-void bsa_group_destroy(bsa_group *g) { delete g; }
+// a group still holding members is freed when its last member leaves
+// (bsa_destroy or a new bsa_comm_init*), never under a member's feet
+void bsa_group_destroy(bsa_group *g) {
+  if (!g) return;
+  {
+    std::lock_guard<std::mutex> lk(g->m);
+    bool members = false;
+    for (int q = 0; q < g->n; ++q) members = members || g->ctx[q] != nullptr;
+    if (members) {
+      g->destroy_pending = true;
+      return;
+    }
+  }
+  delete g;
+}
 
 int bsa_comm_init_group(bsa_ctx *cc, bsa_group *g, int rank) {
   Ctx *c = (Ctx *)cc;

@@ -1,0 +1,444 @@
+// Halo exchange of the row-sharded resident step.
+//
+// Rank r owns the home rows [r rpr, (r + 1) rpr): a spatially compact chunk
+// of the traffic whose 512-row tiles are column tiles of the detect.  Its
+// rows can only conflict with column tiles whose boxes pass the tile-pair
+// test (boxes_may_interact, bsa_box.h) against one of its row tiles, so
+// instead of all-gathering the whole state before every CD call (48 MB at 1M
+// aircraft) each rank
+//   1. prepares its OWN column tiles (K0b, with their boxes);
+//   2. all-gathers the tile boxes (48 B per tile) and a request bitmask of the
+//      tiles holding its resopairs' intruders (ResumeNav reads their state,
+//      asas.py:424-452, wherever they are by now);
+//   3. plans (k_halo_plan): tile t of rank s goes to rank q iff t passes the
+//      box test against some row tile of q, or q requested it -- every rank
+//      evaluates the same test on the same (gathered, bitwise) boxes from its
+//      own side, and the test is symmetric, so sender and receiver agree;
+//   4. exchanges the planned tiles' state (lat lon trk gs alt vs, and gseast /
+//      gsnorth unless they follow from gs / trk) with one grouped RCCL
+//      send / recv per neighbour (device copies in the in-process group),
+//      into the same home positions of the replicated arrays;
+//   5. prepares the received tiles (K0b over the flat halo list).
+// K0d (k_tilepairs) then lists tile pairs of present column tiles only; a
+// kept pair with a missing tile would be a plan bug and is flagged
+// (Counters::halo_miss: the step fails loudly), never swept with stale data.
+// K1b, MVP's per-pair vectors and the bookkeeping read rows of present tiles
+// only.
+//
+// RCCL takes host-side sizes, so every (sender, receiver) pair has a tile
+// capacity, the same on all ranks: exact at bsa_sim_init (every rank holds the
+// whole initial state and plans for all ranks), grown when a step needs more
+// (Counters::halo_ovf aborts the step like a candidate overflow, the demands
+// are max-all-reduced on the host, every rank grows the same capacities and
+// the step re-runs).  A capacity's region is always sent whole: a count and
+// the tile ids, then the tiles' rows.
+//
+// The one-GPU probe of one rank's share (bsa_sim_detect_rows, mode 2) runs
+// steps 1, 3 and 5 with every tile's box already on the GPU.
+#include <algorithm>
+
+#include "bsa_box.h"
+#include "bsa_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace bsa {
+
+constexpr int kHaloMaxRanks = 16;
+constexpr int kHaloMaxF = 8;  // fp64 arrays per halo row
+
+struct HaloCaps {
+  int scap[kHaloMaxRanks], rcap[kHaloMaxRanks];  // this rank's send / receive capacities [tiles]
+  int hoff[kHaloMaxRanks];                       // flat halo list offset of each source
+  unsigned long long soff[kHaloMaxRanks], roff[kHaloMaxRanks];  // region offsets in h_send / h_recv [B]
+};
+
+struct HaloFields {
+  double *f[kHaloMaxF];  // lat lon trk gs alt vs gseast gsnorth (home order, full n)
+  int nf;                // 6: gseast / gsnorth derived from gs / trk by the receiver
+};
+
+static inline __host__ __device__ size_t hdr_bytes(int cap) { return ((size_t)4 * (cap + 1) + 15) / 16 * 16; }
+static inline __host__ __device__ size_t tile_bytes(int nf) { return (size_t)nf * kTile * 8; }
+static inline size_t region_bytes(int cap, int nf) { return cap ? hdr_bytes(cap) + (size_t)cap * tile_bytes(nf) : 0; }
+
+// requests: the tiles of this rank's resopairs' intruders outside its own tiles
+__global__ __launch_bounds__(256) void k_halo_req(int nrows, const unsigned *__restrict__ rptr,
+                                                  const unsigned *__restrict__ rcol, const unsigned *__restrict__ id2h,
+                                                  int a0, int a1, unsigned *__restrict__ req) {
+  const unsigned total = rptr[nrows];
+  for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
+    const unsigned j = rcol[k];
+    if (j == kDangling) continue;
+    const int t = (int)(id2h[j] / (unsigned)kTile);
+    if (t < a0 || t >= a1) atomicOr(&req[t >> 5], 1u << (t & 31));
+  }
+}
+
+struct PlanArgs {
+  int nct, tpr, R, me, a0, a1;
+  const TileBox *tbox;        // own tile boxes (probe: every tile's)
+  const unsigned char *gblk;  // gathered blocks [R][tpr boxes | request words], or NULL (probe)
+  size_t bb;                  // block bytes
+  TileBox *tbox_out;          // exchange: the gathered boxes of other ranks' tiles -> tbox_c
+  uint8_t *recv;              // [nct] tiles this rank needs (the present mask besides its own)
+  uint8_t *send;              // [R][tpr] own tiles each rank needs (exchange), else NULL
+};
+
+__device__ __forceinline__ const TileBox &plan_box(const PlanArgs &a, int t) {
+  if (!a.gblk) return a.tbox[t];
+  const int q = t / a.tpr;
+  return reinterpret_cast<const TileBox *>(a.gblk + (size_t)q * a.bb)[t - q * a.tpr];
+}
+__device__ __forceinline__ bool req_bit(const PlanArgs &a, int q, int t) {
+  const unsigned *w = reinterpret_cast<const unsigned *>(a.gblk + (size_t)q * a.bb + (size_t)a.tpr * sizeof(TileBox));
+  return (w[t >> 5] >> (t & 31)) & 1u;
+}
+
+// blockIdx.y < na: own tile a0 + y (as K0d's row tile) against every other
+// tile t; blockIdx.y == na (exchange): this rank's requests, and the copy of
+// the gathered boxes into tbox_c for K0d
+__global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.nct || (t >= a.a0 && t < a.a1)) return;
+  const int na = a.a1 - a.a0, y = blockIdx.y;
+  if (y < na) {
+    if (boxes_may_interact(a.tbox[a.a0 + y], plan_box(a, t))) {
+      a.recv[t] = 1;
+      if (a.send) a.send[(size_t)(t / a.tpr) * a.tpr + y] = 1;
+    }
+    return;
+  }
+  a.tbox_out[t] = plan_box(a, t);
+  if (req_bit(a, a.me, t)) a.recv[t] = 1;
+}
+
+// the other ranks' requests for own tiles: thread = (rank q, own tile i)
+__global__ __launch_bounds__(256) void k_halo_plan_req(PlanArgs a) {
+  const int na = a.a1 - a.a0;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= a.R * na) return;
+  const int q = x / na, i = x - q * na;
+  if (q != a.me && req_bit(a, q, a.a0 + i)) a.send[(size_t)q * a.tpr + i] = 1;
+}
+
+// ordered compaction of flag(0 .. m-1) by one 256-lane workgroup: f(index,
+// rank) for every set flag; returns the count (every lane)
+template <typename Flag, typename F>
+__device__ __forceinline__ int block_compact(int m, Flag flag, F f) {
+  __shared__ int wsum[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int base = 0;
+  for (int c0 = 0; c0 < m; c0 += 256) {
+    const int i = c0 + (int)threadIdx.x;
+    const bool on = i < m && flag(i);
+    const unsigned long long b = __ballot(on);
+    const int before = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(b);
+    __syncthreads();
+    int off = base;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    if (on) f(i, off + before);
+    base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  return base;
+}
+
+struct ListArgs {
+  int nct, tpr, R, me, a0, a1;
+  int probe;                     // one-GPU probe: source q's slots are [q tpr, (q + 1) tpr), no sends
+  const uint8_t *recv, *send;
+  int *hl;                       // flat halo list (this rank's receive slots)
+  unsigned char *sbuf;           // h_send (the region headers are written here)
+  unsigned *dem;                 // [R] send demand, [R] receive demand, [2R] tiles received
+  Counters *cnt;
+};
+
+// block q: the ordered list of own tiles rank q needs (into the header of the
+// send region for q) and of rank q's tiles this rank needs (into the flat list)
+__global__ __launch_bounds__(256) void k_halo_lists(ListArgs a, HaloCaps cp) {
+  const int q = blockIdx.x;
+  if (q == a.me) return;
+  const int na = a.a1 - a.a0;
+  bool ovf = false;
+  if (!a.probe) {
+    unsigned *hdr = reinterpret_cast<unsigned *>(a.sbuf + cp.soff[q]);
+    const int cap = cp.scap[q];
+    const int sc = block_compact(na, [&](int i) { return a.send[(size_t)q * a.tpr + i] != 0; },
+                                 [&](int i, int k) { if (k < cap) hdr[1 + k] = (unsigned)(a.a0 + i); });
+    if (threadIdx.x == 0) {
+      if (cap) hdr[0] = (unsigned)min(sc, cap);
+      a.dem[q] = (unsigned)sc;
+    }
+    ovf = sc > cap;
+  }
+  const int t0 = q * a.tpr, t1 = min(a.nct, t0 + a.tpr);
+  const int cap = a.probe ? a.tpr : cp.rcap[q];
+  int *hl = a.hl + (a.probe ? (size_t)q * a.tpr : (size_t)cp.hoff[q]);
+  const int rc = block_compact(max(t1 - t0, 0), [&](int i) { return a.recv[t0 + i] != 0; },
+                               [&](int i, int k) { if (k < cap) hl[k] = t0 + i; });
+  for (int k = rc + (int)threadIdx.x; k < cap; k += blockDim.x) hl[k] = -1;
+  if (threadIdx.x == 0) {
+    if (!a.probe) a.dem[a.R + q] = (unsigned)rc;
+    atomicAdd(&a.dem[2 * a.R], (unsigned)min(rc, cap));
+    if (ovf || rc > cap) a.cnt->halo_ovf = 1;
+  }
+}
+
+// rows of the listed own tiles into the send regions: block (slot k, rank q)
+__global__ __launch_bounds__(kTile) void k_halo_pack(int n, int me, HaloFields fl, unsigned char *sbuf, HaloCaps cp) {
+  const int k = blockIdx.x, q = blockIdx.y;
+  if (q == me || k >= cp.scap[q]) return;
+  const unsigned *hdr = reinterpret_cast<const unsigned *>(sbuf + cp.soff[q]);
+  if (k >= (int)hdr[0]) return;
+  const int row = (int)hdr[1 + k] * kTile + (int)threadIdx.x;
+  double *dst = reinterpret_cast<double *>(sbuf + cp.soff[q] + hdr_bytes(cp.scap[q]) + (size_t)k * tile_bytes(fl.nf));
+  for (int f = 0; f < fl.nf; ++f) dst[f * kTile + threadIdx.x] = row < n ? fl.f[f][row] : 0.0;
+}
+
+// received regions -> the home positions of the replicated arrays; every slot
+// is checked against this rank's own plan (a disagreement sets halo_miss)
+__global__ __launch_bounds__(kTile) void k_halo_unpack(int n, int me, HaloFields fl, const unsigned char *rbuf,
+                                                       const int *__restrict__ hlist, HaloCaps cp,
+                                                       Counters *__restrict__ cnt) {
+  const int k = blockIdx.x, q = blockIdx.y;
+  if (q == me || k >= cp.rcap[q]) return;
+  const unsigned *hdr = reinterpret_cast<const unsigned *>(rbuf + cp.roff[q]);
+  const int got = k < (int)hdr[0] ? (int)hdr[1 + k] : -1;
+  const int want = hlist[cp.hoff[q] + k];
+  if (got != want) {
+    if (threadIdx.x == 0) cnt->halo_miss = 1;
+    return;
+  }
+  if (got < 0) return;
+  const int row = got * kTile + (int)threadIdx.x;
+  if (row >= n) return;
+  const double *src =
+      reinterpret_cast<const double *>(rbuf + cp.roff[q] + hdr_bytes(cp.rcap[q]) + (size_t)k * tile_bytes(fl.nf));
+  for (int f = 0; f < fl.nf; ++f) fl.f[f][row] = src[f * kTile + threadIdx.x];
+  if (fl.nf == 6) {  // K4' without wind: gseast / gsnorth = gs sin / cos(trk), bitwise the sender's
+    const double gs = fl.f[3][row], trk = fl.f[2][row];
+    fl.f[7][row] = gs * cos(trk * kD2R);
+    fl.f[6][row] = gs * sin(trk * kD2R);
+  }
+}
+
+// ---------------------------------------------------------------- host side
+static int nct_of(const Ctx *c) { return (int)((c->n + kTile - 1) / kTile); }
+static int tpr_of(const Ctx *c) { return (int)(c->sim_rpr / kTile); }
+static int tiles_of(const Ctx *c, int q) {
+  const int tpr = tpr_of(c);
+  return std::max(0, std::min(nct_of(c), (q + 1) * tpr) - q * tpr);
+}
+static int64_t cap_at(const Ctx *c, int s, int d) { return c->halo_cap[(size_t)s * c->nranks + d]; }
+
+// region offsets in sender s's buffer (destinations in rank order) and its size
+static size_t send_offsets(const Ctx *c, int s, int nf, unsigned long long *off) {
+  size_t at = 0;
+  for (int d = 0; d < c->nranks; ++d) {
+    off[d] = at;
+    if (d != s) at += region_bytes((int)cap_at(c, s, d), nf);
+  }
+  return at;
+}
+
+const uint8_t *halo_present(const Ctx *c) { return (const uint8_t *)c->h_plan.p; }
+
+// the plan's buffers: recv [nct] + send [R][tpr] flags, demands
+static int plan_buffers(Ctx *c, int nct, int R, int tpr, int Rd) {
+  if (!ensure(c, c->h_plan, (size_t)nct + (size_t)R * tpr + 64, "halo plan") ||
+      !ensure(c, c->h_dem, (size_t)(2 * Rd + 1) * 4, "halo demands"))
+    return -1;
+  BSA_HIP(c, hipMemsetAsync(c->h_plan.p, 0, (size_t)nct + (size_t)R * tpr, c->stream));
+  BSA_HIP(c, hipMemsetAsync(c->h_dem.p, 0, (size_t)(2 * Rd + 1) * 4, c->stream));
+  return 0;
+}
+
+// one-GPU plan of the rank owning tiles [a0, a1) (probe and initial capacities):
+// every tile's box is in tbox_c; the present mask and the flat list (source
+// blocks of tpr tiles, full capacity each) come out
+static int plan_local(Ctx *c, int a0, int a1, int tpr) {
+  const int nct = nct_of(c), na = a1 - a0;
+  const int Rp = (nct + tpr - 1) / tpr;
+  if (!ensure(c, c->counters, sizeof(Counters), "counters")) return -1;
+  if (plan_buffers(c, nct, 1, tpr, Rp)) return -1;
+  if (!ensure(c, c->h_hl, (size_t)Rp * tpr * 4, "halo list")) return -1;
+  c->halo_hl = (int64_t)Rp * tpr;
+  c->halo_tot_word = 2 * Rp;
+  uint8_t *recv = (uint8_t *)c->h_plan.p;
+  if (na > 0) {
+    PlanArgs pa{nct, tpr, 1, -1, a0, a1, (const TileBox *)c->tbox_c.p, nullptr, 0, nullptr, recv, nullptr};
+    hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((nct + 255) / 256), (unsigned)na), dim3(256), 0, c->stream, pa);
+    BSA_HIP(c, hipGetLastError());
+  }
+  ListArgs la{nct, tpr, Rp, -1, a0, a1, 1, recv, nullptr, (int *)c->h_hl.p, nullptr, (unsigned *)c->h_dem.p,
+              (Counters *)c->counters.p};
+  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)Rp), dim3(256), 0, c->stream, la, HaloCaps{});
+  BSA_HIP(c, hipGetLastError());
+  return 0;
+}
+
+int halo_mid(Ctx *c, int64_t rb, int64_t re) {
+  const int nct = nct_of(c);
+  const int a0 = (int)(rb / kTile), a1 = std::max(a0, (int)((re + kTile - 1) / kTile)), na = a1 - a0;
+  if (c->halo_mode == 2) {
+    c->halo_fields = 0;
+    return plan_local(c, a0, a1, std::max(na, 1));
+  }
+  // ---- exchange mode (several ranks)
+  const int R = c->nranks, me = c->rank, tpr = tpr_of(c);
+  if (R > kHaloMaxRanks) return fail(c, "halo exchange: at most %d ranks", kHaloMaxRanks);
+  if ((int64_t)c->halo_cap.size() != (int64_t)R * R) return fail(c, "halo exchange: capacities not set");
+  hipStream_t s = c->stream;
+  const int W = (nct + 31) / 32;
+  const size_t bb = ((size_t)tpr * sizeof(TileBox) + (size_t)W * 4 + 15) / 16 * 16;
+  if (!ensure(c, c->h_blk, bb, "halo box block") || !ensure(c, c->h_gblk, bb * R, "halo box blocks")) return -1;
+  if (plan_buffers(c, nct, R, tpr, R)) return -1;
+  // 2. own tile boxes + request bits -> every rank
+  unsigned *req = (unsigned *)((char *)c->h_blk.p + (size_t)tpr * sizeof(TileBox));
+  BSA_HIP(c, hipMemsetAsync(req, 0, (size_t)W * 4, s));
+  if (na > 0)
+    BSA_HIP(c, hipMemcpyAsync(c->h_blk.p, (const TileBox *)c->tbox_c.p + a0, (size_t)na * sizeof(TileBox),
+                              hipMemcpyDeviceToDevice, s));
+  if (c->simp.resume_nav && c->bk_ready && na > 0) {
+    hipLaunchKernelGGL(k_halo_req, dim3(64), dim3(256), 0, s, (int)(c->sim_re - c->sim_rb),
+                       (const unsigned *)c->bk_rptr.p, (const unsigned *)c->bk_rcol.p, (const unsigned *)c->id2h.p,
+                       a0, a1, req);
+    BSA_HIP(c, hipGetLastError());
+  }
+  if (comm_allgather(c, c->h_blk.p, c->h_gblk.p, bb)) return -1;
+  // 3. plan
+  uint8_t *recv = (uint8_t *)c->h_plan.p, *sendf = recv + nct;
+  PlanArgs pa{nct, tpr, R, me, a0, a1, (const TileBox *)c->tbox_c.p, (const unsigned char *)c->h_gblk.p, bb,
+              (TileBox *)c->tbox_c.p, recv, sendf};
+  hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((nct + 255) / 256), (unsigned)(na + 1)), dim3(256), 0, s, pa);
+  BSA_HIP(c, hipGetLastError());
+  if (na > 0) {
+    hipLaunchKernelGGL(k_halo_plan_req, dim3((unsigned)((R * na + 255) / 256)), dim3(256), 0, s, pa);
+    BSA_HIP(c, hipGetLastError());
+  }
+  // capacities and offsets of this rank's regions
+  const int nf = (c->simp.winddim == 0 && c->sim_gs_derivable) ? 6 : 8;
+  HaloCaps cp{};
+  size_t roff = 0;
+  int hoff = 0, smax = 0, rmax = 0;
+  const size_t stot = send_offsets(c, me, nf, cp.soff);
+  for (int q = 0; q < R; ++q) {
+    cp.scap[q] = q == me ? 0 : (int)cap_at(c, me, q);
+    cp.rcap[q] = q == me ? 0 : (int)cap_at(c, q, me);
+    cp.hoff[q] = hoff;
+    cp.roff[q] = roff;
+    hoff += cp.rcap[q];
+    roff += region_bytes(cp.rcap[q], nf);
+    smax = std::max(smax, cp.scap[q]);
+    rmax = std::max(rmax, cp.rcap[q]);
+  }
+  c->halo_hl = hoff;
+  c->halo_tot_word = 2 * R;
+  c->halo_fields = nf;
+  c->halo_tx = (int64_t)stot;
+  c->halo_rx = (int64_t)roff;
+  if (!ensure(c, c->h_send, std::max<size_t>(stot, 16), "halo send") ||
+      !ensure(c, c->h_recv, std::max<size_t>(roff, 16), "halo recv") ||
+      !ensure(c, c->h_hl, (size_t)std::max(hoff, 1) * 4, "halo list"))
+    return -1;
+  ListArgs la{nct, tpr, R, me, a0, a1, 0, recv, sendf, (int *)c->h_hl.p, (unsigned char *)c->h_send.p,
+              (unsigned *)c->h_dem.p, (Counters *)c->counters.p};
+  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)R), dim3(256), 0, s, la, cp);
+  BSA_HIP(c, hipGetLastError());
+  HaloFields fl{};
+  DevBuf *src[8] = {&c->own[0], &c->own[1], &c->own[2], &c->own[3], &c->own[4], &c->own[5], &c->s_gse, &c->s_gsn};
+  for (int f = 0; f < 8; ++f) fl.f[f] = (double *)src[f]->p;
+  fl.nf = nf;
+  // 4. pack, exchange, unpack
+  if (smax > 0) {
+    hipLaunchKernelGGL(k_halo_pack, dim3((unsigned)smax, (unsigned)R), dim3(kTile), 0, s, (int)c->n, me, fl,
+                       (unsigned char *)c->h_send.p, cp);
+    BSA_HIP(c, hipGetLastError());
+  }
+  std::vector<size_t> slen(R), rlen(R), rof(R), peer(R);
+  for (int q = 0; q < R; ++q) {
+    slen[q] = q == me ? 0 : region_bytes(cp.scap[q], nf);
+    rlen[q] = q == me ? 0 : region_bytes(cp.rcap[q], nf);
+    rof[q] = cp.roff[q];
+    unsigned long long po[kHaloMaxRanks];
+    send_offsets(c, q, nf, po);  // where rank q's region for this rank starts in q's buffer
+    peer[q] = po[me];
+  }
+  std::vector<size_t> sof(R);
+  for (int q = 0; q < R; ++q) sof[q] = cp.soff[q];
+  if (comm_halo(c, c->h_send.p, sof.data(), slen.data(), stot, c->h_recv.p, rof.data(), rlen.data(), peer.data()))
+    return -1;
+  if (rmax > 0) {
+    hipLaunchKernelGGL(k_halo_unpack, dim3((unsigned)rmax, (unsigned)R), dim3(kTile), 0, s, (int)c->n, me, fl,
+                       (const unsigned char *)c->h_recv.p, (const int *)c->h_hl.p, cp, (Counters *)c->counters.p);
+    BSA_HIP(c, hipGetLastError());
+  }
+  return 0;
+}
+
+// Exact initial capacities: at bsa_sim_init every rank holds the whole state,
+// so each computes every rank's plan itself (the same numbers on all ranks).
+int halo_init_caps(Ctx *c) {
+  const int R = c->nranks, tpr = tpr_of(c), nct = nct_of(c);
+  c->halo_cap.assign((size_t)R * R, 0);
+  c->halo_grows = 0;
+  if (R <= 1) return 0;
+  if (prep_all_tiles(c, c->simp.rpz, c->simp.hpz, c->simp.tla)) return -1;
+  std::vector<uint8_t> recv((size_t)nct);
+  for (int q = 0; q < R; ++q) {
+    const int a0 = q * tpr, a1 = a0 + tiles_of(c, q);
+    if (plan_local(c, a0, a1, tpr)) return -1;
+    BSA_HIP(c, hipMemcpyAsync(recv.data(), c->h_plan.p, (size_t)nct, hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    for (int t = 0; t < nct; ++t)
+      if (recv[(size_t)t]) c->halo_cap[(size_t)(t / tpr) * R + q]++;
+  }
+  for (int sd = 0; sd < R; ++sd)
+    for (int q = 0; q < R; ++q) {
+      int64_t &m = c->halo_cap[(size_t)sd * R + q];
+      if (m) m = std::min<int64_t>(m + m / 4 + 2, tiles_of(c, sd));
+    }
+  return 0;
+}
+
+// After an aborted step (every rank, collective): the demands of this rank's
+// plan are max-all-reduced into an R x R matrix; capacities below it grow.
+int halo_grow(Ctx *c) {
+  const int R = c->nranks, me = c->rank;
+  if (R <= 1 || (int64_t)c->halo_cap.size() != (int64_t)R * R) return 0;
+  std::vector<unsigned> dem((size_t)2 * R + 1, 0u);
+  if (c->h_dem.p) {
+    BSA_HIP(c, hipMemcpyAsync(dem.data(), c->h_dem.p, dem.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  std::vector<double> m((size_t)R * R, 0.0);
+  for (int q = 0; q < R; ++q) {
+    if (q == me) continue;
+    m[(size_t)me * R + q] = dem[(size_t)q];      // what this rank must send to q
+    m[(size_t)q * R + me] = dem[(size_t)R + q];  // what it must receive from q
+  }
+  if (comm_allreduce_host(c, m.data(), R * R, true)) return -1;
+  bool grew = false;
+  for (int sd = 0; sd < R; ++sd)
+    for (int q = 0; q < R; ++q) {
+      int64_t &cap = c->halo_cap[(size_t)sd * R + q];
+      const int64_t need = (int64_t)m[(size_t)sd * R + q];
+      if (need > cap) {
+        cap = std::min<int64_t>(std::max(2 * cap, need + need / 4 + 2), tiles_of(c, sd));
+        grew = true;
+      }
+    }
+  if (grew) c->halo_grows++;
+  return 0;
+}
+
+void halo_release(Ctx *c) {
+  DevBuf *all[] = {&c->h_blk, &c->h_gblk, &c->h_plan, &c->h_lists, &c->h_send, &c->h_recv, &c->h_hl, &c->h_dem};
+  for (auto *b : all) release(*b);
+  c->halo_cap.clear();
+  c->halo_hl = 0;
+}
+
+}  // namespace bsa

@@ -122,6 +122,8 @@ struct Counters {
   unsigned long long tiles_near;  // of `tiles`: pairs whose boxes overlap (listed first, swept first)
   unsigned long long pad[1];      // (far tile pairs, counted from the list's end)
   unsigned long long k2_demand;   // K2 row buckets: the largest row count beyond Ctx::k2_bucket (0: fit)
+  unsigned long long halo_ovf;    // halo exchange: more tiles to send / receive than the capacities
+  unsigned long long halo_miss;   // halo exchange inconsistent (a kept tile pair without its data): bug
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];
   unsigned long long cshard[kCandShards][16];  // candidates per shard (word 0 of each line)
@@ -257,6 +259,19 @@ struct Ctx {
   unsigned long long bk_kw = 0, bk_kw_alloc = 0;
   bool bk_ready = false;
 
+  // halo exchange of the row-sharded resident step (bsa_halo.hip): each rank
+  // receives only the column tiles its rows' boxes can reach (plus the tiles
+  // of its resopairs' intruders) and prepares only those and its own tiles
+  int halo_mode = 0;               // detect_enqueue (home mode): 0 off, 1 exchange (several ranks),
+                                   // 2 one-GPU probe of one rank's share (bsa_sim_detect_rows)
+  std::vector<int64_t> halo_cap;   // R x R tile capacities [sender * R + receiver], equal on all ranks
+  DevBuf h_blk, h_gblk, h_plan, h_lists, h_send, h_recv, h_hl, h_dem;
+  int64_t halo_hl = 0;             // slots of the flat halo tile list (this rank's receive capacities)
+  int64_t halo_grows = 0;          // capacity regrowths (aborted steps)
+  int64_t halo_rx = 0, halo_tx = 0;  // bytes received / sent per CD step (the capacities' transfers)
+  int halo_fields = 8;             // fp64 arrays per halo row of the last exchange (6 when derivable)
+  int halo_tot_word = 0;           // h_dem word holding the last plan's received-tile total
+
   // 2-D wind field (bsa_set_windfield): lat lon vnorth veast of wf_nvec points
   DevBuf wfield;
   int64_t wf_nvec = 0;
@@ -282,6 +297,11 @@ struct Ctx {
   // type index (int32) and the phase of the last step (u8)
   DevBuf s_ptab, s_ptype, s_phase;
   bool sim_perf = false;
+  // NORESO / RESOOFF membership (bsa_sim_set_reso_lists, u8 in home order) and
+  // the rows whose ResumeNav dropped a pair in the last CD call (u8, home order)
+  DevBuf s_noreso, s_resooff, s_dropped;
+  bool sim_noreso = false, sim_resooff = false;
+  const uint8_t *fuse_noreso = nullptr;  // NORESO list for K2's fused MVP per-pair vectors
   int64_t sim_ntypes = 0;
   void *feed_host = nullptr;
   size_t feed_host_bytes = 0;
@@ -324,6 +344,7 @@ struct BkDev {
   const double *lat, *lon, *gse, *gsn, *trk;  // home order
   const unsigned *h2id, *id2h;                // home <-> aircraft index
   uint8_t *active;
+  uint8_t *dropped;             // per row: ResumeNav dropped one of its pairs (waypoint recovery)
   unsigned long long *gate;
   unsigned *sticky;
   unsigned long long *demand;   // resopairs overflow: pairs needed
@@ -332,6 +353,19 @@ struct BkDev {
 int bk_count(Ctx *c, const BkDev &d);
 int bk_apply(Ctx *c, const BkDev &d);
 void bk_release(Ctx *c);
+
+// halo exchange (bsa_halo.hip).  halo_mid: after K0 prepared the rank's own
+// column tiles (and their boxes), plan which tiles every rank needs, exchange
+// them (mode 1) and leave the flat list of this rank's halo tiles in h_hl
+// (halo_hl slots, -1 = unused) and its present mask in h_plan
+int halo_mid(Ctx *c, int64_t rb, int64_t re);
+int halo_init_caps(Ctx *c);      // bsa_sim_init, several ranks: exact initial capacities (no exchange)
+int halo_grow(Ctx *c);           // after an aborted step, several ranks (collective)
+void halo_release(Ctx *c);
+const uint8_t *halo_present(const Ctx *c);  // the received-tile mask of the last halo_mid
+// K0b over every column tile (fused boxes, no per-detect zeroing): the halo
+// plan's view of all tile boxes when every rank's state is on this GPU (bsa_cd.hip)
+int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla);
 
 // exclusive prefix sum of n words, one launch (bsa_cd.hip)
 int scan_excl(Ctx *c, const unsigned *in, unsigned *out, int n);
@@ -369,6 +403,8 @@ int comm_allgather_inplace(Ctx *c, double *const *f, int nf, size_t rpr); // ran
 int comm_allreduce_host(Ctx *c, double *v, int count, bool max);         // host values (synchronises)
 int comm_gatherv(Ctx *c, int root, const void *send, size_t bytes, void *recv, const size_t *off,
                  const size_t *len);                                     // rank-order blocks to root
+int comm_halo(Ctx *c, const void *send, const size_t *soff, const size_t *slen, size_t stot, void *recv,
+              const size_t *roff, const size_t *rlen, const size_t *peer);  // halo regions (bsa_halo.hip)
 void comm_release(Ctx *c);
 
 // sim / comm teardown (bsa_sim.hip); ACDATA feed teardown (bsa_feed.hip)

@@ -274,9 +274,10 @@ void sim_release(Ctx *c) {
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
                    &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env,
-                   &c->s_ptab, &c->s_ptype, &c->s_phase};
+                   &c->s_ptab, &c->s_ptype, &c->s_phase, &c->s_noreso, &c->s_resooff, &c->s_dropped};
   for (auto *b : all) release(*b);
   bk_release(c);
+  halo_release(c);
   comm_release(c);
 }
 
@@ -351,24 +352,32 @@ void set_rank_rows(Ctx *c) {
   c->sim_re = std::min<int64_t>(n, c->sim_rb + c->sim_rpr);
 }
 
-// one CD step of the batch (enqueue only)
-static int sim_cd(Ctx *c) {
+// one CD step of the batch (enqueue only).  allow_defer: K3's per-row part may
+// run inside the step's K4' (k_sim_pilot_kin<true>); a CD call without
+// kinematics (bsa_sim_cd) launches it itself.
+static int sim_cd(Ctx *c, bool allow_defer) {
   const bsa_sim_params &p = c->simp;
-  if (sim_gather(c)) return -1;
+  // several ranks: the detect's halo exchange (bsa_halo.hip) refreshes the
+  // other ranks' rows this rank reads; one rank holds everything
+  if (c->halo_mode != 1 && sim_gather(c)) return -1;
   unsigned long long *gate = (unsigned long long *)c->sim_ctl.p;
-  // MVP's per-pair vectors are evaluated by K2 as it places each pair (no
-  // NORESO list in the resident step); k_mvp_row folds them after the gate
+  const uint8_t *noreso = c->sim_noreso ? (const uint8_t *)c->s_noreso.p : nullptr;
+  const uint8_t *resooff = c->sim_resooff ? (const uint8_t *)c->s_resooff.p : nullptr;
+  // MVP's per-pair vectors are evaluated by K2 as it places each pair;
+  // k_mvp_row folds them after the gate
   if (p.reso) {
     c->fuse_mvp = &p.mvp;
     c->fuse_gse = (const double *)c->s_gse.p;
     c->fuse_gsn = (const double *)c->s_gsn.p;
     c->fuse_vs = (const double *)c->own[5].p;
     c->fuse_alt = (const double *)c->own[4].p;
+    c->fuse_noreso = noreso;
   }
   c->det_home = true;
   const int de = detect_enqueue(c, p.rpz, p.hpz, p.tla, 0, c->sim_rb, c->sim_re, gate);
   c->det_home = false;
   c->fuse_mvp = nullptr;
+  c->fuse_noreso = nullptr;
   if (de) return -1;
   c->sim_cd_calls++;
   unsigned *sticky = (unsigned *)((char *)c->sim_ctl.p + 16);
@@ -381,6 +390,7 @@ static int sim_cd(Ctx *c) {
   bk.h2id = (const unsigned *)c->h2id.p;
   bk.id2h = (const unsigned *)c->id2h.p;
   bk.active = (uint8_t *)c->s_active.p;
+  bk.dropped = (uint8_t *)c->s_dropped.p;
   bk.gate = gate;
   bk.sticky = sticky;
   bk.demand = (unsigned long long *)((char *)c->sim_ctl.p + 32);
@@ -401,8 +411,8 @@ static int sim_cd(Ctx *c) {
   d.aptrk = (const double *)c->s_aptrk.p;
   d.aptas = (const double *)c->s_aptas.p;
   d.apalt = (const double *)c->s_apalt.p;
-  d.noreso = nullptr;
-  d.resooff = nullptr;
+  d.noreso = noreso;
+  d.resooff = resooff;
   d.asas_alt = (double *)c->s_aalt.p + rb;
   d.o_trk = (double *)c->s_atrk.p + rb;
   d.o_tas = (double *)c->s_atas.p + rb;
@@ -413,7 +423,7 @@ static int sim_cd(Ctx *c) {
   // K3 (+ gate, + asas.active = inconf unless ResumeNav runs) on the detect's own row offsets
   // without the bookkeeping (which runs between K3 and K4') K3's rows are
   // deferred into K4' of this step (k_sim_pilot_kin<true>)
-  const bool defer = !p.resume_nav && c->sim_re > c->sim_rb;
+  const bool defer = allow_defer && !p.resume_nav && c->sim_re > c->sim_rb;
   MvpIn din{};
   if (mvp_device(c, p.mvp, d, (const unsigned *)c->rowoff.p, gate, sticky,
                  p.resume_nav ? nullptr : (const uint8_t *)c->inconf.p, (uint8_t *)c->s_active.p, p.reso != 0,
@@ -426,6 +436,45 @@ static int sim_cd(Ctx *c) {
   }
   // second half: resopairs rewrite, ResumeNav's asas.active, unique / cumulative counts
   return p.resume_nav ? bk_apply(c, bk) : 0;
+}
+
+// An aborted CD call (ctl = sim_ctl words [16, 48): sticky, steps done,
+// resopairs demand, key-block demand): grow what overflowed on THIS rank (the
+// gate is all-reduced, so every rank aborted at the same step; another rank's
+// overflow re-runs the step here with unchanged buffers)
+static int grow_after_abort(Ctx *c, const unsigned long long *ctl) {
+  c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
+  {
+    Counters h;
+    BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
+    if (h.halo_miss)
+      return fail(c, "internal error: the halo exchange and the tile-pair cull disagree (rank %d)", c->rank);
+  }
+  // several ranks: every rank takes part in the capacity agreement (collective)
+  if (c->halo_mode == 1 && halo_grow(c)) return -1;
+  if (ctl[2] > 0)  // this rank's resopairs outgrew their buffer
+    c->bk_cap = std::max(2 * c->bk_cap, ctl[2] + ctl[2] / 4 + 1024);
+  if (ctl[3] > 0)  // this rank's pair keys outgrew their all-gather block
+    c->bk_kw = std::max(2 * c->bk_kw, ctl[3] + ctl[3] / 4 + 1024);
+  // candidate overflow on this rank: enough for the last detect's demand (its
+  // shard counters keep counting past the capacity; every detect after the
+  // abort ran on the same, unchanged state)
+  Counters h;
+  BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
+  if (h.k2_demand) grow_k2_bucket(c, h.k2_demand);  // a K2 row bucket was full on this rank
+  unsigned long long worst = 0;
+  for (int q = 0; q < kCandShards; ++q) worst = std::max(worst, h.cshard[q][0]);
+  if (worst > c->cand_cap / kCandShards)
+    c->cand_cap = std::max(2 * c->cand_cap, (unsigned long long)kCandShards * (worst + worst / 4 + 1024));
+  return 0;
+}
+
+static int check_params(Ctx *c, const bsa_sim_params *p) {
+  if (p->cd_every < 1) return fail(c, "cd_every must be >= 1");
+  if (p->resume_nav != 0 && p->resume_nav != 1) return fail(c, "resume_nav must be 0 or 1");
+  if (p->winddim < 0 || p->winddim > 2) return fail(c, "winddim must be 0, 1 or 2");
+  if (p->reso != 0 && p->reso != 1) return fail(c, "reso must be 0 or 1");
+  return 0;
 }
 
 }  // namespace bsa
@@ -442,9 +491,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   // leaves no half-initialised sim behind (sim_ready stays false)
   c->sim_ready = false;
   if (n <= 0 || n > 0x7fffffff) return bsa::fail(c, "bad n");
-  if (p->cd_every < 1) return bsa::fail(c, "cd_every must be >= 1");
-  if (p->resume_nav != 0 && p->resume_nav != 1) return bsa::fail(c, "resume_nav must be 0 or 1");
-  if (p->winddim < 0 || p->winddim > 2) return bsa::fail(c, "winddim must be 0, 1 or 2");
+  if (bsa::check_params(c, p)) return -1;
   BSA_HIP(c, hipSetDevice(c->device));
   const double *src[] = {s->lat, s->lon, s->alt, s->tas, s->hdg, s->vs, s->gs, s->trk, s->gseast,
                          s->gsnorth, s->ap_trk, s->ap_tas, s->ap_alt, s->ap_vs, s->selalt, s->bank,
@@ -478,8 +525,11 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   if (!bsa::ensure(c, c->s_atrk, N8, "asas trk") || !bsa::ensure(c, c->s_atas, N8, "asas tas") ||
       !bsa::ensure(c, c->s_avs, N8, "asas vs") || !bsa::ensure(c, c->s_ase, (size_t)n * 4, "asase") ||
       !bsa::ensure(c, c->s_asn, (size_t)n * 4, "asasn") || !bsa::ensure(c, c->s_active, n, "active") ||
-      !bsa::ensure(c, c->s_altprev, N8, "pre-step altitude") || !bsa::ensure(c, c->s_ax, N8, "ax"))
+      !bsa::ensure(c, c->s_altprev, N8, "pre-step altitude") || !bsa::ensure(c, c->s_ax, N8, "ax") ||
+      !bsa::ensure(c, c->s_dropped, n, "ResumeNav drops"))
     return -1;
+  BSA_HIP(c, hipMemsetAsync(c->s_dropped.p, 0, n, c->stream));
+  c->sim_noreso = c->sim_resooff = false;  // empty NORESO / RESOOFF lists
   BSA_HIP(c, hipMemsetAsync(c->s_ax.p, 0, N8, c->stream));   // traf.ax: 0 at create
   c->sim_limits = false;
   c->sim_perf = false;
@@ -494,6 +544,10 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   c->simp = *p;
   c->bk_ready = false;  // empty resopairs / previous pair sets
+  // several ranks: halo exchange instead of the full all-gather, with exact
+  // initial capacities (every rank holds the whole state now)
+  c->halo_mode = c->nranks > 1 ? 1 : 0;
+  if (bsa::halo_init_caps(c)) return -1;
   c->sim_steps = c->sim_cd_calls = c->sim_last_conf = c->sim_last_los = 0;
   c->sim_gathered = true;
   c->sim_gs_derivable = false;  // gseast / gsnorth are the host's until K4' runs
@@ -523,7 +577,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 32, c->stream));  // sticky, steps_done, demands
     while (c->sim_steps < target) {
       if (c->sim_steps % c->simp.cd_every == 0)
-        if (bsa::sim_cd(c)) return -1;
+        if (bsa::sim_cd(c, true)) return -1;
       const int64_t nb = std::max<int64_t>(1, (re - rb + 255) / 256);
       bsa::MvpIn mv{};
       if (c->mvp_deferred) memcpy(&mv, c->mvp_defer.data(), sizeof(mv));
@@ -558,20 +612,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     for (int64_t k = base; k < base + done; ++k) cds += (k % c->simp.cd_every == 0) ? 1 : 0;
     c->sim_cd_calls = base_cd + cds;
     c->sim_gathered = c->nranks == 1;
-    if (ctl[2] > 0)  // this rank's resopairs outgrew their buffer
-      c->bk_cap = std::max(2 * c->bk_cap, ctl[2] + ctl[2] / 4 + 1024);
-    if (ctl[3] > 0)  // this rank's pair keys outgrew their all-gather block
-      c->bk_kw = std::max(2 * c->bk_kw, ctl[3] + ctl[3] / 4 + 1024);
-    // candidate overflow on this rank: enough for the last detect's demand (its
-    // shard counters keep counting past the capacity; every detect after the
-    // abort ran on the same, unchanged state)
-    bsa::Counters h;
-    BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
-    if (h.k2_demand) bsa::grow_k2_bucket(c, h.k2_demand);  // a K2 row bucket was full on this rank
-    unsigned long long worst = 0;
-    for (int q = 0; q < bsa::kCandShards; ++q) worst = std::max(worst, h.cshard[q][0]);
-    if (worst > c->cand_cap / bsa::kCandShards)
-      c->cand_cap = std::max(2 * c->cand_cap, (unsigned long long)bsa::kCandShards * (worst + worst / 4 + 1024));
+    if (bsa::grow_after_abort(c, ctl)) return -1;
   }
   return 0;
 }
@@ -662,17 +703,25 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
             {s->bank, c->s_bank.p},    {s->eps, c->s_eps.p},      {s->accel, c->s_accel.p},
             {s->asas_alt, c->s_aalt.p}};
   // the replicated CD inputs are rewritten on every rank (in the sim's home order)
-  bool any_cd = false;
+  bool any_cd = false, all_rep = true;
   std::vector<char> tmp;
   for (int k = 0; k < 19; ++k) {
-    if (!cp[k].src) continue;
+    const bool rep = k < 6 || k == 8 || k == 9;  // the arrays the all-gather replicates
+    if (!cp[k].src) {
+      all_rep = all_rep && !rep;
+      continue;
+    }
     if (k < 10) any_cd = true;
     if (bsa::put_home(c, cp[k].dst, cp[k].src, 8, tmp)) return -1;
   }
   if (any_cd) {
-    c->sim_gathered = true;     // every rank passed the same full arrays
+    // every rank passed the same full arrays: the replicas are consistent only
+    // if ALL replicated arrays were passed; otherwise the next all-gather
+    // repairs the other ranks' rows of the arrays not passed (each rank's
+    // own rows are right either way)
+    if (all_rep) c->sim_gathered = true;
     c->sim_gs_derivable = false;  // (gseast / gsnorth may be the host's)
-    c->reuse_valid = false;     // a state jump rebuilds any reused candidate list
+    c->reuse_valid = false;       // a state jump rebuilds any reused candidate list
   }
   return 0;
 }
@@ -726,10 +775,34 @@ int bsa_sim_detect_rows(bsa_ctx *cc, int64_t row_begin, int64_t row_end, int64_t
   if (row_begin % bsa::kTile != 0) return bsa::fail(c, "row_begin must be a multiple of %d", bsa::kTile);
   BSA_HIP(c, hipSetDevice(c->device));
   if (bsa::sim_gather(c)) return -1;
+  // as one rank of a sharded step: own tiles, halo plan, halo tiles (the
+  // boxes of every tile, which the other ranks would send, are prepared
+  // first, outside the detect's timed stages)
+  if (bsa::prep_all_tiles(c, c->simp.rpz, c->simp.hpz, c->simp.tla)) return -1;
+  const int hm = c->halo_mode;
+  c->halo_mode = 2;
   c->det_home = true;
   const int r = bsa::detect(c, c->simp.rpz, c->simp.hpz, c->simp.tla, 0, row_begin, row_end, n_conf, n_los);
   c->det_home = false;
+  c->halo_mode = hm;
   return r;
+}
+
+int bsa_sim_halo_stats(bsa_ctx *cc, int64_t *out4) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !out4) return -1;
+  BSA_HIP(c, hipSetDevice(c->device));
+  unsigned tiles = 0;
+  if (c->h_dem.p) {  // the received-tile total of the last plan (after its demand words)
+    BSA_HIP(c, hipMemcpyAsync(&tiles, (const unsigned *)c->h_dem.p + c->halo_tot_word, 4, hipMemcpyDeviceToHost,
+                              c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  out4[0] = c->halo_rx;
+  out4[1] = c->halo_tx;
+  out4[2] = tiles;
+  out4[3] = c->halo_grows;
+  return 0;
 }
 
 int bsa_sim_row_ids(bsa_ctx *cc, int32_t *ids) {
@@ -792,6 +865,80 @@ int bsa_sim_resopairs(bsa_ctx *cc, int32_t *idx1, int32_t *idx2, int64_t cap, in
       idx1[at] = (int32_t)H[r];
       idx2[at] = (int32_t)col[k];
     }
+  return 0;
+}
+
+int bsa_sim_cd(bsa_ctx *cc) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_cd before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  for (int attempt = 0;; ++attempt) {
+    if (attempt > 6) return bsa::fail(c, "candidate buffer overflow in the CD call (retries exhausted)");
+    const int64_t base_cd = c->sim_cd_calls;
+    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 32, c->stream));  // sticky, steps_done, demands
+    if (bsa::sim_cd(c, false)) return -1;
+    unsigned long long ctl[4] = {0, 0, 0, 0};
+    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 32, hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    if ((unsigned)ctl[0] == 0) break;
+    // aborted: nothing persistent was written (the state did not move, so
+    // the replicas stay consistent); grow and re-run
+    c->sim_cd_calls = base_cd;
+    if (bsa::grow_after_abort(c, ctl)) return -1;
+  }
+  return 0;
+}
+
+int bsa_sim_set_params(bsa_ctx *cc, const bsa_sim_params *p) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!p) return bsa::fail(c, "NULL sim params");
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_set_params before bsa_sim_init");
+  if (bsa::check_params(c, p)) return -1;
+  if (p->resume_nav && !c->simp.resume_nav) c->bk_ready = false;  // the bookkeeping starts empty
+  c->simp = *p;
+  return 0;
+}
+
+int bsa_sim_set_reso_lists(bsa_ctx *cc, const uint8_t *noreso, const uint8_t *resooff) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_set_reso_lists before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  std::vector<char> tmp;
+  struct {
+    const uint8_t *h;
+    bsa::DevBuf *b;
+    bool *on;
+  } ls[2] = {{noreso, &c->s_noreso, &c->sim_noreso}, {resooff, &c->s_resooff, &c->sim_resooff}};
+  for (auto &l : ls) {
+    *l.on = false;
+    if (!l.h) continue;
+    std::vector<uint8_t> v(l.h, l.h + c->n);
+    for (auto &x : v) x = x ? 1 : 0;
+    if (!bsa::ensure(c, *l.b, (size_t)c->n, "NORESO / RESOOFF list") || bsa::put_home(c, l.b->p, v.data(), 1, tmp))
+      return -1;
+    *l.on = true;
+  }
+  return 0;
+}
+
+int bsa_sim_read_asas(bsa_ctx *cc, bsa_asas_out *o) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !o) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_read_asas before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  struct {
+    void *dst;
+    const void *src;
+    size_t esz;
+  } cp[] = {{o->trk, c->s_atrk.p, 8},   {o->tas, c->s_atas.p, 8},     {o->vs, c->s_avs.p, 8},
+            {o->alt, c->s_aalt.p, 8},   {o->asase, c->s_ase.p, 4},    {o->asasn, c->s_asn.p, 4},
+            {o->active, c->s_active.p, 1}, {o->dropped, c->s_dropped.p, 1}};
+  std::vector<char> tmp;
+  for (auto &e : cp)
+    if (e.dst && bsa::get_home(c, e.dst, e.src, e.esz, c->sim_rb, c->sim_re, tmp)) return -1;
   return 0;
 }
 

@@ -73,6 +73,9 @@ static std::vector<PerAc> per_aircraft(Ctx *c) {
   v.push_back({&c->s_asn, 4, 1});
   v.push_back({&c->s_active, 1, 1});
   v.push_back({&c->inconf, 1, 1});
+  // NORESO / RESOOFF membership and the last ResumeNav's drops (allocated on use)
+  for (auto *b : {&c->s_noreso, &c->s_resooff, &c->s_dropped})
+    if (b->p) v.push_back({b, 1, 1});
   if (c->sim_limits) v.push_back({&c->s_env, 8, 6});
   if (c->sim_perf) {
     v.push_back({&c->s_ptype, 4, 1});
@@ -88,8 +91,6 @@ static int check_sim(Ctx *c, const char *what) {
     c->feed_pending = false;
   }
   if (c->nranks > 1) return fail(c, "%s with several ranks: re-init the sim (rows would move between GPUs)", what);
-  if (c->bk_ready && (c->last_rb != 0 || c->last_re != c->n))
-    return fail(c, "%s: the last detect on this context did not cover the sim's rows", what);
   return 0;
 }
 
@@ -297,6 +298,8 @@ int bsa_sim_create(bsa_ctx *cc, int64_t m, const bsa_sim_state *s) {
               {&c->s_active, 1}, {&c->inconf, 1}};
   for (auto &z : zero)
     BSA_HIP(c, hipMemsetAsync((char *)z.b->p + (size_t)n * z.esz, 0, (size_t)m * z.esz, c->stream));
+  for (auto *b : {&c->s_noreso, &c->s_resooff, &c->s_dropped})  // not in the lists, nothing dropped
+    if (b->p) BSA_HIP(c, hipMemsetAsync((char *)b->p + n, 0, (size_t)m, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
   // new aircraft have no resopairs and were in no previous pair set: empty CSR rows
   if (c->bk_ready) {

@@ -91,6 +91,16 @@ class ResidentSim:
     def step(self, nsteps=1):
         self.ctx.sim_step(nsteps)
 
+    def set_params(self, p):
+        """New parameters for the running sim (bsa_sim_set_params; e.g. ZONER / DTLOOK)."""
+        self.ctx.sim_set_params(p)
+        self.params = p
+
+    def halo_stats(self):
+        """Halo exchange of the sharded step (bsa_sim_halo_stats): rx / tx bytes per CD
+        call, tiles received at the last CD call, capacity regrowths."""
+        return self.ctx.sim_halo_stats()
+
     def update(self, **arrays):
         """Overwrite state arrays (host simulator changed the traffic between
         steps) keeping the ASAS bookkeeping (bsa_sim_update)."""

@@ -287,7 +287,8 @@ int bsa_comm_init(bsa_ctx *ctx, int nranks, int rank, const char *id128);
  * device-to-device copies ordered by HIP events (RCCL refuses two ranks on one
  * GPU; this runs the nranks > 1 paths on one GPU and lets one process drive
  * several).  Create the group, then every rank joins it from its thread; the
- * group outlives its contexts (destroy it after them). */
+ * group is freed by bsa_group_destroy once no context is joined any more
+ * (destroying it earlier defers the free to its last member's leaving). */
 typedef struct bsa_group bsa_group;
 bsa_group *bsa_group_create(int nranks);  /* NULL if nranks is not in [1, 16] */
 void bsa_group_destroy(bsa_group *g);
@@ -372,9 +373,10 @@ int bsa_sim_step(bsa_ctx *ctx, int nsteps);
  * vs / alt are clipped to a per-aircraft envelope (full-n host arrays, copied:
  * hmax [m], vmin / vmax [m/s CAS], vsmin / vsmax [m/s], axmax [m/s^2]), the
  * vertical-speed cap scaled by (1 - ax/axmax) with ax = traf.ax of the
- * previous step (0 after bsa_sim_init).  The envelope is a frozen input
- * (OpenAP's per-phase table update, perfoap.py:115-183, is not modelled);
- * hmax == NULL switches the limits off (the default after bsa_sim_init). */
+ * previous step (0 after bsa_sim_init).  The envelope is a frozen input here;
+ * OpenAP's per-phase envelope update (perfoap.py:115-183) is bsa_sim_set_perf,
+ * which takes precedence.  hmax == NULL switches the limits off (the default
+ * after bsa_sim_init). */
 int bsa_sim_set_limits(bsa_ctx *ctx, const double *hmax, const double *vmin, const double *vmax,
                        const double *vsmin, const double *vsmax, const double *axmax);
 /* OpenAP.update (performance/openap/perfoap.py:115-131) inside the step:
@@ -430,9 +432,20 @@ int bsa_sim_stats(bsa_ctx *ctx, int64_t *out6);
 int bsa_sim_row_ids(bsa_ctx *ctx, int32_t *ids);
 /* Measurement aid: the sim's detect (home order, its rpz / hpz / tla) of the
  * home rows [row_begin, row_end) (row_begin a multiple of 512) against all
- * columns -- one rank's share of a CD step, on one GPU.  The pairs are
- * fetchable like a bsa_detect's; the sim's own state is not changed. */
+ * columns -- one rank's share of a CD step, on one GPU, as that rank computes
+ * it: its own column tiles, the halo plan, the halo tiles (bsa_sim_halo_stats
+ * [2] counts them; the boxes of all tiles, which the other ranks would send,
+ * are prepared before the timed stages).  Its pairs REPLACE the
+ * last CD call's as the fetchable / gatherable pairs (bsa_fetch_pairs); the
+ * sim's state and ASAS bookkeeping are not changed, and the next CD step
+ * detects the sim's own rows again. */
 int bsa_sim_detect_rows(bsa_ctx *ctx, int64_t row_begin, int64_t row_end, int64_t *n_conf, int64_t *n_los);
+/* Halo exchange of the sharded step (several ranks): [0] bytes
+ * this rank receives and [1] sends per CD call (the agreed capacities' regions),
+ * [2] column tiles (512 aircraft) it received at the last CD call -- or, after
+ * bsa_sim_detect_rows, the tiles that rank share needs from other ranks --
+ * and [3] capacity regrowths (aborted and re-run steps) since bsa_sim_init. */
+int bsa_sim_halo_stats(bsa_ctx *ctx, int64_t *out4);
 /* ASAS bookkeeping after the last CD call (resume_nav = 1; replaces
  * ASAS.update's Python sets, asas.py:490-502):
  * [0] |resopairs| of this rank's rows, [1] |confpairs_unique|,
@@ -445,6 +458,37 @@ int bsa_sim_asas_stats(bsa_ctx *ctx, int64_t *out6);
  * row, for an intruder deleted since the last CD call), at most cap pairs;
  * *count = total (call again with a larger buffer when *count > cap). */
 int bsa_sim_resopairs(bsa_ctx *ctx, int32_t *idx1, int32_t *idx2, int64_t cap, int64_t *count);
+
+/* One CD call of the resident sim WITHOUT the kinematics: [all-gather] ->
+ * detect -> resolver -> asas.active or the bookkeeping + ResumeNav, i.e. the
+ * body of ASAS.update (asas.py:478-504), exactly the CD part of a
+ * bsa_sim_step; the state does not move and the step count does not advance.
+ * The ASAS.update drop-in (bluesky_amd/asas.py) runs it after writing the host
+ * simulator's traffic with bsa_sim_update.  Overflows are grown and re-run
+ * inside the call.  Collective with several ranks. */
+int bsa_sim_cd(bsa_ctx *ctx);
+/* Replace the parameters of a running sim (stack commands such as ZONER,
+ * ZONEDH, DTLOOK, RMETHH change asas.R / dh / dtlookahead / the MVP switches
+ * between calls, asas.py:190-395).  Turning resume_nav on starts with empty
+ * bookkeeping. */
+int bsa_sim_set_params(bsa_ctx *ctx, const bsa_sim_params *p);
+/* NORESO / RESOOFF lists (asas.noresolst / asas.resoofflst, MVP.py:44-61) as
+ * full-n uint8 host arrays of membership in aircraft-index order (NULL = empty
+ * list); the step's MVP applies them when mvp.swnoreso / swresooff are set.
+ * They follow bsa_sim_delete / bsa_sim_create (new aircraft are in neither). */
+int bsa_sim_set_reso_lists(bsa_ctx *ctx, const uint8_t *noreso, const uint8_t *resooff);
+/* ASAS outputs of this rank's rows after the last CD call, written into
+ * full-n host arrays (other rows untouched; any pointer may be NULL):
+ * asas.trk / tas / vs / alt, asase / asasn (float32), asas.active, and
+ * dropped = 1 for an ownship of which ResumeNav dropped a resopair in that call
+ * (asas.py:454-468: the reference then starts waypoint recovery with
+ * route.direct, which is autopilot state the host applies; resume_nav = 1). */
+typedef struct bsa_asas_out {
+  double *trk, *tas, *vs, *alt;
+  float *asase, *asasn;
+  uint8_t *active, *dropped;
+} bsa_asas_out;
+int bsa_sim_read_asas(bsa_ctx *ctx, bsa_asas_out *o);
 
 /* ACDATA feed: the per-aircraft fields
  * ScreenIO.send_aircraft_data streams at 5 Hz

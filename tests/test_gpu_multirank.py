@@ -240,3 +240,127 @@ def test_home_ranges_and_row_ids(ctx):
         assert sim.stats()['steps'] == 0
     finally:
         c.close()
+
+
+# ---------------------------------------------------------------- halo exchange
+def sharded_vs_world1(ctx, t, p, world, steps, between=None, resume_nav=False):
+    """World-1 run vs ``world`` in-process ranks: every state array bitwise, the
+    C2-gathered pair lists bitwise (and the ASAS bookkeeping with resume_nav)
+    after each of ``steps`` steps; ``between(k, sim)`` may change parameters
+    before step k on every rank.  Returns the ranks' halo statistics."""
+    init = resident.initial_state(t)
+    ref = resident.ResidentSim(init, p, ctx=ctx)
+    exp = []
+    for k in range(steps):
+        if between:
+            between(k, ref)
+        ref.step(1)
+        st = ref.stats()
+        e = dict(state=ref.read(), pairs=ctx.fetch_pairs(st['n_conf'], st['n_los']))
+        if resume_nav:
+            i, j = ref.resopairs()
+            e.update(bk=ref.asas_stats(), reso=sorted(zip(i.tolist(), j.tolist())))
+        exp.append(e)
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=world, group=g)
+        got = []
+        for k in range(steps):
+            if between:
+                between(k, sim)
+            sim.step(1)
+            e = dict(state=sim.read(), pairs=sim.gather_pairs(root=0), halo=sim.halo_stats())
+            if resume_nav:
+                i, j = sim.resopairs()
+                e.update(bk=sim.asas_stats(), reso=list(zip(i.tolist(), j.tolist())))
+            got.append(e)
+        return got
+
+    res = run_ranks(world, rank, timeout=600)
+    for k in range(steps):
+        for r in range(world):
+            g = res[r][k]
+            for f, v in exp[k]['state'].items():
+                assert np.array_equal(g['state'][f], v), 'step %d rank %d %s' % (k, r, f)
+        pairs = res[0][k]['pairs']
+        for f in ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'li', 'lj', 'inconf', 'tcpamax'):
+            assert np.array_equal(pairs[f], exp[k]['pairs'][f]), 'step %d %s' % (k, f)
+        if resume_nav:
+            assert sorted(sum((res[r][k]['reso'] for r in range(world)), [])) == exp[k]['reso'], k
+            for r in range(world):
+                for f in ('confpairs_unique', 'lospairs_unique', 'confpairs_all', 'lospairs_all'):
+                    assert res[r][k]['bk'][f] == exp[k]['bk'][f], (k, r, f)
+    return [[res[r][k]['halo'] for k in range(steps)] for r in range(world)], exp
+
+
+@pytest.mark.slow
+def test_halo_8ranks_global1m_equal_world1(ctx):
+    """BASELINE configs[4]: 1M aircraft on the globe, ownship rows over 8 ranks
+    (in-process group on one GPU: the same halo plan, pack / exchange / unpack
+    as over RCCL).  3 steps with MVP (CD every step): every state array and the
+    gathered pair lists bitwise equal to the one-rank run; each rank receives far
+    less than the full state (48 MB per CD call at 1M)."""
+    t = synth.workload('global1m')
+    halo, exp = sharded_vs_world1(ctx, t, resident.params(cd_every=1), 8, 3)
+    assert len(exp[-1]['pairs']['ci']) > 0
+    rx = [h[-1]['rx_bytes'] for h in halo]
+    assert max(rx) < 10 * 2 ** 20, rx           # verdict r02: <= 10 MB per rank per CD step
+    assert all(h[-1]['tiles'] > 0 for h in halo)
+    assert all(h[-1]['regrowths'] == 0 for h in halo)   # exact initial capacities
+
+
+def test_halo_requests_and_regrowth_equal_world1(ctx):
+    """ResumeNav reads the state of every resopair's intruder, wherever it is:
+    after conflicts found with a long look-ahead, DTLOOK drops to 20 s, so the
+    box test no longer reaches many kept resopairs' intruders -- they come in
+    through the request bits.  Then ZONER grows the zone: the halo outgrows its
+    capacities, the step aborts, every rank regrows the same capacities and
+    re-runs.  Bitwise equal to the one-rank run throughout (state, pairs,
+    resopairs, global counts)."""
+    t = synth.box(20000, 800.0, seed=83)
+    p0 = resident.params(simdt=5.0, tla=300.0, resume_nav=True)
+    p1 = resident.params(simdt=5.0, tla=20.0, resume_nav=True)
+    p2 = resident.params(simdt=5.0, tla=900.0, rpz=40 * resident.NM, resume_nav=True)
+
+    def between(k, sim):
+        if k == 3:
+            sim.set_params(p1)
+        if k == 6:
+            sim.set_params(p2)
+
+    halo, exp = sharded_vs_world1(ctx, t, p0, 3, 9, between=between, resume_nav=True)
+    assert exp[5]['bk']['resopairs'] > 0
+    assert max(h[-1]['regrowths'] for h in halo) > 0
+
+
+def test_halo_probe_shares_equal_full_detect(ctx):
+    """bsa_sim_detect_rows as one rank of 8 computes its share (own tiles, halo
+    plan, halo tiles only) at the 100k bench workload: the 8 shares' pairs
+    together are exactly the full detect's (same pairs, same payload bits), and
+    each share needs only part of the other ranks' tiles."""
+    t = synth.workload('box100k')
+    n = t.ntraf
+    c2 = _lib.Context(0)
+    try:
+        full = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c2)
+    finally:
+        c2.close()
+    sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
+    rpr = ((n + 7) // 8 + 511) // 512 * 512
+    nct = (n + 511) // 512
+    parts = []
+    for r in range(8):
+        rb, re = r * rpr, min(n, (r + 1) * rpr)
+        nc, nl = ctx.sim_detect_rows(rb, re)
+        parts.append(ctx.fetch_pairs(nc, nl))
+        tiles = ctx.sim_halo_stats()['tiles']
+        assert 0 < tiles < nct - (re - rb + 511) // 512, (r, tiles)
+    for a, b, pay in (('ci', 'cj', ('qdr', 'dist', 'tcpa', 'tinconf')), ('li', 'lj', ())):
+        i = np.concatenate([p[a] for p in parts])
+        j = np.concatenate([p[b] for p in parts])
+        o = np.lexsort((j, i))
+        assert np.array_equal(i[o], full[a]) and np.array_equal(j[o], full[b]), a
+        for f in pay:
+            assert np.array_equal(np.concatenate([p[f] for p in parts])[o], full[f]), f
+    assert sum(int(p['inconf'].sum()) for p in parts) == int(full['inconf'].sum())
+    assert sim.stats()['steps'] == 0
