@@ -16,7 +16,6 @@ sim-steps/s = K / time.  Rows are partitioned, total work is fixed:
 scaling "strong".
 """
 import argparse
-import hashlib
 import json
 import os
 import platform
@@ -42,18 +41,17 @@ TIMING_SAMPLE = 8            # detects per HIP-event-timed detect (bsa_set_timin
                              # costs ~24 us of event bubbles, profiles/r02 kernel trace)
 
 
-def pmc_figures():
+def pmc_figures(lib_sha):
     """Per-launch memory-side bytes etc. from the committed rocprofv3 --pmc
     passes of this bench (tools/pmc_roofline.py) -- only if they were taken on
-    THIS build of libbsaccel.so (sha256 recorded by pmc_roofline.py); else {}."""
+    THE build of libbsaccel this process mapped (the sha256 pmc_roofline.py
+    took from the profiled bench's own output); else {}."""
     try:
         with open(PMC_JSON) as f:
             pmc = json.load(f)
-        with open(_lib.LIB_PATH, 'rb') as f:
-            sha = hashlib.sha256(f.read()).hexdigest()
     except (OSError, ValueError):
         return {}
-    return pmc if pmc.get('_meta', {}).get('lib_sha256') == sha else {}
+    return pmc if pmc.get('_meta', {}).get('lib_sha256') == lib_sha else {}
 
 
 def cpu_model():
@@ -121,12 +119,25 @@ def global1m_line(ctx, rank, world, warmup=2, steps=5):
     tm, ts = ctx.timing_summary()
     st = sim.stats()
     counts = ctx.allreduce_sum([st['n_conf'], st['n_los']])
-    return dict(workload='global1m N=%d (seed 7)' % n, steps=steps, ms_per_step=dt / steps * 1e3,
+    halo = halo_line(ctx, sim) if world > 1 else None
+    return dict(workload='global1m N=%d (seed 7)' % n, halo=halo, steps=steps, ms_per_step=dt / steps * 1e3,
                 sim_steps_per_s=steps / dt, pair_evals_per_s=float(n) * n * steps / dt,
                 n_conf=int(counts[0]), n_los=int(counts[1]),
                 kernels_ms_rank0=dict(k0_prep=tm['prep'], prefilter=tm['prefilter'], exact=tm['exact'],
                                       k2_sort=tm['sort'], detect_total=tm['total']),
                 candidates_rank0=ts['candidates'] / max(ts['detects'], 1))
+
+
+def halo_line(ctx, sim):
+    """Bytes each rank exchanged per CD call (max over ranks; collective)."""
+    h = sim.halo_stats()
+    mx = ctx.allreduce_max([h['rx_bytes'], h['tx_bytes'], h['tiles'], h['regrowths']])
+    tot = ctx.allreduce_sum([h['rx_bytes']])
+    return dict(rx_bytes_per_cd_max_rank=int(mx[0]), tx_bytes_per_cd_max_rank=int(mx[1]),
+                rx_bytes_per_cd_all_ranks=int(tot[0]), tiles_received_max_rank=int(mx[2]),
+                regrowths=int(mx[3]),
+                note='halo exchange (grouped RCCL send/recv of the column tiles a rank\'s rows can reach) '
+                     'instead of the full-state all-gather; 512 aircraft x 6 or 8 fp64 per tile')
 
 
 def timed_steps(ctx, sim, warmup, steps):
@@ -242,16 +253,20 @@ def main():
     value = pairs / dt
     pf_s = tm['prefilter'] * 1e-3
     tested = ts['groups'] / max(ts['detects'], 1) * _lib.PF_BLOCK_PAIRS    # pair tests the prefilter executed
-    pmc = pmc_figures()
+    lib_path, lib_sha = _lib.mapped_library()
+    pmc = pmc_figures(lib_sha)
+    prov = dict(file=os.path.relpath(PMC_JSON, REPO), lib_sha256=lib_sha,
+                passes=pmc.get('_meta', {}).get('passes')) if pmc else None
     pf = pmc.get('k_prefilter', {})
     roof = dict(bound='valu', kernel='k_prefilter (fp32 packed VALU stage-1 test, dominant)',
                 achieved=tested * PF_FLOPS_PER_PAIR / pf_s / 1e12, peak=FP32_PEAK_TFLOPS,
                 unit='TFLOP/s')
     roof['frac'] = roof['achieved'] / roof['peak']
     roof['traffic'] = (pf['hbm_read_bytes'] + pf['hbm_write_bytes']) if 'hbm_write_bytes' in pf else None
-    roof['traffic_source'] = ('profiles/pmc_latest.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per '
-                              'launch), taken on this build of libbsaccel.so' if pmc else
+    roof['traffic_source'] = ('rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch, from_profile (the '
+                              'committed passes of this bench on this very library)' if pmc else
                               'no PMC summary for this build of libbsaccel.so')
+    roof['from_profile'] = prov
     if 'lds_bank_conflict_rate' in pf:
         roof['lds_bank_conflict_rate'] = pf['lds_bank_conflict_rate']
     kin = pmc.get('k_sim_pilot_kin', {})
@@ -259,7 +274,7 @@ def main():
     if kin.get('dur_ns'):
         nrows_r0 = (n + world - 1) // world
         alg = KIN_BYTES_PER_AC * nrows_r0
-        propagation = dict(kernel='k_sim_pilot_kin', bound='hbm', algorithmic_bytes=alg,
+        propagation = dict(kernel='k_sim_pilot_kin', bound='hbm', algorithmic_bytes=alg, from_profile=prov,
                            duration_us_profiled=kin['dur_ns'] * 1e-3,
                            achieved_GBps=alg / kin['dur_ns'], peak_GBps=HBM_PEAK_GBPS,
                            frac=alg / kin['dur_ns'] / HBM_PEAK_GBPS,
@@ -267,7 +282,7 @@ def main():
     ex = pmc.get('k_exact', {})
     exact_fp64 = None
     if ex.get('fp64_flops'):
-        exact_fp64 = dict(kernel='k_exact', fp64_flops_per_launch=ex['fp64_flops'],
+        exact_fp64 = dict(kernel='k_exact', fp64_flops_per_launch=ex['fp64_flops'], from_profile=prov,
                           achieved_TFLOPs=ex['fp64_flops'] / (tm['exact'] * 1e-3) / 1e12,
                           peak_TFLOPs=FP64_PEAK_TFLOPS)
     out = dict(metric='CD pair-evals/s at 100k aircraft (GPU-resident sim step, ASAS every step)',
@@ -289,7 +304,10 @@ def main():
                tile_pairs_rank0=ts['tiles'] / max(ts['detects'], 1),
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),
-               propagation=propagation, exact_fp64=exact_fp64)
+               propagation=propagation, exact_fp64=exact_fp64,
+               build=dict(lib_path=os.path.relpath(lib_path, REPO), lib_sha256=lib_sha))
+    if world > 1:   # the halo exchange that replaced the full-state all-gather
+        out['halo'] = halo_line(ctx, sim)
     if world > 1:   # C2: the last CD call's pair lists of all ranks to rank 0's host
         g0 = time.perf_counter()
         gp = sim.gather_pairs(root=0)

@@ -186,6 +186,8 @@ SIGNATURES.update({
     'bsa_sim_set_reso_lists': (ctypes.c_int, [_vp, _c_u8p, _c_u8p]),
     'bsa_sim_read_asas': (ctypes.c_int, [_vp, ctypes.POINTER(AsasOut)]),
     'bsa_sim_halo_stats': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_sim_set_atmos': (ctypes.c_int, [_vp, ctypes.c_int]),
+    'bsa_sim_read_atmos': (ctypes.c_int, [_vp, _c_dp, _c_dp, _c_dp]),
 })
 
 UNIQUE_ID_BYTES = 128
@@ -217,6 +219,26 @@ def load(path=None):
             raise AccelUnavailable('ABI mismatch: library %d, bindings %d' % (v, ABI_VERSION))
         _lib = lib
         return lib
+
+
+def mapped_library():
+    """(path, sha256) of the libbsaccel this process actually mapped (from
+    /proc/self/maps; measurement provenance: bench.py / tools/pmc_roofline.py)."""
+    import hashlib
+    load()
+    path = None
+    try:
+        with open('/proc/self/maps') as f:
+            for line in f:
+                q = line.split()
+                if len(q) >= 6 and os.path.basename(q[-1]).startswith('libbsaccel'):
+                    path = q[-1]
+                    break
+    except OSError:
+        pass
+    path = path or os.path.realpath(LIB_PATH)
+    with open(path, 'rb') as f:
+        return path, hashlib.sha256(f.read()).hexdigest()
 
 
 def comm_unique_id():
@@ -586,7 +608,8 @@ class Context:
         self.gen += 1
         self.check(self.lib.bsa_sim_create(self.h, m, ctypes.byref(st)), 'bsa_sim_create')
         self.n += m
-        self._rows = (0, self.n)
+        st = self.sim_stats()
+        self._rows = (st['row_begin'], st['row_end'])
 
     def sim_delete(self, idx):
         """bsa_sim_delete: remove aircraft ``idx``; the rest shift down in order
@@ -595,7 +618,8 @@ class Context:
         self.gen += 1
         self.check(self.lib.bsa_sim_delete(self.h, len(d), ptr(d, _c_i64p)), 'bsa_sim_delete')
         self.n -= len(d)
-        self._rows = (0, self.n)
+        st = self.sim_stats()
+        self._rows = (st['row_begin'], st['row_end'])
 
     def sim_step(self, nsteps=1):
         self.gen += 1
@@ -669,6 +693,16 @@ class Context:
         self.gen += 1
         self._rows = (int(row_begin), int(row_end))
         return nc.value, nl.value
+
+    def sim_set_atmos(self, on=True):
+        """bsa_sim_set_atmos: compute traf.p / rho / Temp = vatmos(alt) in every step."""
+        self.check(self.lib.bsa_sim_set_atmos(self.h, int(bool(on))), 'bsa_sim_set_atmos')
+
+    def sim_read_atmos(self):
+        """(p, rho, Temp) of this rank's rows after the last step (full-n arrays)."""
+        o = [np.zeros(self.n) for _ in range(3)]
+        self.check(self.lib.bsa_sim_read_atmos(self.h, *[ptr(a) for a in o]), 'bsa_sim_read_atmos')
+        return tuple(o)
 
     def sim_halo_stats(self):
         """bsa_sim_halo_stats: bytes received / sent per CD call, tiles received at the

@@ -300,6 +300,8 @@ struct Ctx {
   // NORESO / RESOOFF membership (bsa_sim_set_reso_lists, u8 in home order) and
   // the rows whose ResumeNav dropped a pair in the last CD call (u8, home order)
   DevBuf s_noreso, s_resooff, s_dropped;
+  DevBuf s_atm;          // traf.p / rho / Temp = vatmos(traf.alt) of the last step (3 x n), when on
+  bool sim_atmos = false;
   bool sim_noreso = false, sim_resooff = false;
   const uint8_t *fuse_noreso = nullptr;  // NORESO list for K2's fused MVP per-pair vectors
   int64_t sim_ntypes = 0;
@@ -383,6 +385,8 @@ int download_pairs(Ctx *c, HostPairs &h);
 void home_pairs_to_ids(const Ctx *c, int64_t rb, HostPairs &h);
 // resident sim (bsa_sim.hip): the maps of Ctx::h2id_h (host + device, lpos of this rank's rows)
 int set_home_maps(Ctx *c);
+// this rank's 512-aligned home range [sim_rb, sim_re) and rows per rank for c->n (bsa_sim.hip)
+void set_rank_rows(Ctx *c);
 
 // error helpers
 int fail(Ctx *c, const char *fmt, ...);

@@ -37,6 +37,7 @@ struct SimDev {
   const double *ptab;              // OpenAP type table (bsa_sim_set_perf) or NULL: envelope and
   const int *ptype;                //   acceleration follow each aircraft's flight phase
   uint8_t *phase;
+  double *atm;                     // traf.p / rho / Temp (traffic.py:389), 3 x n, or NULL
   int n;
   const double *aptrk, *aptas, *apalt, *apvs, *bank, *eps, *accel;
   const double *atrk, *atas, *avs, *aalt;
@@ -93,6 +94,13 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
     s.phdg = kin::nprem(ptrk, 360.);                  // pilot.py:63
   }
   s.accel = d.accel[k];
+  if (d.atm) {  // Traffic.update's first statement: p, rho, Temp = vatmos(alt) (traffic.py:389)
+    double p, rho, T;
+    kin::vatmos(d.alt[k], p, rho, T);
+    d.atm[k] = p;
+    d.atm[d.n + k] = rho;
+    d.atm[2 * d.n + k] = T;
+  }
   if (d.ptab) {  // OpenAP.update (perfoap.py:115-131) on the pre-step state, then applylimits
     const double *row = d.ptab + (size_t)d.ptype[k] * kin::kPerfCols;
     const int ph = kin::openap_phase(row[22], d.vs[k], d.alt[k]);
@@ -172,6 +180,7 @@ static SimDev sim_dev(Ctx *c) {
   d.ptab = c->sim_perf ? (const double *)c->s_ptab.p : nullptr;
   d.ptype = (const int *)c->s_ptype.p;
   d.phase = (uint8_t *)c->s_phase.p;
+  d.atm = c->sim_atmos ? (double *)c->s_atm.p : nullptr;
   d.n = (int)c->n;
   d.aptrk = (const double *)c->s_aptrk.p;
   d.aptas = (const double *)c->s_aptas.p;
@@ -274,7 +283,7 @@ void sim_release(Ctx *c) {
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
                    &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env,
-                   &c->s_ptab, &c->s_ptype, &c->s_phase, &c->s_noreso, &c->s_resooff, &c->s_dropped};
+                   &c->s_ptab, &c->s_ptype, &c->s_phase, &c->s_noreso, &c->s_resooff, &c->s_dropped, &c->s_atm};
   for (auto *b : all) release(*b);
   bk_release(c);
   halo_release(c);
@@ -454,8 +463,13 @@ static int grow_after_abort(Ctx *c, const unsigned long long *ctl) {
   if (c->halo_mode == 1 && halo_grow(c)) return -1;
   if (ctl[2] > 0)  // this rank's resopairs outgrew their buffer
     c->bk_cap = std::max(2 * c->bk_cap, ctl[2] + ctl[2] / 4 + 1024);
-  if (ctl[3] > 0)  // this rank's pair keys outgrew their all-gather block
-    c->bk_kw = std::max(2 * c->bk_kw, ctl[3] + ctl[3] / 4 + 1024);
+  // pair keys outgrew their all-gather block on some rank: the block width is
+  // part of the all-gather's layout, so every rank grows to the same width
+  // (max-all-reduced demand; collective, every rank aborted at this step)
+  double kdem = (double)ctl[3];
+  if (comm_multi(c) && comm_allreduce_host(c, &kdem, 1, true)) return -1;
+  if (kdem > 0)
+    c->bk_kw = std::max<unsigned long long>(2 * c->bk_kw, (unsigned long long)kdem + (unsigned long long)kdem / 4 + 1024);
   // candidate overflow on this rank: enough for the last detect's demand (its
   // shard counters keep counting past the capacity; every detect after the
   // abort ran on the same, unchanged state)
@@ -530,6 +544,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
     return -1;
   BSA_HIP(c, hipMemsetAsync(c->s_dropped.p, 0, n, c->stream));
   c->sim_noreso = c->sim_resooff = false;  // empty NORESO / RESOOFF lists
+  c->sim_atmos = false;
   BSA_HIP(c, hipMemsetAsync(c->s_ax.p, 0, N8, c->stream));   // traf.ax: 0 at create
   c->sim_limits = false;
   c->sim_perf = false;
@@ -939,6 +954,32 @@ int bsa_sim_read_asas(bsa_ctx *cc, bsa_asas_out *o) {
   std::vector<char> tmp;
   for (auto &e : cp)
     if (e.dst && bsa::get_home(c, e.dst, e.src, e.esz, c->sim_rb, c->sim_re, tmp)) return -1;
+  return 0;
+}
+
+int bsa_sim_set_atmos(bsa_ctx *cc, int on) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_set_atmos before bsa_sim_init");
+  BSA_HIP(c, hipSetDevice(c->device));
+  if (on && !c->sim_atmos) {
+    if (!bsa::ensure(c, c->s_atm, (size_t)c->n * 24, "atmosphere")) return -1;
+    BSA_HIP(c, hipMemsetAsync(c->s_atm.p, 0, (size_t)c->n * 24, c->stream));
+  }
+  c->sim_atmos = on != 0;
+  return 0;
+}
+
+int bsa_sim_read_atmos(bsa_ctx *cc, double *p, double *rho, double *temp) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready || !c->sim_atmos) return bsa::fail(c, "bsa_sim_read_atmos: atmosphere outputs are off");
+  BSA_HIP(c, hipSetDevice(c->device));
+  std::vector<char> tmp;
+  double *dst[3] = {p, rho, temp};
+  for (int k = 0; k < 3; ++k)
+    if (dst[k] && bsa::get_home(c, dst[k], (const char *)c->s_atm.p + (size_t)k * c->n * 8, 8, c->sim_rb, c->sim_re, tmp))
+      return -1;
   return 0;
 }
 

@@ -396,6 +396,13 @@ int bsa_sim_set_perf(bsa_ctx *ctx, int64_t ntypes, const double *table, const in
  * (0..8, phase.py:4-12; needs bsa_sim_set_perf) and of traf.ax, written into
  * full-n host arrays; either pointer may be NULL. */
 int bsa_sim_read_perf(bsa_ctx *ctx, uint8_t *phase, double *ax);
+/* Traffic.update's atmosphere, traf.p / rho / Temp = vatmos(traf.alt) on the
+ * pre-step altitude (traffic.py:389, aero.py:62-74), computed inside the step
+ * when on (off after bsa_sim_init: nothing in the step reads them; a host
+ * performance model in hybrid mode does).  _read: this rank's rows of the last
+ * step into full-n host arrays [Pa, kg/m3, K]; any pointer may be NULL. */
+int bsa_sim_set_atmos(bsa_ctx *ctx, int on);
+int bsa_sim_read_atmos(bsa_ctx *ctx, double *p, double *rho, double *temp);
 /* Overwrite per-aircraft arrays of the resident sim (full-n host arrays, all
  * ranks pass the same) while keeping the ASAS bookkeeping (resopairs, the
  * previous call's pair sets, asas.active / trk / tas / vs) and traf.ax: the
@@ -408,7 +415,10 @@ int bsa_sim_update(bsa_ctx *ctx, const bsa_sim_state *s);
  * asas.py:402-407): append m aircraft whose state is s (m-long host arrays,
  * every field required); asas.trk / tas start at trk / tas, asas.alt at
  * s->asas_alt, asas.vs / active / traf.ax at 0.  They take indices n..n+m-1.
- * One rank only; fails while OpenAP limits are on (set them again after). */
+ * Fails while OpenAP limits are on (set them again after).  Collective with
+ * several ranks (all pass the same arrays): every rank's replicas are completed
+ * first, the rows re-partitioned over the new n afterwards (each rank keeps
+ * the bookkeeping of its new range). */
 int bsa_sim_create(bsa_ctx *ctx, int64_t m, const bsa_sim_state *s);
 /* Traffic.delete for the resident sim (traffic.py:364-378 ->
  * trafficarrays.py:99-117): remove the k aircraft idx[0..k) (any order,
@@ -417,7 +427,8 @@ int bsa_sim_create(bsa_ctx *ctx, int64_t m, const bsa_sim_state *s);
  * resopairs of a deleted ownship go; a resopair whose intruder was deleted
  * stays (bsa_sim_resopairs reports idx2 = -1) until the next CD call's
  * ResumeNav switches the ownship's ASAS off and drops it (asas.py:419-468).
- * One rank only; removing every aircraft is an error (re-init instead). */
+ * Removing every aircraft is an error (re-init instead).  Collective with
+ * several ranks (all pass the same list), re-partitioned as bsa_sim_create. */
 int bsa_sim_delete(bsa_ctx *ctx, int64_t k, const int64_t *idx);
 /* Full-n host copies of the state (collective: gathers all ranks' rows).
  * Any pointer may be NULL. */

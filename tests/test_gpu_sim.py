@@ -449,3 +449,29 @@ def test_resident_row_bucket_overflow_retry_is_exact(ctx):
         assert sim.stats()['n_conf'] == ref.stats()['n_conf'] > 0
     finally:
         c.close()
+
+
+def test_resident_atmosphere_outputs(ctx):
+    """traf.p / rho / Temp = vatmos(traf.alt) (traffic.py:389, the first thing
+    Traffic.update does, on the pre-step altitude) from the resident step when
+    switched on (bsa_sim_set_atmos), against the oracle's vatmos (aero.py:62-74),
+    including through a delete (the arrays follow np.delete)."""
+    from oracle import kinematics as okin
+    t = synth.box(3000, 150.0, seed=97)
+    t.alt[:50] = np.linspace(0.0, 20000.0, 50)   # troposphere, tropopause and stratosphere
+    sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=2), ctx=ctx)
+    ctx.sim_set_atmos(True)
+    for k in range(3):
+        alt0 = sim.read()['alt']
+        sim.step(1)
+        p, rho, T = ctx.sim_read_atmos()
+        ep, erho, eT = okin.vatmos(alt0)
+        for g, e in ((p, ep), (rho, erho), (T, eT)):
+            ok, msg = util.close(g, e, 1.0)
+            assert ok, 'step %d: %s' % (k, msg)
+    sim.delete([3, 7])
+    p2, _, _ = ctx.sim_read_atmos()
+    assert np.array_equal(p2, np.delete(p, [3, 7]))
+    ctx.sim_set_atmos(False)
+    with pytest.raises(_lib.AccelError):
+        ctx.sim_read_atmos()

@@ -2,7 +2,14 @@
 """Turn rocprofv3 --pmc passes of the bench into the per-launch figures that
 bench.py reports next to its live timings (profiles/pmc_latest.json).
 
-usage: pmc_roofline.py OUT.json PASSDIR [PASSDIR ...]
+usage: pmc_roofline.py [--bench-json B.json] OUT.json PASSDIR [PASSDIR ...]
+
+The library the counters belong to is recorded in _meta.lib_sha256, taken
+from the profiled bench's own output line (bench.py prints the sha256 of the
+libbsaccel it actually mapped, BSACCEL_LIB resolved) when --bench-json is
+given, else hashed from $BSACCEL_LIB or the in-tree default.  Nothing edits
+_meta by hand: bench.py reports the PMC figures only when that sha equals the
+sha of the library it mapped itself.
 
 Per kernel and per launch (mean over dispatches):
   hbm_read_bytes   = 2 * FETCH_SIZE[KB] * 1024   (gfx950 FETCH_SIZE counts half of a
@@ -25,7 +32,11 @@ from pmc_summary import load  # noqa: E402
 
 
 def main():
-    out, dirs = sys.argv[1], sys.argv[2:]
+    args = sys.argv[1:]
+    bench_json = None
+    if args[:1] == ['--bench-json']:
+        bench_json, args = args[1], args[2:]
+    out, dirs = args[0], args[1:]
     merged = {}
     for d in dirs:
         for k, cs in load(d).items():
@@ -52,9 +63,18 @@ def main():
             r['fp64_flops'] = 64.0 * (2 * f64[0] + f64[1] + f64[2] + f64[3])
         res[name] = r
     # the library these counters belong to: bench.py reports them only for the same build
-    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'bluesky_amd', 'libbsaccel.so')
-    with open(lib, 'rb') as f:
-        res['_meta'] = {'lib_sha256': hashlib.sha256(f.read()).hexdigest()}
+    meta = {'passes': [os.path.basename(os.path.normpath(d)) for d in dirs]}
+    if bench_json:
+        with open(bench_json) as f:
+            line = [x for x in f if x.startswith('{')][-1]
+        b = json.loads(line)['build']
+        meta.update(lib_sha256=b['lib_sha256'], lib_path=b['lib_path'], sha_source='profiled bench output')
+    else:
+        lib = os.environ.get('BSACCEL_LIB') or os.path.join(
+            os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'bluesky_amd', 'libbsaccel.so')
+        with open(lib, 'rb') as f:
+            meta.update(lib_sha256=hashlib.sha256(f.read()).hexdigest(), lib_path=lib, sha_source='hashed file')
+    res['_meta'] = meta
     with open(out, 'w') as f:
         json.dump(res, f, indent=1, sort_keys=True)
     for k in ('k_prefilter', 'k_exact', 'k_sim_pilot_kin'):
