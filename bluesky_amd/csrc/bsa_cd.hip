@@ -1900,7 +1900,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // BSA_HOME_REC=0/1 overrides.
   static const int home_rec_env = getenv("BSA_HOME_REC") ? atoi(getenv("BSA_HOME_REC")) : -1;
   const bool recs = !home || (home_rec_env >= 0 ? home_rec_env == 1 : (n < (1 << 18) && c->nranks == 1));
-  if (home && (distinct || rb % kTile != 0 || (flags & BSA_FLAG_KWIK)))
+  if (home && (distinct || (rb % kTile != 0 && re > rb) || (flags & BSA_FLAG_KWIK)))  // (a rank without rows: rb = n)
     return fail(c, "home-order detect needs own == intruder, a %d-aligned row slice, no KWIK", kTile);
   const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;
   // KWIK: stage 1 is exact-safe only with the pair's own mean latitude in

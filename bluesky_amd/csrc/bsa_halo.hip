@@ -281,7 +281,8 @@ static int plan_local(Ctx *c, int a0, int a1, int tpr) {
 
 int halo_mid(Ctx *c, int64_t rb, int64_t re) {
   const int nct = nct_of(c);
-  const int a0 = (int)(rb / kTile), a1 = std::max(a0, (int)((re + kTile - 1) / kTile)), na = a1 - a0;
+  // (a rank without rows owns no tile: its clamped rb = n need not be tile-aligned)
+  const int a0 = (int)(rb / kTile), a1 = re > rb ? (int)((re + kTile - 1) / kTile) : a0, na = a1 - a0;
   if (c->halo_mode == 2) {
     c->halo_fields = 0;
     return plan_local(c, a0, a1, std::max(na, 1));

@@ -17,8 +17,9 @@
 // order of the remaining aircraft), so no re-sort is needed.  Limitation: a
 // callsign deleted and re-created before the next CD call counts as a new
 // aircraft here, while the reference's id-keyed sets would match it.
-// One rank only: with several ranks the row partition would move rows (and
-// their bookkeeping) between GPUs; re-init the sim there.
+// Several ranks: every rank completes its replicas first, the change is the
+// same computation everywhere, and the rows (with their bookkeeping) are
+// re-partitioned over the new n (multi_begin / multi_end below).
 #include <algorithm>
 #include <vector>
 
@@ -607,6 +608,9 @@ int bsa_sim_create(bsa_ctx *cc, int64_t m, const bsa_sim_state *s) {
     }
   }
   bsa::set_n(c, nn);
+  // the new aircraft's gseast / gsnorth are the host's (numpy's sin / cos), not
+  // K4's expressions of their gs / trk: the halo sends them until K4' has run
+  c->sim_gs_derivable = false;
   // the new aircraft take the homes after the existing ones, in index order
   for (int64_t k = n; k < nn; ++k) c->h2id_h.push_back((unsigned)k);
   if (bsa::set_home_maps(c)) return -1;

@@ -118,7 +118,7 @@ class ResidentSim:
 
     def create(self, state):
         """Append aircraft (Traffic.create; ``state`` as ``initial_state`` returns,
-        m long each): indices n..n+m-1 (bsa_sim_create, one rank)."""
+        m long each): indices n..n+m-1 (bsa_sim_create; collective with several ranks)."""
         self.ctx.sim_create(state)
 
     def delete(self, idx):

@@ -44,9 +44,10 @@ def run_ranks(world, fn, timeout=240):
             c.close()
         group.close()
     assert not any(alive), 'rank threads hung'
-    for e in err:
-        if e is not None:
-            raise e
+    errs = [e for e in err if e is not None]
+    if errs:   # a rank's own failure, not the barrier timeout it left the others in
+        first = [e for e in errs if 'barrier' not in str(e)] or errs
+        raise AssertionError('rank errors: %s' % ['%d: %r' % (r, e) for r, e in enumerate(err) if e]) from first[0]
     return out
 
 
@@ -364,3 +365,77 @@ def test_halo_probe_shares_equal_full_detect(ctx):
             assert np.array_equal(np.concatenate([p[f] for p in parts])[o], full[f]), f
     assert sum(int(p['inconf'].sum()) for p in parts) == int(full['inconf'].sum())
     assert sim.stats()['steps'] == 0
+
+
+# ---------------------------------------------------------------- create / delete while sharded
+def test_sharded_create_delete_equal_world1(ctx):
+    """Traffic.delete / create during a sharded run (traffic.py:192-378,
+    trafficarrays.py:73-118): 3 ranks delete 10 % of the aircraft -- intruders
+    of live resopairs among them, so dangling pairs cross ranks -- and later
+    create 90; the home ranges are re-partitioned and the bookkeeping rows move
+    with their aircraft.  State, pair lists, resopairs and the global counts
+    stay bitwise equal to the one-rank run at every step."""
+    t = synth.box(3000, 100.0, seed=89)
+    p = resident.params(simdt=2.0, resume_nav=True)
+    rng = np.random.default_rng(89)
+    new = resident.initial_state(synth.box(90, 100.0, seed=90))
+    plan = {}
+
+    def between(k, sim):
+        if k == 3:
+            if 'gone' not in plan:     # the one-rank run goes first: intruders of its resopairs
+                _, j = sim.resopairs()
+                plan['gone'] = np.unique(np.concatenate([rng.choice(j, min(40, len(j)), replace=False),
+                                                         rng.choice(t.ntraf, 260, replace=False)]))
+            sim.delete(plan['gone'])
+        if k == 5:
+            sim.create(new)
+
+    halo, exp = sharded_vs_world1(ctx, t, p, 3, 9, between=between, resume_nav=True)
+    assert len(exp[-1]['state']['lat']) == t.ntraf - len(plan['gone']) + 90
+    assert exp[3]['bk']['resopairs'] > 0
+
+
+def test_sharded_trace_super8del_equal_world1(ctx):
+    """The reference's own DEL / CRE trace (tests/golden/trace_super8del.npz)
+    replayed through the resident step at world 2 equals world 1 bitwise:
+    state, resopairs, the four counts and asas.active after every call."""
+    from tests import util
+    from tests.test_gpu_trace import sim_state
+    from tests.test_oracle_trace import traffic_change
+    st, calls = util.load_trace(util.golden('trace_super8del.npz')[0])
+    p = resident.params(rpz=float(st['rpz']), hpz=float(st['hpz']), tla=float(st['tla']), mar=float(st['mar']),
+                        reso=True, swresohoriz=bool(st['swresohoriz']), swresospd=bool(st['swresospd']),
+                        swresohdg=bool(st['swresohdg']), swresovert=bool(st['swresovert']),
+                        resume_nav=True, simdt=0.05)
+
+    def replay(sim):
+        out = []
+        for c, r in enumerate(calls):
+            n = len(r['lat'])
+            if c and 'ids' in r:
+                deleted, created = traffic_change(calls[c - 1]['ids'], r['ids'])
+                if deleted:
+                    sim.delete(deleted)
+                if created:
+                    sim.create(sim_state(r, slice(n - created, n)))
+            sim.update(lat=r['lat'], lon=r['lon'], trk=r['trk'], gs=r['gs'], alt=r['alt'], vs=r['vs'],
+                       tas=r['tas'], gseast=r['gseast'], gsnorth=r['gsnorth'], selalt=r['selalt'],
+                       ap_vs=r['apvs'], ap_trk=r['aptrk'], ap_tas=r['aptas'], ap_alt=r['apalt'])
+            sim.step(1)
+            i, j = sim.resopairs()
+            out.append((sim.read(), sim.asas_stats(), list(zip(i.tolist(), j.tolist()))))
+        return out
+
+    init = sim_state(calls[0], slice(None))
+    exp = replay(resident.ResidentSim(init, p, ctx=ctx))
+    res = run_ranks(2, lambda r, c, g: replay(resident.ResidentSim(init, p, ctx=c, rank=r, world=2, group=g)))
+    for k, (est, ebk, ereso) in enumerate(exp):
+        for f, v in est.items():
+            for r in range(2):
+                assert np.array_equal(res[r][k][0][f], v), 'call %d rank %d %s' % (k, r, f)
+        assert sorted(res[0][k][2] + res[1][k][2]) == sorted(ereso), k
+        for r in range(2):
+            for f in ('confpairs_unique', 'lospairs_unique', 'confpairs_all', 'lospairs_all'):
+                assert res[r][k][1][f] == ebk[f], (k, r, f)
+    assert any(len(x[2]) for x in exp)
