@@ -581,29 +581,32 @@ __device__ __forceinline__ unsigned wave_incl_scan(unsigned x) {
 // MI355X_MICROARCH 'dequeue').
 constexpr int kTPThreads = 1024;
 constexpr int kSuper = 8;  // tiles per super tile (each side)
-__device__ __forceinline__ uint2 tile_at(const uint2 *__restrict__ list, unsigned long long k,
-                                         unsigned long long near, unsigned long long cap) {
-  return list[k < near ? k : cap - 1 - (k - near)];
-}
+constexpr int kSlicesPerTile = kTile / kGroup;  // 64-row slices (work items) per row tile
+static_assert(kSlicesPerTile == 8, "8 slices per tile (item bit layout, slice boxes = group boxes)");
 // present (halo mode, nullable): column tiles whose data this rank holds --
 // its own [p0, p1) and the halo tiles it received.  A kept pair with any
 // other column tile means the halo plan disagreed with this test (it cannot:
 // the plan runs the same boxes_may_interact on the same boxes): it is flagged
 // (cnt->halo_miss, the step fails loudly), never silently dropped or swept.
-__global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, const TileBox *__restrict__ rb,
+__global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, int nrows, const TileBox *__restrict__ rb,
+                                                          const TileBox *__restrict__ rg,
                                                           const TileBox *__restrict__ cb, int noprune,
                                                           uint2 *__restrict__ out, unsigned long long cap,
                                                           Counters *__restrict__ cnt,
+                                                          unsigned long long *__restrict__ icnt,
                                                           const unsigned *__restrict__ build,
                                                           const uint8_t *__restrict__ present, int p0, int p1) {
   if (build && !build[0]) return;
-  __shared__ TileBox srt[kSuper];            // this super row's tile boxes
+  __shared__ TileBox srt[kSuper];                    // this super row's tile boxes
+  __shared__ TileBox sgb[kSuper * kSlicesPerTile];   // ... and its 64-row slices' boxes
   __shared__ unsigned keep[kTPThreads];      // kept super columns of the chunk
-  __shared__ unsigned wpre[3][kTPThreads / 64];
+  __shared__ unsigned wpre[4][kTPThreads / 64];
   __shared__ unsigned long long bbase[2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int rt0 = blockIdx.x * kSuper, nr = min(kSuper, nrt - rt0);
   if (threadIdx.x < nr) srt[threadIdx.x] = rb[rt0 + threadIdx.x];
+  if (threadIdx.x < nr * kSlicesPerTile && rt0 * kTile + (int)threadIdx.x * kGroup < nrows)
+    sgb[threadIdx.x] = rg[rt0 * kSlicesPerTile + threadIdx.x];
   __syncthreads();
   TileBox sr = srt[0];
   for (int i = 1; i < nr; ++i) sr = box_union(sr, srt[i]);
@@ -634,6 +637,7 @@ __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, cons
       const unsigned e = e0 + threadIdx.x;
       bool kn = false, kf = false;
       int rt = 0, ct = 0;
+      unsigned sm = 0;  // slices of row tile rt whose boxes may interact with column tile ct
       if (e < ne) {
         const unsigned sc2 = keep[e / (kSuper * kSuper)], r = e % (kSuper * kSuper);
         const int i = (int)(r / kSuper);
@@ -649,33 +653,56 @@ __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, cons
                               gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]) == 0.f;
             kn = near;
             kf = !near;
+            for (int q = 0; q < kSlicesPerTile; ++q)
+              if (rt * kTile + q * kGroup < nrows && (noprune || boxes_may_interact(sgb[i * kSlicesPerTile + q], b)))
+                sm |= 1u << q;
           }
         }
       }
-      const unsigned xn = wave_incl_scan(kn ? 1u : 0u), xf = wave_incl_scan(kf ? 1u : 0u);
+      // items (the pair's slices) of each class, and the tile pairs themselves
+      const unsigned ni = (unsigned)__popc(sm);
+      const unsigned xn = wave_incl_scan(kn ? ni : 0u), xf = wave_incl_scan(kf ? ni : 0u);
+      const unsigned tw = (unsigned)__popcll(__ballot(kn)) | (unsigned)__popcll(__ballot(kf)) << 16;
       if (lane == 63) {
         wpre[0][w] = xn;
         wpre[1][w] = xf;
+        wpre[3][w] = tw;
       }
       __syncthreads();
       if (threadIdx.x < 2) {
-        unsigned run = 0;
+        unsigned run = 0, tiles = 0;
         for (int q = 0; q < kTPThreads / 64; ++q) {
           const unsigned v = wpre[threadIdx.x][q];
           wpre[threadIdx.x][q] = run;
           run += v;
+          tiles += (wpre[3][q] >> (16 * threadIdx.x)) & 0xffffu;
         }
-        unsigned long long *ctr = threadIdx.x == 0 ? &cnt->tiles_near : &cnt->pad[0];
-        bbase[threadIdx.x] = run ? atomicAdd(ctr, (unsigned long long)run) : 0ull;
-        if (run) atomicAdd(&cnt->tiles, (unsigned long long)run);
+        bbase[threadIdx.x] = run ? atomicAdd(&icnt[1 + threadIdx.x], (unsigned long long)run) : 0ull;
+        if (tiles) {
+          atomicAdd(&cnt->tiles, (unsigned long long)tiles);
+          if (threadIdx.x == 0) atomicAdd(&cnt->tiles_near, (unsigned long long)tiles);
+        }
       }
       __syncthreads();
-      const uint2 v = make_uint2((unsigned)rt, (unsigned)ct);
-      if (kn) out[bbase[0] + wpre[0][w] + xn - 1] = v;
-      if (kf) out[cap - 1 - (bbase[1] + wpre[1][w] + xf - 1)] = v;
+      if (ni) {  // item = (row tile | slice << 22, column tile); near ones from the front
+        unsigned long long k = (kn ? bbase[0] + wpre[0][w] + xn : bbase[1] + wpre[1][w] + xf) - ni;
+        for (unsigned m = sm; m; m &= m - 1u, ++k) {
+          const uint2 v = make_uint2((unsigned)rt | (unsigned)__builtin_ctz(m) << 22, (unsigned)ct);
+          out[kn ? k : cap - 1 - k] = v;
+        }
+      }
       __syncthreads();  // wpre / bbase are rewritten by the next round
     }
   }
+}
+
+__device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned lane_prefix(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
 // ------------------------------------------------------------------ K1a prefilter
@@ -697,14 +724,6 @@ constexpr float kEABS = 50.f;      // absolute position error budget [m]
 // projection errors are inside s's 1e-6 chord margin) total < 2e-7.
 constexpr float kPlaneMargin = 4e-7f;
 
-__device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long v) {
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return ((unsigned long long)hi << 32) | lo;
-}
-__device__ __forceinline__ unsigned lane_prefix(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-}
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 // stage 2: conservative closest-approach refine of one (row, column) pair.
@@ -769,8 +788,7 @@ constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 // Work distribution knob of the sweep (BSA_PF_SHARDS overrides it for
 // measurements; results never depend on it)
 struct PfKnobs {
-  int shards;  // dequeue counters in use (power of two <= kWorkShards)
-  int pieces;  // work items per (tile pair, 64-row slice): 1, 2, 4 (or 8, BSA_PF_PIECES)
+  int pieces;  // units per item (tile pair, 64-row slice): 1, 2, 4 (or 8, BSA_PF_PIECES)
 };
 #ifndef BSA_PF_WAVES_PER_EU
 #define BSA_PF_WAVES_PER_EU 4
@@ -843,7 +861,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const PFRec *__restrict__ prow, const PFVel *__restrict__ vrow, const float4 *__restrict__ pprow, int nrows,
     const PFRec *__restrict__ pcol, const PFVel *__restrict__ vcol, const float4 *__restrict__ ppcol, int ncols,
     const TileBox *__restrict__ gbox_r, const TileBox *__restrict__ sbox_c, int noprune,
-    const uint2 *__restrict__ tiles, unsigned long long tcap,
+    const uint2 *__restrict__ items, unsigned long long icap,
     Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
     uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn) {
@@ -860,7 +878,6 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ unsigned char sgs[PF_WAVES][kSubsPerBatch];  // the next batch's sub-groups (tile-local)
   if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const unsigned long long ntiles = cnt->tiles, near = cnt->tiles_near;
   unsigned short *q1 = q1s[w];
   unsigned fb = 0;           // fill buffer of q2 (wave-uniform)
   uint2 *q2 = q2s[w][0];
@@ -876,32 +893,33 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   unsigned n2 = 0;        // wave-uniform
   unsigned subs = 0;      // 8-column sub-groups swept by this wave (for the roofline)
   const float qnan = __builtin_nanf("");
-  // Dynamic work distribution: an item is one (tile pair, 64-row slice); each
-  // wave dequeues items from the counter of its shard (blockIdx % shards,
-  // 128 B apart; a returning atomic on one word saturates at ~88 per us).
-  // Near tile pairs (the costly ones) come first in the list.  An item's
-  // sub-group mask is formed as it starts (below).  (Measured slower: claiming the next item ahead (+20 us, also
-  // without spills: a returning atomic in flight joins every later in-order
-  // vmcnt wait, so its latency is moved, not hidden); several items per
-  // dequeue, or PF_GROUP consecutive tile pairs of one slice per item sharing
-  // the row setup, with the next pair's first batch prefetched (+10 / +30 /
-  // +90 us at 2 / 4 / 8: fewer, longer items balance worse); stealing items
-  // from other shards once a wave's shard is dry (+130 us: the drained shards'
-  // counters are hammered by failing returning atomics).)
-  // Item numbering: the low 3 bits of an item id pick the tile pair within a
-  // group of 8 consecutive tile pairs, the next 3 the 64-row slice.  Shard =
-  // item id mod shards and workgroups go to the XCDs round-robin (blockIdx % 8),
-  // so ONE XCD sweeps all 8 slices of a tile pair, close together in time: the
-  // column tile is fetched into that XCD's L2 once instead of into all eight.
-  static_assert(PF_ITEMS_PER_TILE == 8, "item id layout: 3 bits of slice");
-  // pieces > 1: an item's column mask is split into that many pieces, each a
-  // work item of its own, piece p taking the set bits of rank p mod pieces (an
-  // equal share of the sub-groups; contiguous quarters of the mask were uneven
-  // where the dense columns bunch) -- the densest items, 60-85 us each, set the
-  // sweep's span otherwise (tools/pf_trace.py: at the 100k box the last item
-  // starts at 67 us of 97); empty pieces are skipped like empty items
-  const unsigned long long nitems = ((ntiles + 7) / 8) * 64 * (unsigned)kn.pieces;
-  const unsigned shard = blockIdx.x & (kn.shards - 1);
+  // Dynamic work distribution: an item is one (tile pair, 64-row slice) that
+  // K0d listed (the slice's box may reach the column tile's: at the 100k box
+  // 44 % of the 8 x 3 642 slices do not, and each cost its wave a dequeue ->
+  // tile -> box-load chain when all were numbered implicitly), split into
+  // `pieces` units; each wave dequeues units from the counter of its shard
+  // (blockIdx % 32, 128 B apart; a returning atomic on one word saturates at
+  // ~88 per us).  Near tile pairs (the costly ones) come first in the list.  A
+  // unit's sub-group mask is formed as it starts (below).  (Measured slower:
+  // claiming the next item ahead (+20 us, also without spills: a returning
+  // atomic in flight joins every later in-order vmcnt wait, so its latency is
+  // moved, not hidden); several items per dequeue, or PF_GROUP consecutive tile
+  // pairs of one slice per item sharing the row setup, with the next pair's
+  // first batch prefetched (+10 / +30 / +90 us at 2 / 4 / 8: fewer, longer
+  // items balance worse); stealing items from other shards once a wave's shard
+  // is dry (+130 us: the drained shards' counters are hammered by failing
+  // returning atomics); a separate K0e launch listing only the items with a
+  // non-empty sub-group mask, dense ones split further (-8 us of sweep, but the
+  // launch's cold dependent loads took 13 us).)
+  // pieces > 1: a unit takes the set bits of rank p mod pieces of its item's
+  // column mask (an equal share of the sub-groups; contiguous quarters of the
+  // mask were uneven where the dense columns bunch) -- the densest items, 60-85
+  // us each, set the sweep's span otherwise (tools/pf_trace.py); empty pieces
+  // are skipped
+  // K0d's items (complete before this launch): near ones from the front of
+  // the list, the others from its back; each is `pieces` units
+  const unsigned long long inear = work[1], nunits = (work[1] + work[2]) * (unsigned)kn.pieces;
+  const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
   // its own counter (spreads the flush atomics over kCandShards addresses)
@@ -942,40 +960,41 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     {
       unsigned long long m0 = 0;
       if (lane == 0) m0 = atomicAdd(wq, 1ull);
-      item = wave_bcast_u64(m0) * kn.shards + shard;
+      item = wave_bcast_u64(m0);
     }
-    if (item >= nitems) break;
+    // the unit of the shard's item-th dequeue: blocks of 8 consecutive units, 4
+    // consecutive blocks to the 4 shards of one XCD (shard & 7 = the XCD of its
+    // workgroups), so the items of a tile pair -- consecutive in the list -- are
+    // swept on one XCD, close together in time: the column tile enters one L2
+    item = (((item >> 3) * kWorkShards + 4 * (shard & 7) + (shard >> 3)) << 3) | (item & 7ull);
+    if (item >= nunits) break;
 #ifdef BSA_PF_TRACE
     const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
     unsigned tr_subs = 0;
 #endif
     do {  // one item; `break` ends it
-#ifndef PF_XCD_ITEMS
-#define PF_XCD_ITEMS 1
-#endif
-    const unsigned piece = (unsigned)((item >> 3) % (unsigned)kn.pieces);
-    const unsigned long long it = (item & 7ull) | ((item >> 3) / (unsigned)kn.pieces) << 3;
-    const unsigned long long tp = PF_XCD_ITEMS ? (it & 7ull) + ((it >> 6) << 3) : it >> 3;
-    const unsigned slice = PF_XCD_ITEMS ? (unsigned)(it >> 3) & 7u : (unsigned)it & 7u;
-    if (tp >= ntiles) break;
-    const uint2 rc = tile_at(tiles, tp, near, tcap);
-    const int rbase = (int)rc.x * kTile + (int)slice * PF_WROWS;
-    if (rbase >= nrows) break;
-    const int cbase = (int)rc.y * kTile;
+    // the item: (row tile | slice << 22, column tile)
+    const unsigned piece = (unsigned)(item % (unsigned)kn.pieces);
+    const unsigned long long e = item / (unsigned)kn.pieces;
+    const uint2 it = items[e < inear ? e : icap - 1 - (e - inear)];
+    const uint2 rc = make_uint2(it.x & 0x3fffffu, it.y);
+    const unsigned slice = it.x >> 22;
     // column sub-groups of this tile that may interact with the wave's row box:
     // the stage-1 test on box gaps (one sub-group box per lane), evaluated as
-    // the item starts -- its two box loads are as deep as the mask load of a
-    // separate K0e launch was, and the launch is saved
+    // the item starts
     unsigned long long gm;
     {
-      const int nsub = min(kSubsPerTile, (ncols - cbase + kSub - 1) / kSub);
+      const int cb = (int)rc.y * kTile;
+      const int nsub = min(kSubsPerTile, (ncols - cb + kSub - 1) / kSub);
       const int sg = min(lane, nsub - 1);
-      const TileBox sb = sbox_c[cbase / kSub + sg];
+      const TileBox sb = sbox_c[cb / kSub + sg];
       const TileBox rg = gbox_r[((int)rc.x * kTile) / kGroup + (int)slice];
       gm = __ballot(lane < nsub && (noprune || boxes_may_interact(rg, sb)));
     }
     if (kn.pieces > 1)  // piece p: the set bits of rank p, p + pieces, ... (equal shares of a dense mask)
       gm = __ballot(((gm >> lane) & 1ull) && (lane_prefix(gm) & (unsigned)(kn.pieces - 1)) == piece);
+    const int rbase = (int)rc.x * kTile + (int)slice * PF_WROWS;
+    const int cbase = (int)rc.y * kTile;
     if (!gm) break;
     subs += (unsigned)__popcll(gm);
 #ifdef BSA_PF_TRACE
@@ -2066,7 +2085,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (!ensure(c, c->tbox_c, nct * sizeof(TileBox), "column tile boxes") ||
       !ensure(c, c->gbox_c, ngc * sizeof(TileBox), "column group boxes") ||
       !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
-      !ensure(c, c->tilepairs, (size_t)ntp * sizeof(uint2), "tile pairs"))
+      !ensure(c, c->tilepairs, (size_t)ntp * kSlicesPerTile * sizeof(uint2), "prefilter items"))
     return -1;
   FusedBoxes fb{nullptr, nullptr, nullptr};
   ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -2106,11 +2125,12 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     hipLaunchKernelGGL(k_boxes, dim3(nct), dim3(kTile), 0, c->stream, (int)n, (const PFRec *)c->pfcol.p,
                        (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
   // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
+  const unsigned long long icap = (unsigned long long)ntp * kSlicesPerTile;  // items: 8 slices per tile pair
   hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
-                     nrt, nct, tbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
-                     (unsigned long long)ntp, dcnt, build, halo ? halo_present(c) : nullptr, a0, a1);
+                     nrt, nct, (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune,
+                     (uint2 *)c->tilepairs.p, icap, dcnt, (unsigned long long *)c->workq.p, build,
+                     halo ? halo_present(c) : nullptr, a0, a1);
   BSA_HIP(c, hipGetLastError());
-  // (K0e, an item's column sub-group mask, is evaluated by K1a as the item starts)
   if (mark(1)) return -1;
 
   const float T = (float)(tla > 0.0 ? tla : 0.0);
@@ -2118,16 +2138,10 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : lim * lim};
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
-  static const PfKnobs kn0 = [] {
-    const char *v = getenv("BSA_PF_SHARDS");
-    PfKnobs z{v ? atoi(v) : kWorkShards, 1};
-    if (z.shards < 1 || z.shards > kWorkShards || (z.shards & (z.shards - 1))) z.shards = kWorkShards;
-    return z;
-  }();
   // pieces: ~8 items per row tile, a few hundred row tiles fill the waves;
   // fewer rows split the items (BSA_PF_PIECES overrides)
   static const int pieces_env = getenv("BSA_PF_PIECES") ? atoi(getenv("BSA_PF_PIECES")) : 0;
-  PfKnobs kn = kn0;
+  PfKnobs kn{1};
   // (measured, tools/gpu_pieces.sh: 2 pieces at the 100k box, 102 -> 97 us; 4 for
   // one rank of 8 there, 36 -> 29 us; 2 at 125k rows of 1M, 65 -> 53 us; 1
   // from 250k rows up, where 2 cost +15 us)
@@ -2151,13 +2165,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     hipLaunchKernelGGL(k_prefilter<true>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
-                       (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt,
+                       (const uint2 *)c->tilepairs.p, icap, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
-                       (const uint2 *)c->tilepairs.p, (unsigned long long)ntp, dcnt,
+                       (const uint2 *)c->tilepairs.p, icap, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;

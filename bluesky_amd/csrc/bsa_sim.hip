@@ -593,15 +593,22 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     while (c->sim_steps < target) {
       if (c->sim_steps % c->simp.cd_every == 0)
         if (bsa::sim_cd(c, true)) return -1;
-      const int64_t nb = std::max<int64_t>(1, (re - rb + 255) / 256);
+      // K4' workgroup size: one wave (at 100k rows 256-lane groups left half the
+      // CUs one group short, 391 groups on 256 CUs: 0.1753 -> 0.1718 ms per
+      // step with 64; BSA_K4_BLOCK=128/256 for A/B)
+      static const int k4b = [] {
+        const int v = getenv("BSA_K4_BLOCK") ? atoi(getenv("BSA_K4_BLOCK")) : 64;
+        return (v == 64 || v == 128 || v == 256) ? v : 64;
+      }();
+      const int64_t nb = std::max<int64_t>(1, (re - rb + k4b - 1) / k4b);
       bsa::MvpIn mv{};
       if (c->mvp_deferred) memcpy(&mv, c->mvp_defer.data(), sizeof(mv));
       if (c->mvp_deferred)
-        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<true>, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb,
+        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<true>, dim3((unsigned)nb), dim3(k4b), 0, c->stream, (int)rb,
                            (int)re, c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
                            bsa::wind_field(c), bsa::sim_dev(c), mv, c->simp.mvp);
       else
-        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<false>, dim3((unsigned)nb), dim3(256), 0, c->stream, (int)rb,
+        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<false>, dim3((unsigned)nb), dim3(k4b), 0, c->stream, (int)rb,
                            (int)re, c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
                            bsa::wind_field(c), bsa::sim_dev(c), mv, c->simp.mvp);
       c->mvp_deferred = false;
