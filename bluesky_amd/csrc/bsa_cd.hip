@@ -27,6 +27,7 @@
 
 #include "bsa_box.h"
 #include "bsa_geo_math.h"
+#include "bsa_halo.h"
 #include "bsa_internal.h"
 #include "bsa_mvp_math.h"
 
@@ -272,14 +273,20 @@ struct ZeroArgs {
   unsigned char *inconf;
   unsigned long long *tcpamax;
   unsigned *rowcnt;
+  unsigned *x[3];  // more word regions to zero (the halo plan's buffers: HaloPre), or NULL
+  int xn[3];
 };
 __device__ __forceinline__ bool list_word(int k);
 __device__ __forceinline__ void zero_state(const ZeroArgs &z, int t, int nt) {
   constexpr int kWords = (int)(sizeof(Counters) / 8);
   constexpr int kTilesWord = (int)(offsetof(Counters, tiles) / 8);
   constexpr int kNearWord = (int)(offsetof(Counters, tiles_near) / 8);
-  const int m = max(max(2 * (z.nrows + 1), kWorkShards * kWorkStride), kWords);
+  const int m = max(max(max(2 * (z.nrows + 1), kWorkShards * kWorkStride), kWords),
+                    max(max(z.xn[0], z.xn[1]), z.xn[2]));
   for (int k = t; k < m; k += nt) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+      if (k < z.xn[r]) z.x[r][k] = 0u;
     if (k < kWords && (z.full || (k != kTilesWord && k != kNearWord)) && !(z.keep && list_word(k)))
       reinterpret_cast<unsigned long long *>(z.cnt)[k] = 0;
     if (k < kWorkShards * kWorkStride) z.work[k] = 0;
@@ -299,6 +306,8 @@ __device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__res
 // are one tile, so the boxes are reduced right after the records are written.
 struct FusedBoxes {
   TileBox *sbox, *gbox, *tbox;  // gbox == nullptr: not fused (k_boxes runs)
+  TileBox *blk;                 // halo exchange: tile boxes also into the block sent (blk[tile - blk_base])
+  int blk_base;
 };
 
 // fp64 column record of aircraft o: intruder[o] geometry, own[o] velocity /
@@ -339,11 +348,15 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
                                                      ColRec *__restrict__ C, PFRec *__restrict__ PC,
                                                      PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
                                                      ReuseParams rz, FusedBoxes fb, ZeroArgs zs, int tile_base,
-                                                     const int *__restrict__ tile_list) {
+                                                     const int *__restrict__ tile_list, HaloUnpack hu,
+                                                     Counters *__restrict__ hcnt) {
   __shared__ TileBox fgb[kTile / 64];
   // K0z (fused): nothing here reads that state
   if (zs.cnt) zero_state(zs, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
-  const int tile = tile_list ? tile_list[blockIdx.x] : tile_base + (int)blockIdx.x;
+  int tile = tile_list ? tile_list[blockIdx.x] : tile_base + (int)blockIdx.x;
+  // halo exchange: this slot's received tile rows first (each thread writes
+  // the row it prepares below), checked against this rank's plan
+  if (hu.rbuf) tile = halo_unpack_tile(hu, (int)blockIdx.x, tile, hcnt);
   if (tile < 0) return;  // (the whole workgroup: no barrier is skipped by part of it)
   const int k = tile * kTile + (int)threadIdx.x;
   bool over = false;       // reuse: this aircraft overran a budget
@@ -428,6 +441,7 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
   }
   // K0c (fused): this thread wrote PC[k] above, every thread reaches the barrier
   if (fb.gbox) tile_boxes(cnt, tile, PC, fgb, fb.sbox, fb.gbox, fb.tbox);
+  if (fb.blk && threadIdx.x == 0) fb.blk[tile - fb.blk_base] = fb.tbox[tile];  // (written by this thread)
 }
 
 // ------------------------------------------------------------------ K0c tile boxes
@@ -713,7 +727,7 @@ struct RefineParams {
   float R;      // rpz [m]
   float H;      // hpz [m]
   float T;      // max(tla, 0) [s]
-  float lim2;   // ((R + EABS) / (1 - E1))^2
+  float lim2;   // ((R + EABS) / (1 - E1) / R_S)^2 (unit-sphere units, as the refine's positions)
 };
 constexpr float kRS = 6371000.f;   // scale of the unit-sphere chord to metres
 constexpr float kE1 = 0.012f;      // bound on |log(reference dist / estimated dist)|
@@ -727,33 +741,40 @@ constexpr float kPlaneMargin = 4e-7f;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 // stage 2: conservative closest-approach refine of one (row, column) pair.
-// rp = (x, y, z, -) and rv = (u, v, vs, alt) of the row; cp = (x, y, z, -) and
-// cv = (u, v, vs, alt) of the column; u is NaN for an index that must never
-// be refined (quirk column, non-finite position, row within ~0.6 deg of a
-// pole), which keeps the pair through the `vv` test.  Returns false only
-// when no t in [0, max(tla,0)] can lie in both the vertical and the
-// horizontal window of the reference's geometry (DESIGN.md "CPA refine");
-// any NaN keeps the pair.
-__device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, const float4 &cp,
+// rp = (x, y, z, -) and rv = (u, v, vs, alt) of the row, rb = (x, y, rho, -)
+// / rho of its fp32 unit vector (its local east / north basis, staged once per
+// item); cp = (x, y, z, -) and cv = (u, v, vs, alt) of the column.  Positions
+// are unit-sphere chords, u / v are pre-scaled by 1 / R_S (kInvRS) to the
+// same units (times and the vertical terms are unchanged).  u is NaN for an
+// index that must never be refined (quirk column, non-finite position, row
+// within ~0.6 deg of a pole), which keeps the pair through the `vv` test.
+// Returns false only when no t in [0, max(tla,0)] can lie in both the
+// vertical and the horizontal window of the reference's geometry (DESIGN.md
+// "CPA refine"); any NaN keeps the pair.
+constexpr float kInvRS = 1.f / kRS;
+// far: keep without refining when the chord may exceed kRefineChord.  With
+// fp32 unit vectors (|c|^2, |r|^2 within 2e-7 of 1) and the dot product's
+// rounding (< 2e-7), chord^2 = |c|^2 + |r|^2 - 2 c.r <= 2 - 2 c.r + 1e-6, so
+// c.r >= 1 - (kRefineChord^2 - 2e-6) / 2 refines chords <= kRefineChord only.
+constexpr float kFarCos = (float)(1.0 - (kRefineChord * kRefineChord - 2e-6) / 2.0);
+__device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, const float4 &rb, const float4 &cp,
                                           const float4 &cv, const RefineParams &prm) {
   // Branch-free: every lane evaluates every test and the decision is one
   // select at the end -- the same values and the same keep / reject outcome as
   // testing them in order with early returns (far or clamped pairs are kept
   // whatever the rest says), without the exec-mask bookkeeping and the
   // per-branch LDS waits of the early-exit form.
-  const float dx = cp.x - rp.x, dy = cp.y - rp.y, dz = cp.z - rp.z;
-  const bool far = dx * dx + dy * dy + dz * dz > (float)(kRefineChord * kRefineChord);  // > ~190 km: keep
-  // chord projected on the row's local east / north basis
-  //   e = (-y, x, 0) / rho,  n = (-z x / rho, -z y / rho, rho),  rho = cos(lat)
-  // (from the fp32 unit vector; |lat| > ~89.4 deg rows are flagged)
-  const float rho2 = rp.x * rp.x + rp.y * rp.y;
-  const float irho = __builtin_amdgcn_rsqf(rho2);
-  const float rho = rho2 * irho;
-  const float pe = (dy * rp.x - dx * rp.y) * irho * kRS;
-  const float pn = (dz * rho - rp.z * (dx * rp.x + dy * rp.y) * irho) * kRS;
-  const float ve = cv.x - rv.x, vn = cv.y - rv.y;          // own.u[j] - int.u[i]
+  const bool far = cp.x * rp.x + cp.y * rp.y + cp.z * rp.z < kFarCos;  // > ~190 km: keep
+  // the chord projected on the row's local east / north basis
+  //   e = (-y, x, 0) / rho,  n = (-z x / rho, -z y / rho, rho),  rho = cos(lat):
+  // e.r = n.r = 0, so (c - r).e = c.e and (c - r).n = c.n -- no difference
+  // vector, and the per-row basis comes from LDS (|c.e|, |c.n| rounding < 5e-7,
+  // ~3 m, inside kEABS)
+  const float pe = cp.y * rb.x - cp.x * rb.y;
+  const float pn = cp.z * rb.z - rp.z * (cp.x * rb.x + cp.y * rb.y);
+  const float ve = cv.x - rv.x, vn = cv.y - rv.y;          // (own.u[j] - int.u[i]) / R_S
   const float vv = ve * ve + vn * vn;
-  const bool clamp = !(vv >= 4e-6f);                       // reference may clamp dv2; NaN
+  const bool clamp = !(vv >= 4e-6f * kInvRS * kInvRS);     // reference may clamp dv2; NaN
   const float dalt = cv.w - rv.w;                          // own.alt[j] - int.alt[i]
   const float H = prm.H + (rp.w + cp.w);                   // + vertical budgets (reuse; else 0)
   const float dvs = cv.z - rv.z;
@@ -789,6 +810,7 @@ constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 // measurements; results never depend on it)
 struct PfKnobs {
   int pieces;  // units per item (tile pair, 64-row slice): 1, 2, 4 (or 8, BSA_PF_PIECES)
+  int pnear;   // ... per near item (the pair's boxes overlap: the densest items)
 };
 #ifndef BSA_PF_WAVES_PER_EU
 #define BSA_PF_WAVES_PER_EU 4
@@ -875,6 +897,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ unsigned cix[PF_WAVES][64];    //                      sorted column index
   __shared__ float4 rsv[PF_WAVES][PF_WROWS];  // staged rows:       u v vs alt    (refine)
   __shared__ float4 rsp[PF_WAVES][PF_WROWS];  //                    x y z sigma   (refine)
+  __shared__ float4 rbs[PF_WAVES][PF_WROWS];  //                    x/rho y/rho rho - (refine basis)
   __shared__ unsigned char sgs[PF_WAVES][kSubsPerBatch];  // the next batch's sub-groups (tile-local)
   if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -918,7 +941,9 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // are skipped
   // K0d's items (complete before this launch): near ones from the front of
   // the list, the others from its back; each is `pieces` units
-  const unsigned long long inear = work[1], nunits = (work[1] + work[2]) * (unsigned)kn.pieces;
+  // near items take kn.pnear units each, the others kn.pieces
+  const unsigned long long inear = work[1], unear = inear * (unsigned)kn.pnear;
+  const unsigned long long nunits = unear + work[2] * (unsigned)kn.pieces;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
@@ -974,8 +999,11 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 #endif
     do {  // one item; `break` ends it
     // the item: (row tile | slice << 22, column tile)
-    const unsigned piece = (unsigned)(item % (unsigned)kn.pieces);
-    const unsigned long long e = item / (unsigned)kn.pieces;
+    const bool inr = item < unear;
+    const unsigned npc = (unsigned)(inr ? kn.pnear : kn.pieces);
+    const unsigned long long ui = inr ? item : item - unear;
+    const unsigned piece = (unsigned)(ui % npc);
+    const unsigned long long e = inr ? ui / npc : inear + ui / npc;
     const uint2 it = items[e < inear ? e : icap - 1 - (e - inear)];
     const uint2 rc = make_uint2(it.x & 0x3fffffu, it.y);
     const unsigned slice = it.x >> 22;
@@ -991,8 +1019,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       const TileBox rg = gbox_r[((int)rc.x * kTile) / kGroup + (int)slice];
       gm = __ballot(lane < nsub && (noprune || boxes_may_interact(rg, sb)));
     }
-    if (kn.pieces > 1)  // piece p: the set bits of rank p, p + pieces, ... (equal shares of a dense mask)
-      gm = __ballot(((gm >> lane) & 1ull) && (lane_prefix(gm) & (unsigned)(kn.pieces - 1)) == piece);
+    if (npc > 1)  // piece p: the set bits of rank p, p + npc, ... (equal shares of a dense mask)
+      gm = __ballot(((gm >> lane) & 1ull) && (lane_prefix(gm) & (npc - 1u)) == piece);
     const int rbase = (int)rc.x * kTile + (int)slice * PF_WROWS;
     const int cbase = (int)rc.y * kTile;
     if (!gm) break;
@@ -1076,8 +1104,13 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     // the row of this lane for the refine (u = NaN: never refine), position at
     // t = 0 and vertical budget; read from LDS by the drain (a register
     // broadcast would make it wait for the in-flight batch prefetch)
-    rv[lane] = make_float4(AV.flags ? qnan : AV.u, AV.v, AV.vs, A.alt);
+    rv[lane] = make_float4(AV.flags ? qnan : AV.u * kInvRS, AV.v * kInvRS, AV.vs, A.alt);
     rsp[w][lane] = make_float4(AP.x, AP.y, AP.z, A.pad);
+    {  // the row's refine basis (rows within ~0.6 deg of a pole are flagged: u = NaN)
+      const float rho2 = AP.x * AP.x + AP.y * AP.y;
+      const float irho = __builtin_amdgcn_rsqf(rho2);
+      rbs[w][lane] = make_float4(AP.x * irho, AP.y * irho, rho2 * irho, 0.f);
+    }
     unsigned n1 = 0;                 // wave-uniform
     unsigned long long colmask = 0;  // valid slots of the swept batch
 
@@ -1097,7 +1130,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         if (k < n1) {
           gi = (unsigned)rbase + rl;
           gj = sci[cl];
-          keep = NOPRUNE ? true : pf_refine(rsp[w][rl], rv[rl], sx[cl], sv[cl], prm);
+          keep = NOPRUNE ? true : pf_refine(rsp[w][rl], rv[rl], rbs[w][rl], sx[cl], sv[cl], prm);
         }
         const unsigned long long mk = __ballot(keep);
         if (mk) {
@@ -1174,7 +1207,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         slh[pb] = nx.lo;
         slh[pb + 2] = nx.hi;
         sx[lane] = make_float4(np.x, np.y, np.z, nx.pad);
-        sv[lane] = make_float4(nv.flags ? qnan : nv.u, nv.v, nv.vs, nx.alt);
+        sv[lane] = make_float4(nv.flags ? qnan : nv.u * kInvRS, nv.v * kInvRS, nv.vs, nx.alt);
         sci[lane] = (unsigned)jn;
         colmask = __ballot(jn >= 0);
       }
@@ -1772,7 +1805,7 @@ __global__ __launch_bounds__(256) void k_zero(int nrows, int full, int keep, uns
     rctl[0] = rforce ? 1u : 0u;
     if (rforce) rctl[1] = 0u;
   }
-  zero_state(ZeroArgs{nrows, full, keep, cnt, work, inconf, tcpamax, rowcnt},
+  zero_state(ZeroArgs{nrows, full, keep, cnt, work, inconf, tcpamax, rowcnt, {}, {}},
              blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
 }
 
@@ -1866,12 +1899,12 @@ int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla) {
       !ensure(c, c->sbox_c, ((n + kSub - 1) / kSub) * sizeof(TileBox), "column sub-group boxes"))
     return -1;
   const SoA6 own = soa(c->own);
-  const FusedBoxes fb{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p};
-  const ZeroArgs zs{0, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const FusedBoxes fb{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, nullptr, 0};
+  const ZeroArgs zs{0, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
   hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)nct), dim3(kTile), 0, c->stream, (int)n,
                      (const unsigned *)c->h2id.p, 1, 0, own, own, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, stage1_mid(0, false, 0),
-                     ReuseParams{}, fb, zs, 0, (const int *)nullptr);
+                     ReuseParams{}, fb, zs, 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr);
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -1961,7 +1994,14 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   };
   if (n == 0 || nrows == 0) {
     if (zero(false, nullptr, 0)) return -1;
-    if (halo && halo_mid(c, rb, re)) return -1;  // a rank without rows still takes part in the exchange
+    if (halo) {  // a rank without rows still takes part in the exchange
+      HaloPre hp;
+      HaloUnpack hu;
+      if (halo_pre(c, rb, re, &hp)) return -1;
+      for (int r = 0; r < 3; ++r)
+        if (hp.zn[r]) BSA_HIP(c, hipMemsetAsync(hp.z[r], 0, (size_t)hp.zn[r] * 4, c->stream));
+      if (halo_mid(c, rb, re, &hu)) return -1;
+    }
     if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
     for (int e = 1; e < 5; ++e)
       if (mark(e)) return -1;
@@ -2087,27 +2127,35 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
       !ensure(c, c->tilepairs, (size_t)ntp * kSlicesPerTile * sizeof(uint2), "prefilter items"))
     return -1;
-  FusedBoxes fb{nullptr, nullptr, nullptr};
-  ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+  FusedBoxes fb{nullptr, nullptr, nullptr, nullptr, 0};
+  ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
+  // halo mode: the plan's buffers are zeroed and the own tile boxes written
+  // into the exchanged block by this K0b (no memset / copy launches)
+  HaloPre hp{};
+  if (halo && halo_pre(c, rb, re, &hp)) return -1;
   if (!reuse) {
-    fb = FusedBoxes{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p};
+    fb = FusedBoxes{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, hp.blk, hp.blk_base};
     zs = ZeroArgs{(int)nrows, 1, 0, dcnt, (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
-                  (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p};
+                  (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p, {hp.z[0], hp.z[1], hp.z[2]},
+                  {hp.zn[0], hp.zn[1], hp.zn[2]}};
   }
   hipLaunchKernelGGL(k_prep_cols, dim3(halo ? (unsigned)(a1 - a0) : blocks_for(n, kTile)), dim3(kTile), 0,
                      c->stream, (int)n, perm_c, home ? 1 : 0, recs ? 1 : 0, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs,
-                     halo ? a0 : 0, (const int *)nullptr);
+                     halo ? a0 : 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr);
   BSA_HIP(c, hipGetLastError());
   if (halo) {
-    if (halo_mid(c, rb, re)) return -1;
-    if (c->halo_hl > 0) {  // the received tiles' records and boxes (no per-detect zeroing here)
-      const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
+    HaloUnpack hu{};
+    if (halo_mid(c, rb, re, &hu)) return -1;
+    if (c->halo_hl > 0) {  // the received tiles: unpacked (exchange), records and boxes (no zeroing here)
+      const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
+      FusedBoxes fb2 = fb;
+      fb2.blk = nullptr;
       hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)c->halo_hl), dim3(kTile), 0, c->stream, (int)n, perm_c, 1,
                          recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
-                         (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs2, 0,
-                         (const int *)c->h_hl.p);
+                         (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, 0,
+                         (const int *)c->h_hl.p, hu, dcnt);
       BSA_HIP(c, hipGetLastError());
     }
   }
@@ -2135,18 +2183,22 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
 
   const float T = (float)(tla > 0.0 ? tla : 0.0);
   const float lim = (float)((rpz + kEABS + (reuse ? 2.0 * c->reuse_sh : 0.0)) / (1.0 - kE1));
-  const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : lim * lim};
+  const float liml = lim / kRS;  // unit-sphere units (pf_refine)
+  const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : liml * liml};
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
   // pieces: ~8 items per row tile, a few hundred row tiles fill the waves;
   // fewer rows split the items (BSA_PF_PIECES overrides)
   static const int pieces_env = getenv("BSA_PF_PIECES") ? atoi(getenv("BSA_PF_PIECES")) : 0;
-  PfKnobs kn{1};
+  PfKnobs kn{1, 1};
   // (measured, tools/gpu_pieces.sh: 2 pieces at the 100k box, 102 -> 97 us; 4 for
   // one rank of 8 there, 36 -> 29 us; 2 at 125k rows of 1M, 65 -> 53 us; 1
   // from 250k rows up, where 2 cost +15 us)
   kn.pieces = nrows >= 3 * (1 << 16) ? 1 : (nrows >= (1 << 15) ? 2 : 4);
   if (pieces_env == 1 || pieces_env == 2 || pieces_env == 4 || pieces_env == 8) kn.pieces = pieces_env;
+  static const int pnear_env = getenv("BSA_PF_PIECES_NEAR") ? atoi(getenv("BSA_PF_PIECES_NEAR")) : 0;
+  kn.pnear = kn.pieces;
+  if (pnear_env == 1 || pnear_env == 2 || pnear_env == 4 || pnear_env == 8) kn.pnear = pnear_env;
 #ifdef BSA_PF_TRACE
   {
     static DevBuf tb;

@@ -6,19 +6,23 @@
 // test (boxes_may_interact, bsa_box.h) against one of its row tiles, so
 // instead of all-gathering the whole state before every CD call (48 MB at 1M
 // aircraft) each rank
-//   1. prepares its OWN column tiles (K0b, with their boxes);
+//   1. prepares its OWN column tiles (K0b, with their boxes), which also
+//      zeroes the plan's buffers and writes its tile boxes into the block it
+//      sends (no memset / copy launches: every launch boundary costs ~4.5 us);
 //   2. all-gathers the tile boxes (48 B per tile) and a request bitmask of the
 //      tiles holding its resopairs' intruders (ResumeNav reads their state,
 //      asas.py:424-452, wherever they are by now);
-//   3. plans (k_halo_plan): tile t of rank s goes to rank q iff t passes the
-//      box test against some row tile of q, or q requested it -- every rank
-//      evaluates the same test on the same (gathered, bitwise) boxes from its
-//      own side, and the test is symmetric, so sender and receiver agree;
+//   3. plans (k_halo_plan + k_halo_lists): tile t of rank s goes to rank q iff
+//      t passes the box test against some row tile of q, or q requested it --
+//      every rank evaluates the same test on the same (gathered, bitwise) boxes
+//      from its own side, and the test is symmetric, so sender and receiver
+//      agree;
 //   4. exchanges the planned tiles' state (lat lon trk gs alt vs, and gseast /
 //      gsnorth unless they follow from gs / trk) with one grouped RCCL
 //      send / recv per neighbour (device copies in the in-process group),
 //      into the same home positions of the replicated arrays;
-//   5. prepares the received tiles (K0b over the flat halo list).
+//   5. unpacks and prepares the received tiles (one K0b over the flat halo
+//      list: each workgroup unpacks its tile's rows, then prepares them).
 // K0d (k_tilepairs) then lists tile pairs of present column tiles only; a
 // kept pair with a missing tile would be a plan bug and is flagged
 // (Counters::halo_miss: the step fails loudly), never swept with stale data.
@@ -38,29 +42,16 @@
 #include <algorithm>
 
 #include "bsa_box.h"
+#include "bsa_halo.h"
 #include "bsa_internal.h"
 
 #pragma clang fp contract(off)
 
 namespace bsa {
 
-constexpr int kHaloMaxRanks = 16;
-constexpr int kHaloMaxF = 8;  // fp64 arrays per halo row
-
-struct HaloCaps {
-  int scap[kHaloMaxRanks], rcap[kHaloMaxRanks];  // this rank's send / receive capacities [tiles]
-  int hoff[kHaloMaxRanks];                       // flat halo list offset of each source
-  unsigned long long soff[kHaloMaxRanks], roff[kHaloMaxRanks];  // region offsets in h_send / h_recv [B]
-};
-
-struct HaloFields {
-  double *f[kHaloMaxF];  // lat lon trk gs alt vs gseast gsnorth (home order, full n)
-  int nf;                // 6: gseast / gsnorth derived from gs / trk by the receiver
-};
-
-static inline __host__ __device__ size_t hdr_bytes(int cap) { return ((size_t)4 * (cap + 1) + 15) / 16 * 16; }
-static inline __host__ __device__ size_t tile_bytes(int nf) { return (size_t)nf * kTile * 8; }
-static inline size_t region_bytes(int cap, int nf) { return cap ? hdr_bytes(cap) + (size_t)cap * tile_bytes(nf) : 0; }
+static inline size_t region_bytes(int cap, int nf) {
+  return cap ? halo_hdr_bytes(cap) + (size_t)cap * halo_tile_bytes(nf) : 0;
+}
 
 // requests: the tiles of this rank's resopairs' intruders outside its own tiles
 __global__ __launch_bounds__(256) void k_halo_req(int nrows, const unsigned *__restrict__ rptr,
@@ -93,33 +84,6 @@ __device__ __forceinline__ const TileBox &plan_box(const PlanArgs &a, int t) {
 __device__ __forceinline__ bool req_bit(const PlanArgs &a, int q, int t) {
   const unsigned *w = reinterpret_cast<const unsigned *>(a.gblk + (size_t)q * a.bb + (size_t)a.tpr * sizeof(TileBox));
   return (w[t >> 5] >> (t & 31)) & 1u;
-}
-
-// blockIdx.y < na: own tile a0 + y (as K0d's row tile) against every other
-// tile t; blockIdx.y == na (exchange): this rank's requests, and the copy of
-// the gathered boxes into tbox_c for K0d
-__global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.nct || (t >= a.a0 && t < a.a1)) return;
-  const int na = a.a1 - a.a0, y = blockIdx.y;
-  if (y < na) {
-    if (boxes_may_interact(a.tbox[a.a0 + y], plan_box(a, t))) {
-      a.recv[t] = 1;
-      if (a.send) a.send[(size_t)(t / a.tpr) * a.tpr + y] = 1;
-    }
-    return;
-  }
-  a.tbox_out[t] = plan_box(a, t);
-  if (req_bit(a, a.me, t)) a.recv[t] = 1;
-}
-
-// the other ranks' requests for own tiles: thread = (rank q, own tile i)
-__global__ __launch_bounds__(256) void k_halo_plan_req(PlanArgs a) {
-  const int na = a.a1 - a.a0;
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= a.R * na) return;
-  const int q = x / na, i = x - q * na;
-  if (q != a.me && req_bit(a, q, a.a0 + i)) a.send[(size_t)q * a.tpr + i] = 1;
 }
 
 // ordered compaction of flag(0 .. m-1) by one 256-lane workgroup: f(index,
@@ -155,10 +119,9 @@ struct ListArgs {
   Counters *cnt;
 };
 
-// block q: the ordered list of own tiles rank q needs (into the header of the
-// send region for q) and of rank q's tiles this rank needs (into the flat list)
-__global__ __launch_bounds__(256) void k_halo_lists(ListArgs a, HaloCaps cp) {
-  const int q = blockIdx.x;
+// the ordered list of own tiles rank q needs (into the header of the send
+// region for q) and of rank q's tiles this rank needs (into the flat list)
+__device__ void halo_lists_q(const ListArgs &a, const HaloCaps &cp, int q) {
   if (q == a.me) return;
   const int na = a.a1 - a.a0;
   bool ovf = false;
@@ -184,7 +147,41 @@ __global__ __launch_bounds__(256) void k_halo_lists(ListArgs a, HaloCaps cp) {
     atomicAdd(&a.dem[2 * a.R], (unsigned)min(rc, cap));
     if (ovf || rc > cap) a.cnt->halo_ovf = 1;
   }
+  __syncthreads();  // block_compact's shared words are reused by the next q
 }
+
+// The plan.  blockIdx.y < ny: own tiles a0 + y, a0 + y + ny, ... (as K0d's
+// row tiles) against every other tile t = blockIdx.x * 256 + lane; y == ny
+// (exchange): this rank's requests, and the copy of the gathered boxes into
+// tbox_c for K0d; y == ny + 1 (exchange): the other ranks' requests for own
+// tiles.  (Ordering the lists in the last workgroup to finish, behind a
+// release fence per workgroup, took longer than the separate k_halo_lists
+// launch: 16.8 us against 4.5 + 4.4 at 1M, R = 8.)
+__global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a, int ny) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int na = a.a1 - a.a0, y = blockIdx.y;
+  if (y < ny) {
+    if (t < a.nct && !(t >= a.a0 && t < a.a1)) {
+      const TileBox b = plan_box(a, t);
+      for (int i = y; i < na; i += ny)
+        if (boxes_may_interact(a.tbox[a.a0 + i], b)) {
+          a.recv[t] = 1;
+          if (a.send) a.send[(size_t)(t / a.tpr) * a.tpr + i] = 1;
+        }
+    }
+  } else if (y == ny) {
+    if (a.gblk && t < a.nct && !(t >= a.a0 && t < a.a1)) {
+      a.tbox_out[t] = plan_box(a, t);
+      if (req_bit(a, a.me, t)) a.recv[t] = 1;
+    }
+  } else if (a.gblk && t < a.R * na) {  // y == ny + 1: thread = (rank q, own tile i)
+    const int q = t / na, i = t - q * na;
+    if (q != a.me && req_bit(a, q, a.a0 + i)) a.send[(size_t)q * a.tpr + i] = 1;
+  }
+}
+
+// block q: the lists of source / destination q (halo_lists_q)
+__global__ __launch_bounds__(256) void k_halo_lists(ListArgs a, HaloCaps cp) { halo_lists_q(a, cp, blockIdx.x); }
 
 // rows of the listed own tiles into the send regions: block (slot k, rank q)
 __global__ __launch_bounds__(kTile) void k_halo_pack(int n, int me, HaloFields fl, unsigned char *sbuf, HaloCaps cp) {
@@ -193,35 +190,8 @@ __global__ __launch_bounds__(kTile) void k_halo_pack(int n, int me, HaloFields f
   const unsigned *hdr = reinterpret_cast<const unsigned *>(sbuf + cp.soff[q]);
   if (k >= (int)hdr[0]) return;
   const int row = (int)hdr[1 + k] * kTile + (int)threadIdx.x;
-  double *dst = reinterpret_cast<double *>(sbuf + cp.soff[q] + hdr_bytes(cp.scap[q]) + (size_t)k * tile_bytes(fl.nf));
+  double *dst = reinterpret_cast<double *>(sbuf + cp.soff[q] + halo_hdr_bytes(cp.scap[q]) + (size_t)k * halo_tile_bytes(fl.nf));
   for (int f = 0; f < fl.nf; ++f) dst[f * kTile + threadIdx.x] = row < n ? fl.f[f][row] : 0.0;
-}
-
-// received regions -> the home positions of the replicated arrays; every slot
-// is checked against this rank's own plan (a disagreement sets halo_miss)
-__global__ __launch_bounds__(kTile) void k_halo_unpack(int n, int me, HaloFields fl, const unsigned char *rbuf,
-                                                       const int *__restrict__ hlist, HaloCaps cp,
-                                                       Counters *__restrict__ cnt) {
-  const int k = blockIdx.x, q = blockIdx.y;
-  if (q == me || k >= cp.rcap[q]) return;
-  const unsigned *hdr = reinterpret_cast<const unsigned *>(rbuf + cp.roff[q]);
-  const int got = k < (int)hdr[0] ? (int)hdr[1 + k] : -1;
-  const int want = hlist[cp.hoff[q] + k];
-  if (got != want) {
-    if (threadIdx.x == 0) cnt->halo_miss = 1;
-    return;
-  }
-  if (got < 0) return;
-  const int row = got * kTile + (int)threadIdx.x;
-  if (row >= n) return;
-  const double *src =
-      reinterpret_cast<const double *>(rbuf + cp.roff[q] + hdr_bytes(cp.rcap[q]) + (size_t)k * tile_bytes(fl.nf));
-  for (int f = 0; f < fl.nf; ++f) fl.f[f][row] = src[f * kTile + threadIdx.x];
-  if (fl.nf == 6) {  // K4' without wind: gseast / gsnorth = gs sin / cos(trk), bitwise the sender's
-    const double gs = fl.f[3][row], trk = fl.f[2][row];
-    fl.f[7][row] = gs * cos(trk * kD2R);
-    fl.f[6][row] = gs * sin(trk * kD2R);
-  }
 }
 
 // ---------------------------------------------------------------- host side
@@ -245,63 +215,91 @@ static size_t send_offsets(const Ctx *c, int s, int nf, unsigned long long *off)
 
 const uint8_t *halo_present(const Ctx *c) { return (const uint8_t *)c->h_plan.p; }
 
-// the plan's buffers: recv [nct] + send [R][tpr] flags, demands
-static int plan_buffers(Ctx *c, int nct, int R, int tpr, int Rd) {
-  if (!ensure(c, c->h_plan, (size_t)nct + (size_t)R * tpr + 64, "halo plan") ||
-      !ensure(c, c->h_dem, (size_t)(2 * Rd + 1) * 4, "halo demands"))
+// the plan's buffers: recv [nct] + send [R][tpr] flags, demands ([R] send,
+// [R] receive, the total received).  hp: the own-tile
+// K0b zeroes them (the regions are recorded there); NULL: memsets here.
+static int plan_buffers(Ctx *c, int nct, int R, int tpr, int Rd, HaloPre *hp) {
+  const size_t pbytes = (size_t)nct + (size_t)R * tpr, dwords = (size_t)(2 * Rd + 1);
+  if (!ensure(c, c->h_plan, pbytes + 64, "halo plan") || !ensure(c, c->h_dem, dwords * 4, "halo demands"))
     return -1;
-  BSA_HIP(c, hipMemsetAsync(c->h_plan.p, 0, (size_t)nct + (size_t)R * tpr, c->stream));
-  BSA_HIP(c, hipMemsetAsync(c->h_dem.p, 0, (size_t)(2 * Rd + 1) * 4, c->stream));
+  if (hp) {
+    hp->z[0] = (unsigned *)c->h_plan.p;
+    hp->zn[0] = (int)((pbytes + 3) / 4);
+    hp->z[1] = (unsigned *)c->h_dem.p;
+    hp->zn[1] = (int)dwords;
+  } else {
+    BSA_HIP(c, hipMemsetAsync(c->h_plan.p, 0, pbytes, c->stream));
+    BSA_HIP(c, hipMemsetAsync(c->h_dem.p, 0, dwords * 4, c->stream));
+  }
+  return 0;
+}
+
+constexpr int kPlanRows = 16;  // k_halo_plan: grid rows over the own tiles
+static inline int tile_lo(int64_t rb) { return (int)(rb / kTile); }
+// (a rank without rows owns no tile: its clamped rb = n need not be tile-aligned)
+static inline int tile_hi(int64_t rb, int64_t re) { return re > rb ? (int)((re + kTile - 1) / kTile) : tile_lo(rb); }
+
+// box block of the exchange: [tpr own tile boxes | W request words]
+static size_t block_bytes(int tpr, int W) { return ((size_t)tpr * sizeof(TileBox) + (size_t)W * 4 + 15) / 16 * 16; }
+
+int halo_pre(Ctx *c, int64_t rb, int64_t re, HaloPre *hp) {
+  *hp = HaloPre{};
+  const int nct = nct_of(c), a0 = tile_lo(rb), a1 = tile_hi(rb, re), na = a1 - a0;
+  if (!ensure(c, c->counters, sizeof(Counters), "counters")) return -1;
+  if (c->halo_mode == 2) {  // probe: source blocks of tpr = na tiles, full capacity each
+    const int tpr = std::max(na, 1), Rp = (nct + tpr - 1) / tpr;
+    if (plan_buffers(c, nct, 1, tpr, Rp, hp)) return -1;
+    return ensure(c, c->h_hl, (size_t)Rp * tpr * 4, "halo list") ? 0 : -1;
+  }
+  const int R = c->nranks, tpr = tpr_of(c), W = (nct + 31) / 32;
+  const size_t bb = block_bytes(tpr, W);
+  if (!ensure(c, c->h_blk, bb, "halo box block") || !ensure(c, c->h_gblk, bb * R, "halo box blocks")) return -1;
+  if (plan_buffers(c, nct, R, tpr, R, hp)) return -1;
+  hp->z[2] = (unsigned *)((char *)c->h_blk.p + (size_t)tpr * sizeof(TileBox));  // request words
+  hp->zn[2] = W;
+  hp->blk = (TileBox *)c->h_blk.p;
+  hp->blk_base = a0;
   return 0;
 }
 
 // one-GPU plan of the rank owning tiles [a0, a1) (probe and initial capacities):
 // every tile's box is in tbox_c; the present mask and the flat list (source
-// blocks of tpr tiles, full capacity each) come out
+// blocks of tpr tiles, full capacity each) come out.  The buffers were zeroed
+// by the caller (plan_buffers).
 static int plan_local(Ctx *c, int a0, int a1, int tpr) {
   const int nct = nct_of(c), na = a1 - a0;
   const int Rp = (nct + tpr - 1) / tpr;
-  if (!ensure(c, c->counters, sizeof(Counters), "counters")) return -1;
-  if (plan_buffers(c, nct, 1, tpr, Rp)) return -1;
-  if (!ensure(c, c->h_hl, (size_t)Rp * tpr * 4, "halo list")) return -1;
   c->halo_hl = (int64_t)Rp * tpr;
   c->halo_tot_word = 2 * Rp;
   uint8_t *recv = (uint8_t *)c->h_plan.p;
-  if (na > 0) {
-    PlanArgs pa{nct, tpr, 1, -1, a0, a1, (const TileBox *)c->tbox_c.p, nullptr, 0, nullptr, recv, nullptr};
-    hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((nct + 255) / 256), (unsigned)na), dim3(256), 0, c->stream, pa);
-    BSA_HIP(c, hipGetLastError());
-  }
+  PlanArgs pa{nct, tpr, 1, -1, a0, a1, (const TileBox *)c->tbox_c.p, nullptr, 0, nullptr, recv, nullptr};
   ListArgs la{nct, tpr, Rp, -1, a0, a1, 1, recv, nullptr, (int *)c->h_hl.p, nullptr, (unsigned *)c->h_dem.p,
               (Counters *)c->counters.p};
+  const int ny = std::max(1, std::min(na, kPlanRows));
+  hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((nct + 255) / 256), (unsigned)ny), dim3(256), 0, c->stream, pa, ny);
+  BSA_HIP(c, hipGetLastError());
   hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)Rp), dim3(256), 0, c->stream, la, HaloCaps{});
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
 
-int halo_mid(Ctx *c, int64_t rb, int64_t re) {
+int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu) {
+  hu->rbuf = nullptr;
   const int nct = nct_of(c);
-  // (a rank without rows owns no tile: its clamped rb = n need not be tile-aligned)
-  const int a0 = (int)(rb / kTile), a1 = re > rb ? (int)((re + kTile - 1) / kTile) : a0, na = a1 - a0;
+  const int a0 = tile_lo(rb), a1 = tile_hi(rb, re), na = a1 - a0;
   if (c->halo_mode == 2) {
     c->halo_fields = 0;
     return plan_local(c, a0, a1, std::max(na, 1));
   }
-  // ---- exchange mode (several ranks)
+  // ---- exchange mode (several ranks); halo_pre's buffers, zeroed by the own-tile K0b
   const int R = c->nranks, me = c->rank, tpr = tpr_of(c);
   if (R > kHaloMaxRanks) return fail(c, "halo exchange: at most %d ranks", kHaloMaxRanks);
   if ((int64_t)c->halo_cap.size() != (int64_t)R * R) return fail(c, "halo exchange: capacities not set");
   hipStream_t s = c->stream;
   const int W = (nct + 31) / 32;
-  const size_t bb = ((size_t)tpr * sizeof(TileBox) + (size_t)W * 4 + 15) / 16 * 16;
-  if (!ensure(c, c->h_blk, bb, "halo box block") || !ensure(c, c->h_gblk, bb * R, "halo box blocks")) return -1;
-  if (plan_buffers(c, nct, R, tpr, R)) return -1;
-  // 2. own tile boxes + request bits -> every rank
+  const size_t bb = block_bytes(tpr, W);
+  // 2. own tile boxes (written by K0b) + request bits -> every rank
   unsigned *req = (unsigned *)((char *)c->h_blk.p + (size_t)tpr * sizeof(TileBox));
-  BSA_HIP(c, hipMemsetAsync(req, 0, (size_t)W * 4, s));
-  if (na > 0)
-    BSA_HIP(c, hipMemcpyAsync(c->h_blk.p, (const TileBox *)c->tbox_c.p + a0, (size_t)na * sizeof(TileBox),
-                              hipMemcpyDeviceToDevice, s));
   if (c->simp.resume_nav && c->bk_ready && na > 0) {
     hipLaunchKernelGGL(k_halo_req, dim3(64), dim3(256), 0, s, (int)(c->sim_re - c->sim_rb),
                        (const unsigned *)c->bk_rptr.p, (const unsigned *)c->bk_rcol.p, (const unsigned *)c->id2h.p,
@@ -309,21 +307,11 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re) {
     BSA_HIP(c, hipGetLastError());
   }
   if (comm_allgather(c, c->h_blk.p, c->h_gblk.p, bb)) return -1;
-  // 3. plan
-  uint8_t *recv = (uint8_t *)c->h_plan.p, *sendf = recv + nct;
-  PlanArgs pa{nct, tpr, R, me, a0, a1, (const TileBox *)c->tbox_c.p, (const unsigned char *)c->h_gblk.p, bb,
-              (TileBox *)c->tbox_c.p, recv, sendf};
-  hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((nct + 255) / 256), (unsigned)(na + 1)), dim3(256), 0, s, pa);
-  BSA_HIP(c, hipGetLastError());
-  if (na > 0) {
-    hipLaunchKernelGGL(k_halo_plan_req, dim3((unsigned)((R * na + 255) / 256)), dim3(256), 0, s, pa);
-    BSA_HIP(c, hipGetLastError());
-  }
   // capacities and offsets of this rank's regions
   const int nf = (c->simp.winddim == 0 && c->sim_gs_derivable) ? 6 : 8;
   HaloCaps cp{};
   size_t roff = 0;
-  int hoff = 0, smax = 0, rmax = 0;
+  int hoff = 0, smax = 0;
   const size_t stot = send_offsets(c, me, nf, cp.soff);
   for (int q = 0; q < R; ++q) {
     cp.scap[q] = q == me ? 0 : (int)cap_at(c, me, q);
@@ -333,7 +321,6 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re) {
     hoff += cp.rcap[q];
     roff += region_bytes(cp.rcap[q], nf);
     smax = std::max(smax, cp.scap[q]);
-    rmax = std::max(rmax, cp.rcap[q]);
   }
   c->halo_hl = hoff;
   c->halo_tot_word = 2 * R;
@@ -344,15 +331,23 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re) {
       !ensure(c, c->h_recv, std::max<size_t>(roff, 16), "halo recv") ||
       !ensure(c, c->h_hl, (size_t)std::max(hoff, 1) * 4, "halo list"))
     return -1;
+  // 3. plan + lists, one launch
+  uint8_t *recv = (uint8_t *)c->h_plan.p, *sendf = recv + nct;
+  PlanArgs pa{nct, tpr, R, me, a0, a1, (const TileBox *)c->tbox_c.p, (const unsigned char *)c->h_gblk.p, bb,
+              (TileBox *)c->tbox_c.p, recv, sendf};
   ListArgs la{nct, tpr, R, me, a0, a1, 0, recv, sendf, (int *)c->h_hl.p, (unsigned char *)c->h_send.p,
               (unsigned *)c->h_dem.p, (Counters *)c->counters.p};
+  const int ny = std::max(1, std::min(na, kPlanRows));
+  hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((std::max(nct, R * na) + 255) / 256), (unsigned)(ny + 2)),
+                     dim3(256), 0, s, pa, ny);
+  BSA_HIP(c, hipGetLastError());
   hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)R), dim3(256), 0, s, la, cp);
   BSA_HIP(c, hipGetLastError());
   HaloFields fl{};
   DevBuf *src[8] = {&c->own[0], &c->own[1], &c->own[2], &c->own[3], &c->own[4], &c->own[5], &c->s_gse, &c->s_gsn};
   for (int f = 0; f < 8; ++f) fl.f[f] = (double *)src[f]->p;
   fl.nf = nf;
-  // 4. pack, exchange, unpack
+  // 4. pack, exchange (the halo K0b unpacks: hu)
   if (smax > 0) {
     hipLaunchKernelGGL(k_halo_pack, dim3((unsigned)smax, (unsigned)R), dim3(kTile), 0, s, (int)c->n, me, fl,
                        (unsigned char *)c->h_send.p, cp);
@@ -371,11 +366,11 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re) {
   for (int q = 0; q < R; ++q) sof[q] = cp.soff[q];
   if (comm_halo(c, c->h_send.p, sof.data(), slen.data(), stot, c->h_recv.p, rof.data(), rlen.data(), peer.data()))
     return -1;
-  if (rmax > 0) {
-    hipLaunchKernelGGL(k_halo_unpack, dim3((unsigned)rmax, (unsigned)R), dim3(kTile), 0, s, (int)c->n, me, fl,
-                       (const unsigned char *)c->h_recv.p, (const int *)c->h_hl.p, cp, (Counters *)c->counters.p);
-    BSA_HIP(c, hipGetLastError());
-  }
+  hu->rbuf = (const unsigned char *)c->h_recv.p;
+  hu->cp = cp;
+  hu->fl = fl;
+  hu->R = R;
+  hu->n = (int)c->n;
   return 0;
 }
 
@@ -390,7 +385,10 @@ int halo_init_caps(Ctx *c) {
   std::vector<uint8_t> recv((size_t)nct);
   for (int q = 0; q < R; ++q) {
     const int a0 = q * tpr, a1 = a0 + tiles_of(c, q);
-    if (plan_local(c, a0, a1, tpr)) return -1;
+    const int Rp = (nct + tpr - 1) / tpr;
+    if (plan_buffers(c, nct, 1, tpr, Rp, nullptr) || !ensure(c, c->h_hl, (size_t)Rp * tpr * 4, "halo list") ||
+        plan_local(c, a0, a1, tpr))
+      return -1;
     BSA_HIP(c, hipMemcpyAsync(recv.data(), c->h_plan.p, (size_t)nct, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
     for (int t = 0; t < nct; ++t)

@@ -356,11 +356,11 @@ int bk_count(Ctx *c, const BkDev &d);
 int bk_apply(Ctx *c, const BkDev &d);
 void bk_release(Ctx *c);
 
-// halo exchange (bsa_halo.hip).  halo_mid: after K0 prepared the rank's own
-// column tiles (and their boxes), plan which tiles every rank needs, exchange
-// them (mode 1) and leave the flat list of this rank's halo tiles in h_hl
-// (halo_hl slots, -1 = unused) and its present mask in h_plan
-int halo_mid(Ctx *c, int64_t rb, int64_t re);
+// halo exchange (bsa_halo.hip; halo_pre / halo_mid and the device pieces in
+// bsa_halo.h).  halo_mid: after K0 prepared the rank's own column tiles (and
+// their boxes), plan which tiles every rank needs, exchange them (mode 1) and
+// leave the flat list of this rank's halo tiles in h_hl (halo_hl slots, -1 =
+// unused) and its present mask in h_plan
 int halo_init_caps(Ctx *c);      // bsa_sim_init, several ranks: exact initial capacities (no exchange)
 int halo_grow(Ctx *c);           // after an aborted step, several ranks (collective)
 void halo_release(Ctx *c);
