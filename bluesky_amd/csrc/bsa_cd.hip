@@ -30,6 +30,7 @@
 #include "bsa_halo.h"
 #include "bsa_internal.h"
 #include "bsa_mvp_math.h"
+#include "bsa_prep.h"
 
 #pragma clang fp contract(off)
 
@@ -108,94 +109,6 @@ __global__ __launch_bounds__(256) void k_keys(int cnt, int base, const double *_
   key[k] = curve_key(p);
   idx[k] = (unsigned)o;
 }
-
-// ------------------------------------------------------------------ K0b prep
-// Horizontal half-bound in unit-sphere chord units: a pair is
-// kept iff chord < s_i + s_j,  s = ((R/2 + (|gs| + 0.5e-3) tla)(1 + 1e-5)) / 6.3e6 + 1e-6.
-// s >= 0.5 (a reach beyond ~3000 km) or non-finite -> INF (never pruned
-// horizontally); the bound also caps the magnitudes in the fp32 test (kPlaneMargin).
-__device__ __forceinline__ float reach_h(double rpz, double gs, double tlap) {
-  const double s = ((0.5 * rpz + (fabs(gs) + 0.5e-3) * tlap) * (1.0 + 1e-5)) / 6.3e6 + 1e-6;
-  return (s < 0.5) ? (float)s : INFINITY;
-}
-// vertical half-bound [m]: kept iff |dalt| < h_i + h_j
-__device__ __forceinline__ double reach_v(double hpz, double vs, double alt, double tlap) {
-  return (0.5 * hpz + (fabs(vs) + 0.5e-6) * tlap) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(alt);
-}
-
-// Prefilter record from the fp64 unit vector, reach and altitude.
-// lo / hi = alt -/+ h rounded to fp32 (error
-// <= 1e-3 m at flight levels, inside h's 0.5 m + 1e-6 |alt| margin); a
-// non-finite h keeps the pair vertically (lo = -INF, hi = +INF).
-__device__ __forceinline__ PFRec make_pf(double px, double py, double pz, float s, double alt, double h,
-                                         float sv = 0.f) {
-  PFRec p;
-  p.x = (float)px;
-  p.y = (float)py;
-  p.z = (float)pz;
-  p.s = s;
-  if (isfinite(h)) {
-    p.lo = (float)(alt - h);
-    p.hi = (float)(alt + h);
-  } else {
-    p.lo = -INFINITY;
-    p.hi = INFINITY;
-  }
-  p.alt = (float)alt;
-  p.pad = sv;  // vertical budget of a reusable list (0 otherwise), read by the refine
-  return p;
-}
-
-// Midpoint stage 1.  A conflict or LoS of a pair needs a
-// t* in [0, T] (T = max(tla, 0)) with |D + dV t*| <= R and |dalt + dvs t*| <= H
-// in the reference's flat frame at the row (D: its dx / dy, dV: du / dv;
-// also when dv2 / dvs were clamped, see 3.2).  Hence |D + dV T/2| <= R + |dV| T/2
-// and |dalt + dvs T/2| <= H + |dvs| T/2: every aircraft is tested at its
-// position half-way through the look-ahead, m = p + (T/2) (u e + v n) / R_S
-// (e, n its own east / north unit vectors), with half the speed reach.  In
-// the row's tangent frame m_j - m_i = B_i (p_est + dV T/2) / R_S
-// + (T/2) (B_j - B_i) V_j / R_S - (1 - cos c) p_i, where p_est is the chord's
-// tangent part (the reference's D = sigma p_est, |1 - sigma| < 0.012 for the
-// chords involved), ||B_j - B_i|| <= chord (pi/2 + (1 + pi/2) / rho'), and
-// 1 - cos c = chord^2 / 2.  A conflicting pair has chord <= cmax (its dist is
-// <= R + (|V_i| + |V_j|) T with every |V| <= kVcap), so
-//   s = [(R/2 + |V| T/2)(1 + 1e-5) + 0.012 (R/2 + |V| T) + |V| (T/2) kb cmax] / 6.3e6
-//       + cmax^2 / 4 + 1e-6
-// per aircraft bounds |m_j - m_i| / 2 for every such pair.  Aircraft faster
-// than kVcap, with a non-finite velocity, or within cmax of a pole-ish
-// latitude (rho' = cos(lat) - cmax < 0.05) get s = INF (never pruned
-// horizontally).  Vertically a = alt + vs T/2, h = H/2 + (|vs| + 1.5e-6) T/2
-// (+ the same rounding margins as reach_v; 1.5e-6 covers the dvs clamp).
-constexpr double kVcap = 400.0;  // [m/s]
-__device__ __forceinline__ PFRec make_pf_mid(double px, double py, double pz, double sinl, double cosl,
-                                             double coslo, double sinlo, double u, double v, double gs,
-                                             double alt, double vs, double rpz, double hpz, double tlap) {
-  const double ag = fabs(gs) + 0.5e-3;
-  const double ht = 0.5 * tlap;
-  const double cmax = (rpz + (ag + kVcap + 0.5e-3) * tlap) * (1.0 + 1e-5) / 6.35e6;
-  const double rhop = cosl - cmax;
-  double mx = px, my = py, mz = pz;
-  float s = INFINITY;
-  if (fabs(gs) <= kVcap && isfinite(u) && isfinite(v) && rhop >= 0.05 && cmax <= 0.1) {
-    const double kb = 1.5707963267948966 + 2.5707963267948966 / rhop;
-    const double sm = ((0.5 * rpz + ag * ht) * (1.0 + 1e-5) + 0.012 * (0.5 * rpz + ag * tlap) +
-                       ag * ht * kb * cmax) / 6.3e6 + 0.25 * cmax * cmax + 1e-6;
-    const double f = ht / 6371000.0;
-    mx = px + f * (-u * sinlo - v * sinl * coslo);
-    my = py + f * (u * coslo - v * sinl * sinlo);
-    mz = pz + f * (v * cosl);
-    s = (sm < 0.5) ? (float)sm : INFINITY;
-  }
-  const double am = alt + vs * ht;
-  const double h = (0.5 * hpz + (fabs(vs) + 1.5e-6) * ht) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(am);
-  PFRec p = make_pf(mx, my, mz, s, am, h);
-  p.alt = (float)alt;
-  return p;
-}
-
-struct SoA6 {
-  const double *lat, *lon, *trk, *gs, *alt, *vs;
-};
 
 // Row records, sorted position k -> original row perm[k]: own[i] geometry,
 // intruder[i] velocity / altitude (StateBasedCD.py:39-40,65-69 orientation).
@@ -298,9 +211,6 @@ __device__ __forceinline__ void zero_state(const ZeroArgs &z, int t, int nt) {
   }
 }
 
-__device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__restrict__ P, TileBox *gb,
-                                           TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
-                                           TileBox *__restrict__ tbox);
 
 // K0c fused into K0b (no candidate-list reuse): the workgroup's kTile records
 // are one tile, so the boxes are reduced right after the records are written.
@@ -309,30 +219,6 @@ struct FusedBoxes {
   TileBox *blk;                 // halo exchange: tile boxes also into the block sent (blk[tile - blk_base])
   int blk_base;
 };
-
-// fp64 column record of aircraft o: intruder[o] geometry, own[o] velocity /
-// altitude (the per-aircraft factors of StateBasedCD.py's broadcasts)
-__device__ __forceinline__ ColRec col_record(const SoA6 &own, const SoA6 &intr, int o) {
-  const double la = intr.lat[o], lo = intr.lon[o];
-  const double rad = la * kD2R;
-  const double trk = own.trk[o] * kD2R;
-  const double gs = own.gs[o];
-  const double olat = own.lat[o];
-  ColRec c;
-  c.lat = la;
-  c.lon = lo;
-  c.sinlat = sin(rad);
-  c.coslat = cos(rad);
-  c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);  // geo.py:127
-  c.u = gs * sin(trk);                          // StateBasedCD.py:31-32
-  c.v = gs * cos(trk);
-  c.alt = own.alt[o];
-  c.vs = own.vs[o];
-  c.eps = (olat == 0.0) ? 0.000001 : 0.0;      // geo.py:128 (column-indexed)
-  c.olat = olat;
-  for (int q = 0; q < 5; ++q) c.pad[q] = 0.0;
-  return c;
-}
 
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
 // Workgroup = kTile lanes (one tile of sorted records).  rec = 0 (the
@@ -454,101 +340,12 @@ __device__ __forceinline__ float wmax(float v) {
   return v;
 }
 
-// Bounds of every group of kGroup (= one wave's 64 lanes) consecutive sorted
-// records and of every tile (kTile / kGroup groups).  NaN coordinates drop out
-// of the min/max (fminf/fmaxf), which is safe: a record with a NaN coordinate
-// never passes the reach test.
-constexpr int kGroup = 64;
-static_assert(kTile % kGroup == 0, "tiles are whole groups");
-constexpr int kGroupsPerTile = kTile / kGroup;
-constexpr int kSub = 8;  // column sub-group (culling granularity; one stage-1 chunk)
-static_assert(kGroup % kSub == 0 && (kSub & (kSub - 1)) == 0, "sub-groups tile a group");
-
-
 // Counters words that belong to the candidate list (kept across detects by reuse)
 __device__ __forceinline__ bool list_word(int k) {
   constexpr int kCand = (int)(offsetof(Counters, cand) / 8), kTiles = (int)(offsetof(Counters, tiles) / 8);
   constexpr int kGroups = (int)(offsetof(Counters, groups) / 8), kStamp = (int)(offsetof(Counters, stamp) / 8);
   constexpr int kNear = (int)(offsetof(Counters, tiles_near) / 8);
   return k == kCand || k == kTiles || k == kNear || k == kGroups || k >= kStamp;
-}
-
-__device__ __forceinline__ float xmin(float v, int o) { return fminf(v, __shfl_xor(v, o)); }
-__device__ __forceinline__ float xmax(float v, int o) { return fmaxf(v, __shfl_xor(v, o)); }
-
-// Boxes of one kTile-record tile (workgroup = kTile lanes, one wave per
-// kGroup-record group, lane = record): kSub-record sub-group boxes to sbox
-// (nullable), group boxes to gbox, their union to tbox[tile].  Shared by
-// k_boxes and the fused K0b+K0c path of k_prep_cols.
-__device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__restrict__ P, TileBox *gb,
-                                           TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
-                                           TileBox *__restrict__ tbox) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int g = tile * kGroupsPerTile + w;
-  const int k = g * kGroup + lane;
-  const int ngroups = (cnt + kGroup - 1) / kGroup;
-  float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  float smax = 0.f;
-  if (k < cnt) {
-    const PFRec p = P[k];
-    lo[0] = hi[0] = p.x;
-    lo[1] = hi[1] = p.y;
-    lo[2] = hi[2] = p.z;
-    lo[3] = p.lo;
-    hi[3] = p.hi;
-    smax = p.s == p.s ? p.s : INFINITY;
-  }
-  auto mkbox = [&](int count) {
-    TileBox b;
-    for (int q = 0; q < 3; ++q) {
-      b.lo[q] = lo[q];
-      b.hi[q] = hi[q];
-    }
-    b.vlo = lo[3];
-    b.vhi = hi[3];
-    b.smax = smax;
-    b.pad0 = 0.f;
-    b.count = count;
-    b.pad1 = 0;
-    return b;
-  };
-  for (int o = 1; o < kSub; o <<= 1) {  // within each kSub-lane sub-group
-    for (int q = 0; q < 4; ++q) {
-      lo[q] = xmin(lo[q], o);
-      hi[q] = xmax(hi[q], o);
-    }
-    smax = xmax(smax, o);
-  }
-  const int sg = g * (kGroup / kSub) + lane / kSub;
-  if (sbox && (lane & (kSub - 1)) == 0 && sg * kSub < cnt) sbox[sg] = mkbox(min(kSub, cnt - sg * kSub));
-  for (int o = kSub; o < 64; o <<= 1) {
-    for (int q = 0; q < 4; ++q) {
-      lo[q] = xmin(lo[q], o);
-      hi[q] = xmax(hi[q], o);
-    }
-    smax = xmax(smax, o);
-  }
-  if (lane == 0) {
-    TileBox b;
-    for (int q = 0; q < 3; ++q) {
-      b.lo[q] = lo[q];
-      b.hi[q] = hi[q];
-    }
-    b.vlo = lo[3];
-    b.vhi = hi[3];
-    b.smax = smax;
-    b.pad0 = 0.f;
-    b.count = g < ngroups ? min(kGroup, cnt - g * kGroup) : 0;
-    b.pad1 = 0;
-    gb[w] = b;
-    if (g < ngroups) gbox[g] = b;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    TileBox u = gb[0];
-    for (int q = 1; q < kGroupsPerTile; ++q) u = box_union(u, gb[q]);
-    tbox[tile] = u;
-  }
 }
 
 __global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restrict__ P,
@@ -1795,16 +1592,22 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
 // nothing of the candidate list: its counts, tiles and groups), the dequeue
 // shards and the per-row outputs / counts.  Grid-stride, one word per lane
 // (zero_state, shared with the fused K0z+K0b path of k_prep_cols).
+// tbox (nullable): the tile boxes of cnt records from their group boxes (the
+// records and group boxes were written by the resident step's K4').
 __global__ __launch_bounds__(256) void k_zero(int nrows, int full, int keep, unsigned *__restrict__ rctl,
                                               int rforce, Counters *__restrict__ cnt,
                                               unsigned long long *__restrict__ work,
                                               unsigned char *__restrict__ inconf,
                                               unsigned long long *__restrict__ tcpamax,
-                                              unsigned *__restrict__ rowcnt) {
+                                              unsigned *__restrict__ rowcnt, int tcnt,
+                                              const TileBox *__restrict__ gbox, TileBox *__restrict__ tbox) {
   if (rctl && blockIdx.x == 0 && threadIdx.x == 0) {  // reuse: build this detect? (force: age 0)
     rctl[0] = rforce ? 1u : 0u;
     if (rforce) rctl[1] = 0u;
   }
+  if (tbox)
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < (tcnt + kTile - 1) / kTile; t += gridDim.x * blockDim.x)
+      tile_from_groups(tcnt, t, gbox, tbox);
   zero_state(ZeroArgs{nrows, full, keep, cnt, work, inconf, tcpamax, rowcnt, {}, {}},
              blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
 }
@@ -1876,7 +1679,14 @@ static int next_events(Ctx *c, hipEvent_t **ev) {
 
 // stage 1 at the look-ahead midpoints unless KWIK, candidate
 // reuse, BSA_FLAG_STAGE1_T0 or the BSA_STAGE1_T0 environment variable
-static int stage1_mid(int flags, bool reuse, int kwik) {
+// home mode: K1b reads stored fp64 column records (else builds them from the
+// state arrays); BSA_HOME_REC=0/1 overrides (see detect_enqueue)
+bool home_records(const Ctx *c) {
+  static const int home_rec_env = getenv("BSA_HOME_REC") ? atoi(getenv("BSA_HOME_REC")) : -1;
+  return home_rec_env >= 0 ? home_rec_env == 1 : (c->n < (1 << 18) && c->nranks == 1);
+}
+
+int stage1_mid(int flags, bool reuse, int kwik) {
   static const bool t0_env = getenv("BSA_STAGE1_T0") && atoi(getenv("BSA_STAGE1_T0")) != 0;
   return (!reuse && !kwik && !(flags & BSA_FLAG_STAGE1_T0) && !t0_env) ? 1 : 0;
 }
@@ -1950,8 +1760,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // slice of several; with one rank below 2^18 aircraft the stored records
   // win (each aircraft is in ~5 candidates there: K1b 27 -> 18 us at 100k).
   // BSA_HOME_REC=0/1 overrides.
-  static const int home_rec_env = getenv("BSA_HOME_REC") ? atoi(getenv("BSA_HOME_REC")) : -1;
-  const bool recs = !home || (home_rec_env >= 0 ? home_rec_env == 1 : (n < (1 << 18) && c->nranks == 1));
+  const bool recs = !home || home_records(c);
   if (home && (distinct || (rb % kTile != 0 && re > rb) || (flags & BSA_FLAG_KWIK)))  // (a rank without rows: rb = n)
     return fail(c, "home-order detect needs own == intruder, a %d-aligned row slice, no KWIK", kTile);
   const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;
@@ -1971,6 +1780,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // the reuse budgets (whose drift checks assume t = 0 points); the
   // BSA_STAGE1_T0 environment variable selects t = 0 for A/B measurements
   const int mid = stage1_mid(flags, reuse, kwik);
+  // the resident step's K4' already wrote this detect's column records and
+  // boxes from the state it computed (Ctx::sim_prepped; any detect consumes or
+  // invalidates them: it rewrites the same buffers)
+  const bool prepped = c->sim_prepped && home && !halo && !reuse && rb == 0 && re == n && flags == 0 &&
+                       c->sim_prep_key[0] == rpz && c->sim_prep_key[1] == hpz && c->sim_prep_key[2] == tla &&
+                       c->sim_prep_key[3] == (double)mid && c->sim_prep_n == n;
+  c->sim_prepped = false;
   // stage events of this detect: only one detect in ev_every is timed (each
   // record costs a ~5 us bubble before the next kernel, bsa_set_timing_sample)
   hipEvent_t *ev = nullptr;
@@ -1983,12 +1799,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (mark(0)) return -1;
   Counters *dcnt = (Counters *)c->counters.p;
   // K0z: zero the per-detect state (launched once the reuse decision is known)
-  auto zero = [&](bool keep, unsigned *rctl, int rforce) -> int {
+  auto zero = [&](bool keep, unsigned *rctl, int rforce, bool tiles = false) -> int {
     const int64_t m = std::max<int64_t>(2 * (nrows + 1), 256);
     hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>(blocks_for(m, 256), 1024)), dim3(256), 0,
                        c->stream, (int)nrows, 1, keep ? 1 : 0, rctl, rforce, dcnt,
                        (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
-                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p);
+                       (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p, (int)n,
+                       (const TileBox *)c->gbox_c.p, tiles ? (TileBox *)c->tbox_c.p : (TileBox *)nullptr);
     BSA_HIP(c, hipGetLastError());
     return 0;
   };
@@ -2139,6 +1956,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                   (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p, {hp.z[0], hp.z[1], hp.z[2]},
                   {hp.zn[0], hp.zn[1], hp.zn[2]}};
   }
+  if (prepped) {  // K0b + K0c ran in the previous step's K4': K0z + the tile boxes here
+    if (zero(false, nullptr, 0, true)) return -1;
+  } else
   hipLaunchKernelGGL(k_prep_cols, dim3(halo ? (unsigned)(a1 - a0) : blocks_for(n, kTile)), dim3(kTile), 0,
                      c->stream, (int)n, perm_c, home ? 1 : 0, recs ? 1 : 0, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,

@@ -240,6 +240,9 @@ struct Ctx {
   int64_t sim_last_conf = 0, sim_last_los = 0;
   bool sim_gathered = true;  // replicas consistent with every rank's rows
   bool sim_gs_derivable = false;  // gseast / gsnorth of every row follow from gs / trk (K4' without wind ran)
+  bool sim_prepped = false;       // the last K4' wrote the next detect's column records / boxes (one rank)
+  double sim_prep_key[4] = {0, 0, 0, 0};  // ... for rpz, hpz, tla, stage-1 mode
+  int64_t sim_prep_n = 0;
   DevBuf s_tas, s_hdg, s_gse, s_gsn;                        // traffic state besides own[]
   DevBuf s_aptrk, s_aptas, s_apalt, s_apvs, s_selalt, s_bank, s_eps, s_accel;  // frozen
   DevBuf s_atrk, s_atas, s_avs, s_aalt, s_ase, s_asn, s_active;  // ASAS (full n)
@@ -361,6 +364,8 @@ void bk_release(Ctx *c);
 // their boxes), plan which tiles every rank needs, exchange them (mode 1) and
 // leave the flat list of this rank's halo tiles in h_hl (halo_hl slots, -1 =
 // unused) and its present mask in h_plan
+bool home_records(const Ctx *c);                  // home-mode detect stores fp64 column records
+int stage1_mid(int flags, bool reuse, int kwik);  // midpoint stage 1 for this detect?
 int halo_init_caps(Ctx *c);      // bsa_sim_init, several ranks: exact initial capacities (no exchange)
 int halo_grow(Ctx *c);           // after an aborted step, several ranks (collective)
 void halo_release(Ctx *c);

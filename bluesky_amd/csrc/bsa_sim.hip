@@ -23,6 +23,7 @@
 
 #include "bsa_kin_math.h"
 #include "bsa_mvp_row.h"
+#include "bsa_prep.h"
 
 #pragma clang fp contract(off)
 
@@ -46,26 +47,18 @@ struct SimDev {
   unsigned long long *steps_done;  // steps completed in the batch
 };
 
-// Pilot.APorASAS (pilot.py:28-63; no wind, constant wind or a 2-D field) +
-// UpdateAirSpeed/GroundSpeed/Position, rows [rb, re).  FUSE (a CD step without
-// the ASAS bookkeeping): K3's per-row part (bsa_mvp_row.h: the dv fold, the
-// finalize, asas.active = inconf, or DoNothing) runs first in the same lane --
-// the row's new ASAS targets are what its pilot reads next (traffic.py:397),
-// one launch and one pass over the row state fewer.  The gate check of
-// k_mvp_row is made by every lane, so the whole grid agrees on an abort.
-template <bool FUSE>
-__global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, int winddim, double vwn,
-                                                       double vwe, WindField wf, SimDev d, MvpIn mv,
-                                                       bsa_mvp_params mp) {
-  if (FUSE) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && mv.gate[0] != 0) mv.sticky[0] = 1u;
-    if (*d.sticky || mv.gate[0] != 0) return;
-  } else if (*d.sticky) {
-    return;
-  }
-  const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
-  if (k >= re) return;
+struct PrepArgs {
+  PrepOut out;
+  TileBox *sbox, *gbox;  // (the tile boxes follow from the group boxes in the detect's K0z)
+  double rpz, hpz, tla;
+  int mid, rec, n;
+};
+
+// one row of K4' (below)
+template <bool FUSE, bool PREP>
+__device__ __forceinline__ void pilot_kin_row(int rb, int k, double simdt, int winddim, double vwn, double vwe,
+                                              const WindField &wf, const SimDev &d, const MvpIn &mv,
+                                              const bsa_mvp_params &mp, const PrepArgs &pa) {
   if (FUSE) mvp_row(rb, k - rb, mp, mv);
   if (winddim == 2) {  // pilot.py:32 and traffic.py:463 read the field at the same pre-step position
     kin::windfield_2d(wf, d.lat[k], d.lon[k], vwn, vwe);
@@ -133,7 +126,43 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   d.gsn[k] = o.gsnorth;
   d.altprev[k] = s.alt;
   d.ax[k] = o.ax;
+  if (PREP) prep_home_record(k, o.lat, o.lon, o.trk, o.gs, o.alt, o.vs, pa.rpz, pa.hpz, pa.tla, pa.mid, pa.rec, pa.out);
 }
+
+// Pilot.APorASAS (pilot.py:28-63; no wind, constant wind or a 2-D field) +
+// UpdateAirSpeed/GroundSpeed/Position, rows [rb, re).  FUSE (a CD step without
+// the ASAS bookkeeping): K3's per-row part (bsa_mvp_row.h: the dv fold, the
+// finalize, asas.active = inconf, or DoNothing) runs first in the same lane --
+// the row's new ASAS targets are what its pilot reads next (traffic.py:397),
+// one launch and one pass over the row state fewer.  The gate check of
+// k_mvp_row is made by every lane, so the whole grid agrees on an abort.
+// PREP (one rank, the next step is a CD step): the lane also writes the next
+// detect's column record of its row from the state it has just computed
+// (bsa_prep.h: k_prep_cols' expressions, bitwise its records), and each wave
+// reduces its group's sub-group and group boxes; that detect then skips its
+// K0b launch, its K0z unites the group boxes into tile boxes
+// (detect_enqueue, Ctx::sim_prepped).
+template <bool FUSE, bool PREP>
+__global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, int winddim, double vwn,
+                                                         double vwe, WindField wf, SimDev d, MvpIn mv,
+                                                         bsa_mvp_params mp, PrepArgs pa) {
+  if (FUSE) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && mv.gate[0] != 0) mv.sticky[0] = 1u;
+    if (*d.sticky || mv.gate[0] != 0) return;
+  } else if (*d.sticky) {
+    return;
+  }
+  const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
+  if (PREP) {  // every lane reaches the wave's group reduction
+    if (k < re) pilot_kin_row<FUSE, PREP>(rb, k, simdt, winddim, vwn, vwe, wf, d, mv, mp, pa);
+    group_boxes(pa.n, k / kGroup, pa.out.PC, pa.sbox, pa.gbox);
+    return;
+  }
+  if (k >= re) return;
+  pilot_kin_row<FUSE, PREP>(rb, k, simdt, winddim, vwn, vwe, wf, d, mv, mp, pa);
+}
+
 
 // field list of one all-gather: fp64 arrays (full n) + optionally one uint8 array
 struct Fields {
@@ -565,6 +594,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   if (bsa::halo_init_caps(c)) return -1;
   c->sim_steps = c->sim_cd_calls = c->sim_last_conf = c->sim_last_los = 0;
   c->sim_gathered = true;
+  c->sim_prepped = false;
   c->sim_gs_derivable = false;  // gseast / gsnorth are the host's until K4' runs
   if (c->feed_pending) {  // a snapshot of the previous sim is dropped
     BSA_HIP(c, hipEventSynchronize(c->feed_ev));
@@ -600,18 +630,51 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
         const int v = getenv("BSA_K4_BLOCK") ? atoi(getenv("BSA_K4_BLOCK")) : 64;
         return (v == 64 || v == 128 || v == 256) ? v : 64;
       }();
-      const int64_t nb = std::max<int64_t>(1, (re - rb + k4b - 1) / k4b);
+      // one rank, the next step a CD step: K4' also prepares that detect's
+      // column records and boxes (its K0b launch is skipped; BSA_SIM_PREP=0 off)
+      static const bool prep_env = !(getenv("BSA_SIM_PREP") && atoi(getenv("BSA_SIM_PREP")) == 0);
+      const bool prep = prep_env && c->nranks == 1 && c->home && !c->reuse_on && c->halo_mode == 0 && rb == 0 &&
+                        re == c->n && (c->sim_steps + 1) % c->simp.cd_every == 0;
+      bsa::PrepArgs pa{};
+      if (prep) {
+        const int64_t n = c->n;
+        pa.rec = bsa::home_records(c) ? 1 : 0;
+        if ((pa.rec && !bsa::ensure(c, c->colrec, n * sizeof(bsa::ColRec), "column records")) ||
+            !bsa::ensure(c, c->pfcol, n * sizeof(bsa::PFRec), "prefilter columns") ||
+            !bsa::ensure(c, c->pfvcol, n * sizeof(bsa::PFVel), "prefilter column velocities") ||
+            !bsa::ensure(c, c->pfpcol, n * sizeof(float4), "prefilter column positions") ||
+            !bsa::ensure(c, c->tbox_c, ((n + bsa::kTile - 1) / bsa::kTile) * sizeof(bsa::TileBox), "column tile boxes") ||
+            !bsa::ensure(c, c->gbox_c, ((n + bsa::kGroup - 1) / bsa::kGroup) * sizeof(bsa::TileBox), "column group boxes") ||
+            !bsa::ensure(c, c->sbox_c, ((n + bsa::kSub - 1) / bsa::kSub) * sizeof(bsa::TileBox), "column sub-group boxes"))
+          return -1;
+        pa.out = bsa::PrepOut{(bsa::ColRec *)c->colrec.p, (bsa::PFRec *)c->pfcol.p, (bsa::PFVel *)c->pfvcol.p,
+                              (float4 *)c->pfpcol.p};
+        pa.sbox = (bsa::TileBox *)c->sbox_c.p;
+        pa.gbox = (bsa::TileBox *)c->gbox_c.p;
+        pa.rpz = c->simp.rpz;
+        pa.hpz = c->simp.hpz;
+        pa.tla = c->simp.tla;
+        pa.mid = bsa::stage1_mid(0, false, 0);
+        pa.n = (int)n;
+      }
+      const int blk = k4b;  // (PREP: whole waves = whole groups, rb = 0)
+      const int64_t nb = std::max<int64_t>(1, (re - rb + blk - 1) / blk);
       bsa::MvpIn mv{};
       if (c->mvp_deferred) memcpy(&mv, c->mvp_defer.data(), sizeof(mv));
-      if (c->mvp_deferred)
-        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<true>, dim3((unsigned)nb), dim3(k4b), 0, c->stream, (int)rb,
-                           (int)re, c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
-                           bsa::wind_field(c), bsa::sim_dev(c), mv, c->simp.mvp);
-      else
-        hipLaunchKernelGGL(bsa::k_sim_pilot_kin<false>, dim3((unsigned)nb), dim3(k4b), 0, c->stream, (int)rb,
-                           (int)re, c->simp.simdt, c->simp.winddim, c->simp.windnorth, c->simp.windeast,
-                           bsa::wind_field(c), bsa::sim_dev(c), mv, c->simp.mvp);
+      const auto K4 = c->mvp_deferred ? (prep ? bsa::k_sim_pilot_kin<true, true> : bsa::k_sim_pilot_kin<true, false>)
+                                      : (prep ? bsa::k_sim_pilot_kin<false, true> : bsa::k_sim_pilot_kin<false, false>);
+      hipLaunchKernelGGL(K4, dim3((unsigned)nb), dim3(blk), 0, c->stream, (int)rb, (int)re, c->simp.simdt,
+                         c->simp.winddim, c->simp.windnorth, c->simp.windeast, bsa::wind_field(c), bsa::sim_dev(c), mv,
+                         c->simp.mvp, pa);
       c->mvp_deferred = false;
+      c->sim_prepped = prep;
+      if (prep) {
+        c->sim_prep_key[0] = pa.rpz;
+        c->sim_prep_key[1] = pa.hpz;
+        c->sim_prep_key[2] = pa.tla;
+        c->sim_prep_key[3] = (double)pa.mid;
+        c->sim_prep_n = c->n;
+      }
       BSA_HIP(c, hipGetLastError());
       c->sim_gs_derivable = true;  // every rank's rows now hold K4's gs / trk / gse / gsn
       c->sim_gathered = c->nranks == 1;
@@ -627,6 +690,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     // grows only the buffers that overflowed on IT (another rank's overflow
     // re-runs the step with unchanged buffers here) and all ranks re-run it
     c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
+    c->sim_prepped = false;  // (an aborted K4' prepared nothing)
     const int64_t done = (int64_t)ctl[1];
     c->sim_steps = base + done;
     c->sim_gs_derivable = derivable0 || done > 0;  // K4' ran for the completed steps only
@@ -736,6 +800,7 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
     if (k < 10) any_cd = true;
     if (bsa::put_home(c, cp[k].dst, cp[k].src, 8, tmp)) return -1;
   }
+  c->sim_prepped = false;  // prepared records are of the old state
   if (any_cd) {
     // every rank passed the same full arrays: the replicas are consistent only
     // if ALL replicated arrays were passed; otherwise the next all-gather
@@ -920,6 +985,7 @@ int bsa_sim_set_params(bsa_ctx *cc, const bsa_sim_params *p) {
   if (bsa::check_params(c, p)) return -1;
   if (p->resume_nav && !c->simp.resume_nav) c->bk_ready = false;  // the bookkeeping starts empty
   c->simp = *p;
+  c->sim_prepped = false;
   return 0;
 }
 

@@ -344,6 +344,7 @@ static void set_n(Ctx *c, int64_t n) {
   c->perm_valid = false;   // the spatial order is over the old indices
   c->reuse_valid = false;  // so is any reusable candidate list
   c->sim_gathered = true;  // every replica is complete after the change
+  c->sim_prepped = false;  // prepared records are of the old traffic
 }
 
 // length of each full-n per-aircraft buffer for n aircraft (several ranks: the
