@@ -35,6 +35,9 @@ OPS_PER_PAIR = 110           # algorithmic fp64 ops per pair-eval
 PF_FLOPS_PER_PAIR = 9        # prefilter stage-1 fp32 flops per tested pair:
                              # acc = K + k (1) + 3 FMA (6); lo - hi, hi - lo (2)
 KIN_BYTES_PER_AC = 234       # K4 algorithmic HBM bytes per aircraft-step
+PREP_BYTES_PER_AC = 128 + 32 + 16 + 16 + 48 / 8 + 48 / 64   # K4' also writing the next detect's column
+                             # records (fp64 128 B when stored, PFRec, PFVel, position) and sub-group /
+                             # group boxes (one rank)
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E (spec)
 PMC_JSON = os.path.join(REPO, 'profiles', 'pmc_latest.json')
 TIMING_SAMPLE = 8            # detects per HIP-event-timed detect (bsa_set_timing_sample; each timed one
@@ -273,8 +276,11 @@ def main():
     propagation = None
     if kin.get('dur_ns'):
         nrows_r0 = (n + world - 1) // world
-        alg = KIN_BYTES_PER_AC * nrows_r0
+        prep = world == 1 and not args.reuse and os.environ.get('BSA_SIM_PREP', '1') != '0'
+        alg = int((KIN_BYTES_PER_AC + (PREP_BYTES_PER_AC if prep else 0)) * nrows_r0)
         propagation = dict(kernel='k_sim_pilot_kin', bound='hbm', algorithmic_bytes=alg, from_profile=prov,
+                           bytes_per_aircraft=dict(kinematics=KIN_BYTES_PER_AC,
+                                                   next_detect_records=PREP_BYTES_PER_AC if prep else 0),
                            duration_us_profiled=kin['dur_ns'] * 1e-3,
                            achieved_GBps=alg / kin['dur_ns'], peak_GBps=HBM_PEAK_GBPS,
                            frac=alg / kin['dur_ns'] / HBM_PEAK_GBPS,
