@@ -525,6 +525,7 @@ struct RefineParams {
   float H;      // hpz [m]
   float T;      // max(tla, 0) [s]
   float lim2;   // ((R + EABS) / (1 - E1) / R_S)^2 (unit-sphere units, as the refine's positions)
+  float zero;   // 0 (diagnostic builds: -DBSA_PF_REFINE_X2 evaluates the refine twice)
 };
 constexpr float kRS = 6371000.f;   // scale of the unit-sphere chord to metres
 constexpr float kE1 = 0.012f;      // bound on |log(reference dist / estimated dist)|
@@ -600,7 +601,13 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
 #ifndef PF_Q1
 #define PF_Q1 512  // per-wave stage-1 queue: u16 (row_local << 6 | column slot)
 #endif
-constexpr int PF_Q2 = 128;   // per-wave stage-2 queue: uint2 (sorted row, sorted column)
+// Refine survivors go straight to the wave's reserved block of PF_RES
+// candidate slots (one returning atomic per block; the unused tail of a wave's
+// last block is filled with kCandHole, which K1b skips)
+#ifndef PF_RES
+#define PF_RES 128
+#endif
+constexpr unsigned kCandHole = 0xffffffffu;  // candidate slot without a pair (both words)
 constexpr int PF_WROWS = 64;   // rows per wave (one per lane)
 constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 // Work distribution knob of the sweep (BSA_PF_SHARDS overrides it for
@@ -669,8 +676,8 @@ constexpr unsigned kTraceWave = 256;
 // per-lane counts).  The queue is drained after every batch (or when full)
 // with all 64 lanes busy through stage 2 (refine) on LDS-resident inputs (the
 // batch's staged columns, the item's staged rows, row unit vectors by
-// ds_bpermute).  Stage-2 survivors go to a second queue flushed to HBM with
-// one atomic on the wave's candidate shard.
+// ds_bpermute).  Stage-2 survivors are written straight to the wave's
+// reserved block of candidate slots (one atomic on its shard per PF_RES slots).
 template <bool NOPRUNE>
 // 4 waves per SIMD = PF_BLOCKS_PER_CU resident workgroups: up to 128 VGPRs,
 // no spills (at 5 waves the 96-VGPR cap spilled to scratch, and every scratch
@@ -685,7 +692,6 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     unsigned long long *__restrict__ work, RefineParams prm,
     uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
-  __shared__ uint2 q2s[PF_WAVES][2][PF_Q2];  // double-buffered: one fills while the other's flush atomic flies
   __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
   __shared__ float4 cen[PF_WAVES][32];      //                      e e' n n'     (stage 1)
   __shared__ float4 clh[PF_WAVES][32];      //                      lo lo' hi hi' (stage 1)
@@ -699,10 +705,6 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned short *q1 = q1s[w];
-  unsigned fb = 0;           // fill buffer of q2 (wave-uniform)
-  uint2 *q2 = q2s[w][0];
-  unsigned long long pbase = 0;  // pending flush: lane 0's atomic result, consumed one flush later
-  unsigned pn = 0;               // entries of the pending buffer (wave-uniform)
   float *ska = (float *)cka[w];
   float *sen = (float *)cen[w];
   float *slh = (float *)clh[w];
@@ -710,7 +712,6 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   float4 *sv = csv[w];
   unsigned *sci = cix[w];
   float4 *rv = rsv[w];
-  unsigned n2 = 0;        // wave-uniform
   unsigned subs = 0;      // 8-column sub-groups swept by this wave (for the roofline)
   const float qnan = __builtin_nanf("");
   // Dynamic work distribution: an item is one (tile pair, 64-row slice) that
@@ -748,26 +749,30 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   const unsigned long long ccap = cap / kCandShards;
   uint2 *ccand = cand + (unsigned long long)(shard % kCandShards) * ccap;
   unsigned long long *cshard = &cnt->cshard[shard % kCandShards][0];
-  // q2 flush, double-buffered: reserve room for the fill buffer with a
-  // returning atomic and write the PREVIOUS buffer out to the room its atomic
-  // (issued one flush earlier) returned -- no wave waits on a fresh atomic
-  auto write_pending = [&]() {
-    if (!pn) return;
-    const unsigned long long base = wave_bcast_u64(pbase);
-    const uint2 *pq = q2s[w][fb ^ 1];
-    for (unsigned k = lane; k < pn; k += 64)
-      if (base + k < ccap) ccand[base + k] = pq[k];
-    pn = 0;
-  };
-  auto flush2 = [&]() {
-    __builtin_amdgcn_wave_barrier();
-    write_pending();
-    if (lane == 0) pbase = atomicAdd(cshard, (unsigned long long)n2);
-    pn = n2;
-    fb ^= 1u;
-    q2 = q2s[w][fb];
-    n2 = 0;
-    __builtin_amdgcn_wave_barrier();
+  // the wave's candidate slots [wpos, wend) (wave-uniform): a refine round's
+  // survivors (mask mk) take the next slots in lane order; a round that does
+  // not fit reserves the next PF_RES-slot block (one returning atomic on the
+  // shard counter) and continues there.  (The LDS stage-2 queue this replaces
+  // waited on the previous flush's atomic at every flush: ~25 k flushes per
+  // sweep, the densest items flushing every ~64 survivors.)
+  unsigned long long wpos = 0, wend = 0;
+  unsigned nemit = 0;  // candidates this wave wrote (statistics)
+  auto emit = [&](unsigned long long mk, bool keep, uint2 v) {
+    const unsigned c = (unsigned)__popcll(mk), pre = lane_prefix(mk);
+    const unsigned long long room = wend - wpos;
+    unsigned long long idx = wpos + pre;
+    if (c > room) {
+      unsigned long long r = 0;
+      if (lane == 0) r = atomicAdd(cshard, (unsigned long long)PF_RES);
+      const unsigned long long nb = wave_bcast_u64(r);
+      if (pre >= room) idx = nb + (pre - room);
+      wpos = nb + (c - room);
+      wend = nb + PF_RES;
+    } else {
+      wpos += c;
+    }
+    if (keep && idx < ccap) ccand[idx] = v;
+    nemit += c;
   };
 #ifdef BSA_PF_STAMPS
   // [4] stage-1 survivors, [5] refine rounds, [6] batches, [7] enqueue loop trips
@@ -928,16 +933,17 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
           gi = (unsigned)rbase + rl;
           gj = sci[cl];
           keep = NOPRUNE ? true : pf_refine(rsp[w][rl], rv[rl], rbs[w][rl], sx[cl], sv[cl], prm);
+#ifdef BSA_PF_REFINE_X2
+          {  // the same test on inputs the compiler cannot prove equal: the refine's cost, measured
+            float4 c2 = sx[cl];
+            c2.x += prm.zero;
+            keep = keep & (NOPRUNE ? true : pf_refine(rsp[w][rl], rv[rl], rbs[w][rl], c2, sv[cl], prm));
+          }
+#endif
         }
         const unsigned long long mk = __ballot(keep);
         if (mk) {
-          if (keep) q2[n2 + lane_prefix(mk)] = make_uint2(gi, gj);
-          n2 = __builtin_amdgcn_readfirstlane(n2 + (unsigned)__popcll(mk));
-          if (n2 > (unsigned)(PF_Q2 - 64)) {
-            PF_STAMP(2);
-            flush2();
-            PF_STAMP(3);
-          }
+          emit(mk, keep, make_uint2(gi, gj));
         }
       }
       n1 = 0;
@@ -1062,13 +1068,6 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       PF_STAMP(1);
       if (!more) break;
     }
-    // reserve room for the item's candidates now (the atomic's result is
-    // consumed one flush later): at the end of the sweep every wave would
-    // otherwise flush at once, queueing on the shard counters
-#ifndef PF_ITEM_FLUSH
-#define PF_ITEM_FLUSH 1
-#endif
-    if (PF_ITEM_FLUSH && n2) flush2();
     } while (0);
 #ifdef BSA_PF_TRACE
     if (lane == 0 && pf_trace) {  // per-wave record region (no atomics)
@@ -1084,18 +1083,23 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 #endif
   }
   PF_STAMP(0);
-  if (n2) flush2();
-  write_pending();
+  for (unsigned long long k = wpos + lane; k < wend; k += 64)  // the last block's unused tail
+    if (k < ccap) ccand[k] = make_uint2(kCandHole, kCandHole);
   // the roofline's sub-group count: one atomic per workgroup, spread over 32
   // lines (4096 waves adding to one word serialised at ~12 ns each, ~50 us of
   // the sweep's tail when the waves finish together)
-  __shared__ unsigned wsubs[PF_WAVES];
-  if (lane == 0) wsubs[w] = subs;
+  __shared__ unsigned wsubs[PF_WAVES], wcand[PF_WAVES];
+  if (lane == 0) {
+    wsubs[w] = subs;
+    wcand[w] = nemit;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned t = 0;
+    unsigned t = 0, tc = 0;
     for (int q = 0; q < PF_WAVES; ++q) t += wsubs[q];
     if (t) atomicAdd(&cnt->gpart[blockIdx.x & 31][0], (unsigned long long)t);
+    for (int q = 0; q < PF_WAVES; ++q) tc += wcand[q];
+    if (tc) atomicAdd(&cnt->gpart[blockIdx.x & 31][1], (unsigned long long)tc);  // candidates (not slots)
   }
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
@@ -1350,6 +1354,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
 #pragma unroll
     for (int q = 1; q < kCandShards; ++q) sh += (idx >= pre[q]) ? 1 : 0;
     const uint2 p = cand[(unsigned long long)sh * ccap + (idx - pre[sh])];
+    if (p.x == kCandHole) {  // an unused reserved slot (the tail of a wave's last block)
+      cflag[idx] = 0;
+      continue;
+    }
     // home mode (perm_r == NULL, the resident sim): rows are the home slice
     // [rb, rb + nrows) of the columns; the key's row is the home row, its
     // column the aircraft index (so K2 orders each row's pairs by index)
@@ -1477,7 +1485,9 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
   const unsigned t0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (t0 == 0) {
     unsigned long long pre[kCandShards + 1];
-    const unsigned long long ncand = cand_prefix(cnt, cap, pre);
+    (void)cand_prefix(cnt, cap, pre);
+    unsigned long long ncand = 0;  // candidates written (the shard counts include reserved, unused slots)
+    for (int q = 0; q < 32; ++q) ncand += cnt->gpart[q][1];
     cnt->conf = ovf ? 0 : P;
     cnt->los = ovf ? 0 : L;
     cnt->cand = ncand;
@@ -2004,7 +2014,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const float T = (float)(tla > 0.0 ? tla : 0.0);
   const float lim = (float)((rpz + kEABS + (reuse ? 2.0 * c->reuse_sh : 0.0)) / (1.0 - kE1));
   const float liml = lim / kRS;  // unit-sphere units (pf_refine)
-  const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : liml * liml};
+  const RefineParams rp{(float)rpz, (float)hpz, T, kwik ? INFINITY : liml * liml, 0.f};
   // ---- K1a prefilter: persistent grid, PF_BLOCKS_PER_CU workgroups per CU
   // (LDS-limited residency), at least one workgroup per dequeue shard
   // pieces: ~8 items per row tile, a few hundred row tiles fill the waves;
@@ -2132,6 +2142,7 @@ int detect_finish(Ctx *c, bool *retry) {
     worst = std::max(worst, h.cshard[q][0]);
     total += h.cshard[q][0];
   }
+  total = h.cand;  // (the shard counts include reserved, unused slots; K2 summed the written ones)
   if (worst > c->cand_cap / kCandShards) {
     c->cand_cap = (unsigned long long)kCandShards * (worst + worst / 4 + 1024);
     c->reuse_valid = false;
