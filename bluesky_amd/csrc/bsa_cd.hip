@@ -30,6 +30,7 @@
 #include "bsa_halo.h"
 #include "bsa_internal.h"
 #include "bsa_mvp_math.h"
+#include "bsa_mvp_row.h"
 #include "bsa_prep.h"
 
 #pragma clang fp contract(off)
@@ -177,6 +178,16 @@ constexpr double kRefineChord = 0.03;  // the refine keeps (without refining) pa
 constexpr int kWorkShards = 32;  // dequeue counters (4 per XCD group): a returning atomic on one
                                  // word saturates at ~88 dequeues/us (MI355X_MICROARCH 'dequeue')
 constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
+
+// K2 with row buckets (k_rank_rows): one workgroup per kRankRows rows; the
+// pair counts of every block (k_rowblk) follow the 2 (nrows + 1) per-row
+// counts, so the row offsets need no scan with a look-back chain.  (K1b
+// counting them with atomics, one per wave and block, cost 12 us at the 100k
+// box: the per-block words were hit by every wave of a block's rows at once.)
+constexpr int kRankRows = 512;
+constexpr int kRankLds = 1536;  // pairs per block folded from LDS (54 KB: 2 blocks per CU)
+__host__ __device__ __forceinline__ int rank_blocks(int nrows) { return (nrows + kRankRows - 1) / kRankRows; }
+__host__ __device__ __forceinline__ int rowcnt_words(int nrows) { return 2 * (nrows + 1) + 2 * rank_blocks(nrows); }
 
 // Per-detect state to zero (k_zero, or fused into k_prep_cols: cnt != nullptr)
 struct ZeroArgs {
@@ -399,6 +410,70 @@ static_assert(kSlicesPerTile == 8, "8 slices per tile (item bit layout, slice bo
 // other column tile means the halo plan disagreed with this test (it cannot:
 // the plan runs the same boxes_may_interact on the same boxes): it is flagged
 // (cnt->halo_miss, the step fails loudly), never silently dropped or swept.
+// K0d's test of one (row tile rt, column tile ct) pair: its class (near: the
+// boxes overlap, far: they only may interact) and the mask of the row tile's
+// 64-row slices whose boxes may reach the column tile (sg: the slice boxes)
+__device__ __forceinline__ unsigned tp_classify(const TileBox &a, const TileBox *sg, const TileBox &b, int rt, int ct,
+                                                int nrows, int noprune, const uint8_t *__restrict__ present, int p0,
+                                                int p1, Counters *__restrict__ cnt, bool &kn, bool &kf) {
+  unsigned sm = 0;
+  if ((noprune || boxes_may_interact(a, b)) && present && !(ct >= p0 && ct < p1) && !present[ct]) {
+    cnt->halo_miss = 1;
+  } else if (noprune || boxes_may_interact(a, b)) {
+    const bool near = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]) == 0.f &&
+                      gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]) == 0.f &&
+                      gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]) == 0.f;
+    kn = near;
+    kf = !near;
+    for (int q = 0; q < kSlicesPerTile; ++q)
+      if (rt * kTile + q * kGroup < nrows && (noprune || boxes_may_interact(sg[q], b))) sm |= 1u << q;
+  }
+  return sm;
+}
+
+// K0d's list append of one round (every lane of the NT-lane workgroup calls
+// it): the items (slices) of each class and the tile pairs themselves, one
+// returning atomic per class (near ones from the front of the list, the
+// others from its back)
+template <int NT>
+__device__ __forceinline__ void tp_emit(bool kn, bool kf, unsigned sm, int rt, int ct, uint2 *__restrict__ out,
+                                        unsigned long long cap, Counters *__restrict__ cnt,
+                                        unsigned long long *__restrict__ icnt, unsigned (*wpre)[NT / 64],
+                                        unsigned long long *bbase) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned ni = (unsigned)__popc(sm);
+  const unsigned xn = wave_incl_scan(kn ? ni : 0u), xf = wave_incl_scan(kf ? ni : 0u);
+  const unsigned tw = (unsigned)__popcll(__ballot(kn)) | (unsigned)__popcll(__ballot(kf)) << 16;
+  if (lane == 63) {
+    wpre[0][w] = xn;
+    wpre[1][w] = xf;
+    wpre[3][w] = tw;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    unsigned run = 0, tiles = 0;
+    for (int q = 0; q < NT / 64; ++q) {
+      const unsigned v = wpre[threadIdx.x][q];
+      wpre[threadIdx.x][q] = run;
+      run += v;
+      tiles += (wpre[3][q] >> (16 * threadIdx.x)) & 0xffffu;
+    }
+    bbase[threadIdx.x] = run ? atomicAdd(&icnt[1 + threadIdx.x], (unsigned long long)run) : 0ull;
+    if (tiles) {
+      atomicAdd(&cnt->tiles, (unsigned long long)tiles);
+      if (threadIdx.x == 0) atomicAdd(&cnt->tiles_near, (unsigned long long)tiles);
+    }
+  }
+  __syncthreads();
+  if (ni) {  // item = (row tile | slice << 22, column tile); near ones from the front
+    unsigned long long k = (kn ? bbase[0] + wpre[0][w] + xn : bbase[1] + wpre[1][w] + xf) - ni;
+    for (unsigned m = sm; m; m &= m - 1u, ++k) {
+      const uint2 v = make_uint2((unsigned)rt | (unsigned)__builtin_ctz(m) << 22, (unsigned)ct);
+      out[kn ? k : cap - 1 - k] = v;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, int nrows, const TileBox *__restrict__ rb,
                                                           const TileBox *__restrict__ rg,
                                                           const TileBox *__restrict__ cb, int noprune,
@@ -454,56 +529,44 @@ __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, int 
         const int i = (int)(r / kSuper);
         rt = rt0 + i;
         ct = (int)sc2 * kSuper + (int)(r % kSuper);
-        if (i < nr && ct < nct) {
-          const TileBox a = srt[i], b = cb[ct];
-          if ((noprune || boxes_may_interact(a, b)) && present && !(ct >= p0 && ct < p1) && !present[ct]) {
-            cnt->halo_miss = 1;
-          } else if (noprune || boxes_may_interact(a, b)) {
-            const bool near = gap(a.lo[0], a.hi[0], b.lo[0], b.hi[0]) == 0.f &&
-                              gap(a.lo[1], a.hi[1], b.lo[1], b.hi[1]) == 0.f &&
-                              gap(a.lo[2], a.hi[2], b.lo[2], b.hi[2]) == 0.f;
-            kn = near;
-            kf = !near;
-            for (int q = 0; q < kSlicesPerTile; ++q)
-              if (rt * kTile + q * kGroup < nrows && (noprune || boxes_may_interact(sgb[i * kSlicesPerTile + q], b)))
-                sm |= 1u << q;
-          }
-        }
+        if (i < nr && ct < nct) sm = tp_classify(srt[i], &sgb[i * kSlicesPerTile], cb[ct], rt, ct, nrows, noprune,
+                                                 present, p0, p1, cnt, kn, kf);
       }
-      // items (the pair's slices) of each class, and the tile pairs themselves
-      const unsigned ni = (unsigned)__popc(sm);
-      const unsigned xn = wave_incl_scan(kn ? ni : 0u), xf = wave_incl_scan(kf ? ni : 0u);
-      const unsigned tw = (unsigned)__popcll(__ballot(kn)) | (unsigned)__popcll(__ballot(kf)) << 16;
-      if (lane == 63) {
-        wpre[0][w] = xn;
-        wpre[1][w] = xf;
-        wpre[3][w] = tw;
-      }
-      __syncthreads();
-      if (threadIdx.x < 2) {
-        unsigned run = 0, tiles = 0;
-        for (int q = 0; q < kTPThreads / 64; ++q) {
-          const unsigned v = wpre[threadIdx.x][q];
-          wpre[threadIdx.x][q] = run;
-          run += v;
-          tiles += (wpre[3][q] >> (16 * threadIdx.x)) & 0xffffu;
-        }
-        bbase[threadIdx.x] = run ? atomicAdd(&icnt[1 + threadIdx.x], (unsigned long long)run) : 0ull;
-        if (tiles) {
-          atomicAdd(&cnt->tiles, (unsigned long long)tiles);
-          if (threadIdx.x == 0) atomicAdd(&cnt->tiles_near, (unsigned long long)tiles);
-        }
-      }
-      __syncthreads();
-      if (ni) {  // item = (row tile | slice << 22, column tile); near ones from the front
-        unsigned long long k = (kn ? bbase[0] + wpre[0][w] + xn : bbase[1] + wpre[1][w] + xf) - ni;
-        for (unsigned m = sm; m; m &= m - 1u, ++k) {
-          const uint2 v = make_uint2((unsigned)rt | (unsigned)__builtin_ctz(m) << 22, (unsigned)ct);
-          out[kn ? k : cap - 1 - k] = v;
-        }
-      }
+      tp_emit<kTPThreads>(kn, kf, sm, rt, ct, out, cap, cnt, icnt, wpre, bbase);
       __syncthreads();  // wpre / bbase are rewritten by the next round
     }
+  }
+}
+
+// K0d without the super level, for few column tiles (the 100k box: 196):
+// one workgroup per row tile, one lane per column tile -- the super pass's
+// union loads, its scan and its barrier were a third of K0d's chain there
+constexpr int kTPDirectThreads = 256;
+constexpr int kTPDirectMax = 1024;  // column tiles up to which K0d runs direct
+__global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
+    int nrt, int nct, int nrows, const TileBox *__restrict__ rb, const TileBox *__restrict__ rg,
+    const TileBox *__restrict__ cb, int noprune, uint2 *__restrict__ out, unsigned long long cap,
+    Counters *__restrict__ cnt, unsigned long long *__restrict__ icnt, const unsigned *__restrict__ build,
+    const uint8_t *__restrict__ present, int p0, int p1) {
+  if (build && !build[0]) return;
+  __shared__ TileBox sgb[kSlicesPerTile];
+  __shared__ unsigned wpre[4][kTPDirectThreads / 64];
+  __shared__ unsigned long long bbase[2];
+  const int rt = blockIdx.x;
+  // every box load issued before the first barrier (one round trip)
+  TileBox bc = cb[min((int)threadIdx.x, nct - 1)];
+  if (threadIdx.x < kSlicesPerTile && rt * kTile + (int)threadIdx.x * kGroup < nrows)
+    sgb[threadIdx.x] = rg[rt * kSlicesPerTile + threadIdx.x];
+  const TileBox a = rb[rt];
+  __syncthreads();
+  for (int c0 = 0; c0 < nct; c0 += kTPDirectThreads) {
+    const int ct = c0 + (int)threadIdx.x;
+    bool kn = false, kf = false;
+    unsigned sm = 0;
+    if (c0 > 0 && ct < nct) bc = cb[ct];
+    if (ct < nct) sm = tp_classify(a, sgb, bc, rt, ct, nrows, noprune, present, p0, p1, cnt, kn, kf);
+    tp_emit<kTPDirectThreads>(kn, kf, sm, rt, ct, out, cap, cnt, icnt, wpre, bbase);
+    __syncthreads();  // wpre / bbase are rewritten by the next round
   }
 }
 
@@ -690,7 +753,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const uint2 *__restrict__ items, unsigned long long icap,
     Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
-    uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn) {
+    uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn, int diag) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
   __shared__ float4 cen[PF_WAVES][32];      //                      e e' n n'     (stage 1)
@@ -933,6 +996,10 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
           gi = (unsigned)rbase + rl;
           gj = sci[cl];
           keep = NOPRUNE ? true : pf_refine(rsp[w][rl], rv[rl], rbs[w][rl], sx[cl], sv[cl], prm);
+          // an aircraft against itself (rows = the columns [diag, diag + nrows)):
+          // never a pair (StateBasedCD.py's +1e9 I sentinel), ~40 % of the
+          // refine survivors at the 100k box otherwise
+          keep = keep && (diag < 0 || gj != (unsigned)diag + gi);
 #ifdef BSA_PF_REFINE_X2
           {  // the same test on inputs the compiler cannot prove equal: the refine's cost, measured
             float4 c2 = sx[cl];
@@ -1333,7 +1400,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
     const uint2 *__restrict__ cand, Counters *__restrict__ cnt, SoA6 hs,
     unsigned long long cap, double rpz, double hpz, double tla, int rb, int nrows,
     unsigned char *__restrict__ cflag, double *__restrict__ cpay, unsigned char *__restrict__ inconf,
-    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, unsigned *__restrict__ kb,
+    unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, uint2 *__restrict__ kb,
     int B,
     unsigned *__restrict__ rctl, const Snap *__restrict__ snap_cur, Snap *__restrict__ snap_build, int nsnap) {
   if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
@@ -1354,58 +1421,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
 #pragma unroll
     for (int q = 1; q < kCandShards; ++q) sh += (idx >= pre[q]) ? 1 : 0;
     const uint2 p = cand[(unsigned long long)sh * ccap + (idx - pre[sh])];
-    if (p.x == kCandHole) {  // an unused reserved slot (the tail of a wave's last block)
-      cflag[idx] = 0;
-      continue;
-    }
-    // home mode (perm_r == NULL, the resident sim): rows are the home slice
-    // [rb, rb + nrows) of the columns; the key's row is the home row, its
-    // column the aircraft index (so K2 orders each row's pairs by index)
-    const unsigned oi = perm_r ? perm_r[p.x] : (unsigned)rb + p.x, oj = perm_c[p.y];
     unsigned char flag = 0;
-    if (perm_r ? oi != oj : oi != p.y) {
-      PairResult o;
-      if (MODE == kExactHome) {  // the records from the state arrays (rows = columns' slice)
-        const ColRec ri = col_record(hs, hs, (int)oi), cj = col_record(hs, hs, (int)p.y);
-        o = eval_pair<false>(reinterpret_cast<const RowRec &>(ri), cj, rpz, hpz, tla);
-      } else {
-        o = eval_pair<MODE == kExactKwik>(R[p.x], C[p.y], rpz, hpz, tla);
-      }
-      flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
-      const int row = (int)oi - rb;
-      // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
-      double *rec = cpay + idx * kPayStride;
-      if (flag) rec[0] = __longlong_as_double((long long)(((unsigned long long)oi << 32) | oj));
-      if (o.conf) {
-        rec[1] = o.qdr;
-        rec[2] = o.dist;
-        rec[3] = o.tcpa;
-        rec[4] = o.tin;
-        rec[5] = o.dcpa;
-        inconf[row] = 1;
-        // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
-        // positive tcpa can raise it, and positive doubles order as integers.
-        if (o.tcpa > 0.0)
-          atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
-        if (B) {  // row bucket: the pair's column at the slot its count returned
-          const unsigned s = atomicAdd(&rowcnt[row], 1u);
-          if (s < (unsigned)B) kb[(size_t)row * B + s] = oj;
-          else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
+    int row = 0;
+    // p.x == kCandHole: an unused reserved slot (the tail of a wave's last block)
+    if (p.x != kCandHole) {
+      // home mode (perm_r == NULL, the resident sim): rows are the home slice
+      // [rb, rb + nrows) of the columns; the key's row is the home row, its
+      // column the aircraft index (so K2 orders each row's pairs by index)
+      const unsigned oi = perm_r ? perm_r[p.x] : (unsigned)rb + p.x, oj = perm_c[p.y];
+      if (perm_r ? oi != oj : oi != p.y) {
+        PairResult o;
+        if (MODE == kExactHome) {  // the records from the state arrays (rows = columns' slice)
+          const ColRec ri = col_record(hs, hs, (int)oi), cj = col_record(hs, hs, (int)p.y);
+          o = eval_pair<false>(reinterpret_cast<const RowRec &>(ri), cj, rpz, hpz, tla);
         } else {
-          atomicAdd(&rowcnt[row], 1u);
+          o = eval_pair<MODE == kExactKwik>(R[p.x], C[p.y], rpz, hpz, tla);
         }
-      }
-      if (o.los) {
-        if (B) {
-          const unsigned s = atomicAdd(&rowcnt[nrows + 1 + row], 1u);
-          if (s < (unsigned)B) kb[((size_t)nrows + row) * B + s] = oj;
-          else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
-        } else {
-          atomicAdd(&rowcnt[nrows + 1 + row], 1u);
+        flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
+        row = (int)oi - rb;
+        // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
+        double *rec = cpay + idx * kPayStride;
+        if (flag && !B) rec[0] = __longlong_as_double((long long)(((unsigned long long)oi << 32) | oj));
+        if (o.conf) {
+          rec[1] = o.qdr;
+          rec[2] = o.dist;
+          rec[3] = o.tcpa;
+          rec[4] = o.tin;
+          rec[5] = o.dcpa;
+          inconf[row] = 1;
+          // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
+          // positive tcpa can raise it, and positive doubles order as integers.
+          if (o.tcpa > 0.0)
+            atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
+          if (B) {  // row bucket: (column, candidate) at the slot its count returned
+            const unsigned s = atomicAdd(&rowcnt[row], 1u);
+            if (s < (unsigned)B) kb[(size_t)row * B + s] = make_uint2(oj, (unsigned)idx);
+            else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
+          } else {
+            atomicAdd(&rowcnt[row], 1u);
+          }
+        }
+        if (o.los) {
+          if (B) {
+            const unsigned s = atomicAdd(&rowcnt[nrows + 1 + row], 1u);
+            if (s < (unsigned)B) kb[((size_t)nrows + row) * B + s] = make_uint2(oj, (unsigned)idx);
+            else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
+          } else {
+            atomicAdd(&rowcnt[nrows + 1 + row], 1u);
+          }
         }
       }
     }
-    cflag[idx] = flag;
+    if (!B) cflag[idx] = flag;
   }
 }
 
@@ -1455,6 +1522,7 @@ struct MvpFuse {
   MvpPairIn in;
   double4 *pdv;
   uint8_t *pfl;
+  double4 *rowdv;  // k_rank_rows: each row's folded dv (mvp_fold), or NULL
 };
 
 // One lane per pair slot of the scattered lists (grid-stride over P + L, the
@@ -1476,10 +1544,7 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
                                               int *__restrict__ li, int *__restrict__ lj,
                                               unsigned long long *__restrict__ stats,
                                               unsigned long long *__restrict__ gate,
-                                              const unsigned *__restrict__ build, MvpFuse mf,
-                                              const unsigned char *__restrict__ cflag,
-                                              const unsigned *__restrict__ rowcnt, const unsigned *__restrict__ kb,
-                                              int B) {
+                                              const unsigned *__restrict__ build, MvpFuse mf) {
   const bool ovf = cand_overflow(cnt, cap);
   const unsigned P = rowoff[nrows], L = rowoff[2 * nrows + 1] - P;
   const unsigned t0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1516,51 +1581,6 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
   }
   if (ovf) return;
   const unsigned stride = gridDim.x * blockDim.x;
-  if (B) {
-    // row buckets (K1b): one lane per candidate; a pair's rank among its row's
-    // bucket (the row's columns, in any order) is its place in the segment
-    unsigned long long pre[kCandShards + 1];
-    const unsigned long long ncand = cand_prefix(cnt, cap, pre);
-    for (unsigned long long k = t0; k < ncand; k += stride) {
-      const unsigned char f = cflag[k];
-      if (!f) continue;
-      const unsigned long long kk = (unsigned long long)__double_as_longlong(cpay[k * kPayStride]);
-      const int row = (int)(kk >> 32) - rb;
-      const unsigned col = (unsigned)kk;
-      if (f & 1) {
-        const unsigned *b = kb + (size_t)row * B;
-        const unsigned c = rowcnt[row];
-        unsigned rank = 0;
-        for (unsigned y = 0; y < c; ++y) rank += (b[y] < col) ? 1u : 0u;
-        const unsigned pos = rowoff[row] + rank;
-        ci[pos] = (int)(kk >> 32);
-        cj[pos] = (int)col;
-        double pay[5];
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-          pay[q] = cpay[k * kPayStride + 1 + q];
-          out[(size_t)q * P + pos] = pay[q];
-        }
-        if (mf.pdv) {
-          double4 dv;
-          uint8_t fl;
-          mvp_pair(mf.p, mf.in, (int)(kk >> 32), (int)col, pay[0], pay[1], pay[2], pay[3], dv, fl);
-          mf.pdv[pos] = dv;
-          mf.pfl[pos] = fl;
-        }
-      }
-      if (f & 2) {
-        const unsigned *b = kb + ((size_t)nrows + row) * B;
-        const unsigned c = rowcnt[nrows + 1 + row];
-        unsigned rank = 0;
-        for (unsigned y = 0; y < c; ++y) rank += (b[y] < col) ? 1u : 0u;
-        const unsigned pos = rowoff[nrows + 1 + row] - P + rank;
-        li[pos] = (int)(kk >> 32);
-        lj[pos] = (int)col;
-      }
-    }
-    return;
-  }
   for (unsigned x = t0; x < P + L; x += stride) {
     const bool conf = x < P;
     const unsigned long long *keys = conf ? skey : lkey;
@@ -1596,6 +1616,195 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
       lj[pos] = (int)col;
     }
   }
+}
+
+// K2 with row buckets (K1b wrote each row's (column, candidate) entries in
+// any order and the pair counts of every kRankRows-row block): workgroup b
+// takes rows [b kRankRows, (b + 1) kRankRows), one per lane.  Its conflict /
+// LoS bases are the block counts before b (and P, the total, for the LoS
+// list), its rows' offsets an LDS scan of their counts -- rowoff comes out
+// exactly as the scan of the scatter path made it, without a scan launch and
+// its look-back chain.  Then the block's pairs, flattened (one lane each):
+// the row by binary search over the offsets, the pair's rank among its row's
+// bucket (the row's columns) its place in np.where's row-major order
+// (StateBasedCD.py:93-95), its payload gathered from its candidate record.
+// Block 0 / lane 0 publishes the totals as k_rank does.
+// the conflict / LoS pair counts of every kRankRows-row block (behind the
+// per-row counts: bcnt[b], bcnt[nb + b]); one wave per block, kRankRows / 64
+// rows per lane (one load round trip; an overflowed detect's sums are never
+// read: k_rank_rows checks the overflow itself)
+__global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__ rowcnt) {
+  const int nb = rank_blocks(nrows), b = blockIdx.x, lane = threadIdx.x;
+  unsigned c = 0, l = 0;
+#pragma unroll
+  for (int q = 0; q < kRankRows / 64; ++q) {
+    const int r = b * kRankRows + q * 64 + lane;
+    c += r < nrows ? rowcnt[r] : 0u;
+    l += r < nrows ? rowcnt[nrows + 1 + r] : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += (unsigned)__shfl_xor((int)c, o);
+    l += (unsigned)__shfl_xor((int)l, o);
+  }
+  if (lane == 0) {
+    rowcnt[2 * (nrows + 1) + b] = c;
+    rowcnt[2 * (nrows + 1) + nb + b] = l;
+  }
+}
+
+__global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
+                                                         unsigned *__restrict__ rowoff,
+                                                         const unsigned *__restrict__ rowcnt,
+                                                         const uint2 *__restrict__ kb, int B,
+                                                         const double *__restrict__ cpay, int rb,
+                                                         int *__restrict__ ci, int *__restrict__ cj,
+                                                         double *__restrict__ out, int *__restrict__ li,
+                                                         int *__restrict__ lj, unsigned long long *__restrict__ stats,
+                                                         unsigned long long *__restrict__ gate,
+                                                         const unsigned *__restrict__ build, MvpFuse mf) {
+  constexpr int W = kRankRows / 64;
+  __shared__ unsigned red[4][W];
+  __shared__ unsigned soff[2][kRankRows + 1];  // the block's rows' exclusive offsets (conf, LoS), + total
+  // the block's MVP pair vectors for the fold (when they fit; else through pdv / pfl)
+  __shared__ double4 sdv[kRankLds];
+  __shared__ uint8_t sfl[kRankLds];
+  const int nb = rank_blocks(nrows), b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const unsigned *bcnt = rowcnt + 2 * (nrows + 1);
+  const int r = b * kRankRows + t;
+  const unsigned c = r < nrows ? rowcnt[r] : 0u, l = r < nrows ? rowcnt[nrows + 1 + r] : 0u;
+  const bool ovf = cand_overflow(cnt, cap);
+  // P / L = all conflict / LoS pairs, cb / lb = those of the blocks before b
+  unsigned P = 0, L = 0, cb = 0, lb = 0;
+  for (int q = t; q < nb; q += kRankRows) {
+    const unsigned x = bcnt[q], y = bcnt[nb + q];
+    P += x;
+    L += y;
+    cb += q < b ? x : 0u;
+    lb += q < b ? y : 0u;
+  }
+  {
+    unsigned v[4] = {P, L, cb, lb};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      for (int o = 32; o > 0; o >>= 1) v[k] += (unsigned)__shfl_xor((int)v[k], o);
+      if (lane == 0) red[k][w] = v[k];
+    }
+  }
+  const unsigned xc = wave_incl_scan(c), xl = wave_incl_scan(l);
+  __shared__ unsigned wsum[2][W];
+  if (lane == 63) {
+    wsum[0][w] = xc;
+    wsum[1][w] = xl;
+  }
+  __syncthreads();
+  P = L = cb = lb = 0;
+  unsigned wc = 0, wl = 0, tc = 0, tl = 0;
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    P += red[0][q];
+    L += red[1][q];
+    cb += red[2][q];
+    lb += red[3][q];
+    wc += q < w ? wsum[0][q] : 0u;
+    wl += q < w ? wsum[1][q] : 0u;
+    tc += wsum[0][q];
+    tl += wsum[1][q];
+  }
+  if (b == 0 && t == 0) {
+    unsigned long long ncand = 0;  // candidates written (the shard counts include reserved, unused slots)
+    for (int q = 0; q < 32; ++q) ncand += cnt->gpart[q][1];
+    cnt->conf = ovf ? 0 : P;
+    cnt->los = ovf ? 0 : L;
+    cnt->cand = ncand;
+    unsigned long long g = 0;
+    for (int q = 0; q < 32; ++q) g += cnt->gpart[q][0];
+    cnt->groups = g;
+    const bool built = !build || build[0];  // a reused list swept nothing this detect
+    bool list_ovf = false;  // (see k_rank)
+    for (int q = 0; q < kCandShards; ++q) list_ovf |= cnt->cshard[q][0] > cap / kCandShards;
+    if (built && !list_ovf) {
+      stats[0] += cnt->groups;
+      stats[2] += cnt->tiles;
+      stats[4] += 1;
+    }
+    if (!ovf) {
+      stats[1] += ncand;
+      stats[3] += 1;
+    }
+    if (gate) {
+      gate[0] = ovf ? 1 : 0;
+      gate[1] = ovf ? 0 : P;
+    }
+  }
+  if (ovf) return;
+  const unsigned ec = wc + xc - c, el = wl + xl - l;  // exclusive, within the block
+  soff[0][t] = ec;
+  soff[1][t] = el;
+  if (t == 0) {
+    soff[0][kRankRows] = tc;
+    soff[1][kRankRows] = tl;
+  }
+  if (r < nrows) {
+    rowoff[r] = cb + ec;
+    rowoff[nrows + 1 + r] = P + lb + el;
+  }
+  if (b == nb - 1 && t == 0) {
+    rowoff[nrows] = P;
+    rowoff[2 * nrows + 1] = P + L;
+  }
+  __syncthreads();
+  const bool lds_fold = mf.rowdv && tc <= (unsigned)kRankLds;
+  for (unsigned x = t; x < tc + tl; x += kRankRows) {
+    const bool conf = x < tc;
+    const unsigned q = conf ? x : x - tc;
+    const unsigned *so = soff[conf ? 0 : 1];
+    int lo = 0, hi = kRankRows;  // the last row i with so[i] <= q (rows without pairs share their successor's offset)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (so[mid] <= q) lo = mid;
+      else hi = mid;
+    }
+    const unsigned k = q - so[lo], m = so[lo + 1] - so[lo];
+    const int row = b * kRankRows + lo;
+    const uint2 *bk = kb + ((size_t)(conf ? 0 : nrows) + row) * B;
+    const uint2 e = bk[k];
+    unsigned rank = 0;
+    for (unsigned y = 0; y < m; ++y) rank += (bk[y].x < e.x) ? 1u : 0u;
+    if (conf) {
+      const unsigned pos = cb + so[lo] + rank;
+      ci[pos] = rb + row;
+      cj[pos] = (int)e.x;
+      double pay[5];
+#pragma unroll
+      for (int f = 0; f < 5; ++f) {
+        pay[f] = cpay[(size_t)e.y * kPayStride + 1 + f];
+        out[(size_t)f * P + pos] = pay[f];
+      }
+      if (mf.pdv) {  // resident step: MVP's per-pair vector (MVP.py:33-56), folded below
+        double4 dv;
+        uint8_t fl;
+        mvp_pair(mf.p, mf.in, rb + row, (int)e.x, pay[0], pay[1], pay[2], pay[3], dv, fl);
+        if (lds_fold) {
+          sdv[so[lo] + rank] = dv;
+          sfl[so[lo] + rank] = fl;
+        } else {
+          mf.pdv[pos] = dv;
+          mf.pfl[pos] = fl;
+        }
+      }
+    } else {
+      const unsigned pos = lb + so[lo] + rank;
+      li[pos] = rb + row;
+      lj[pos] = (int)e.x;
+    }
+  }
+  // K3's fold of each row's pairs, in order (MVP.py:44-61): from LDS, or
+  // from pdv / pfl (this workgroup's stores are visible to its lanes after
+  // the barrier)
+  if (!mf.rowdv) return;
+  __syncthreads();
+  if (r < nrows)
+    mf.rowdv[r] = lds_fold ? mvp_fold(sdv, sfl, ec, ec + c) : mvp_fold(mf.pdv, mf.pfl, cb + ec, cb + ec + c);
 }
 
 // Zero the per-detect state: counters (but `tiles` unless full; with keep,
@@ -1750,7 +1959,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->inconf, (size_t)(nrows > 0 ? nrows : 1), "inconf") ||
       !ensure(c, c->tcpamax, (size_t)(nrows > 0 ? nrows : 1) * 8, "tcpamax") ||
       !ensure(c, c->workq, kWorkShards * kWorkStride * 8, "work counters") ||
-      !ensure(c, c->rowcnt, (size_t)(2 * (nrows + 1)) * 4, "row counts") ||
+      !ensure(c, c->rowcnt, (size_t)rowcnt_words((int)nrows) * 4, "row counts") ||
       !ensure(c, c->rowoff, (size_t)(2 * (nrows + 1)) * 4, "row offsets"))
     return -1;
   const bool distinct = c->has_intruder;
@@ -1811,7 +2020,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // K0z: zero the per-detect state (launched once the reuse decision is known)
   auto zero = [&](bool keep, unsigned *rctl, int rforce, bool tiles = false) -> int {
     const int64_t m = std::max<int64_t>(2 * (nrows + 1), 256);
-    hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>(blocks_for(m, 256), 1024)), dim3(256), 0,
+    hipLaunchKernelGGL(k_zero, dim3((unsigned)std::min<int64_t>(blocks_for(m, 256 * 4), 256)), dim3(256), 0,
                        c->stream, (int)nrows, 1, keep ? 1 : 0, rctl, rforce, dcnt,
                        (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
                        (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p, (int)n,
@@ -2004,10 +2213,17 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
   // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
   const unsigned long long icap = (unsigned long long)ntp * kSlicesPerTile;  // items: 8 slices per tile pair
-  hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
-                     nrt, nct, (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune,
-                     (uint2 *)c->tilepairs.p, icap, dcnt, (unsigned long long *)c->workq.p, build,
-                     halo ? halo_present(c) : nullptr, a0, a1);
+  static const bool tp_super = getenv("BSA_TP_SUPER") && atoi(getenv("BSA_TP_SUPER")) == 1;  // (A/B)
+  if (nct <= kTPDirectMax && !tp_super)
+    hipLaunchKernelGGL(k_tilepairs_direct, dim3((unsigned)nrt), dim3(kTPDirectThreads), 0, c->stream, nrt, nct,
+                       (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
+                       icap, dcnt, (unsigned long long *)c->workq.p, build, halo ? halo_present(c) : nullptr, a0,
+                       a1);
+  else
+    hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
+                       nrt, nct, (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune,
+                       (uint2 *)c->tilepairs.p, icap, dcnt, (unsigned long long *)c->workq.p, build,
+                       halo ? halo_present(c) : nullptr, a0, a1);
   BSA_HIP(c, hipGetLastError());
   if (mark(1)) return -1;
 
@@ -2041,6 +2257,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     c->trace_bytes = need;
   }
 #endif
+  // rows sharing the column records: row i is column roff + i (its diagonal)
+  const int diag = shared ? (int)roff : -1;
   const unsigned pf_grid = (unsigned)std::max<long long>(
       kWorkShards, std::min<long long>(ntp * PF_ITEMS_PER_TILE / PF_WAVES + 1, 256 * PF_BLOCKS_PER_CU));
   if (noprune)
@@ -2048,20 +2266,20 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag);
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count, one
   // resident round (4 workgroups per CU at its register budget)
   // K2 row buckets (B pairs per row per list; a fuller row retries wider, then without)
   const int B = c->k2_bucket;
-  if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * 4, "K2 row buckets")) return -1;
+  if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * sizeof(uint2), "K2 row buckets")) return -1;
   {
     const auto KEX = !recs ? k_exact<kExactHome> : (kwik ? k_exact<kExactKwik> : k_exact<kExactRec>);
     hipLaunchKernelGGL(KEX, dim3(256 * 4), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
@@ -2069,16 +2287,18 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (int)nrows,
                        (unsigned char *)c->cflag.p, (double *)c->cpay.p,
                        (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
-                       (unsigned *)c->rowcnt.p, (unsigned *)c->kbuck.p, B,
+                       (unsigned *)c->rowcnt.p, (uint2 *)c->kbuck.p, B,
                        reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
                        (const Snap *)c->snap_cur.p, (Snap *)c->snap_build.p, (int)n);
   }
   BSA_HIP(c, hipGetLastError());
   if (mark(3)) return -1;
-  // ---- K2: row offsets, scatter into row segments, per-row rank + gather
-  const int nscan = (int)(2 * (nrows + 1));
-  if (scan_excl(c, (const unsigned *)c->rowcnt.p, (unsigned *)c->rowoff.p, nscan)) return -1;
-  if (!B) {  // (row buckets: k_rank reads K1b's buckets, no scatter)
+  // ---- K2: row offsets and the pairs in row-major order: from K1b's row
+  // buckets (k_rank_rows, one launch), or scan + scatter into row segments +
+  // per-segment rank (bucket width 0)
+  if (!B) {
+    const int nscan = (int)(2 * (nrows + 1));
+    if (scan_excl(c, (const unsigned *)c->rowcnt.p, (unsigned *)c->rowoff.p, nscan)) return -1;
     hipLaunchKernelGGL(k_scatter, dim3(256 * 4), dim3(256), 0, c->stream, (const Counters *)dcnt, cap, (int)rb,
                        (int)nrows, (const unsigned char *)c->cflag.p, (const double *)c->cpay.p,
                        (const unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
@@ -2088,6 +2308,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   }
   MvpFuse mf{};
   c->fuse_done = false;
+  c->fuse_rowdv = false;
   if (c->fuse_mvp) {
     if (!ensure(c, c->mvp_pdv, std::max<unsigned long long>(cap, 1) * sizeof(double4), "mvp pair dv") ||
         !ensure(c, c->mvp_pfl, std::max<unsigned long long>(cap, 1), "mvp pair flags"))
@@ -2098,14 +2319,28 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     mf.pdv = (double4 *)c->mvp_pdv.p;
     mf.pfl = (uint8_t *)c->mvp_pfl.p;
     c->fuse_done = true;
+    if (B) {  // K2 also folds each row's vectors (MvpIn::rowdv)
+      if (!ensure(c, c->mvp_rowdv, (size_t)std::max<int64_t>(nrows, 1) * sizeof(double4), "mvp row dv")) return -1;
+      mf.rowdv = (double4 *)c->mvp_rowdv.p;
+      c->fuse_rowdv = true;
+    }
   }
-  hipLaunchKernelGGL(k_rank, dim3(256 * 4), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
-                     (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey2.p,
-                     (const unsigned *)c->cval2.p, (const double *)c->cpay.p,
-                     (const unsigned long long *)c->lkey2.p, (int)rb, (int *)c->out_ci.p, (int *)c->out_cj.p,
-                     (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
-                     (unsigned long long *)c->stats.p, gate, build, mf, (const unsigned char *)c->cflag.p,
-                     (const unsigned *)c->rowcnt.p, (const unsigned *)c->kbuck.p, B);
+  if (B) {
+    hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows)), dim3(64), 0, c->stream, (int)nrows,
+                       (unsigned *)c->rowcnt.p);
+    hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)rank_blocks((int)nrows)), dim3(kRankRows), 0, c->stream,
+                       (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p, (const unsigned *)c->rowcnt.p,
+                       (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb, (int *)c->out_ci.p,
+                       (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
+                       (unsigned long long *)c->stats.p, gate, build, mf);
+  } else {
+    hipLaunchKernelGGL(k_rank, dim3(256 * 4), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
+                       (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey2.p,
+                       (const unsigned *)c->cval2.p, (const double *)c->cpay.p,
+                       (const unsigned long long *)c->lkey2.p, (int)rb, (int *)c->out_ci.p, (int *)c->out_cj.p,
+                       (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
+                       (unsigned long long *)c->stats.p, gate, build, mf);
+  }
   BSA_HIP(c, hipGetLastError());
   if (mark(4)) return -1;
   c->ev_valid = c->ev_valid || timed;

@@ -72,14 +72,26 @@ static bool barrier(Ctx *c) {
   return true;
 }
 
+// the members' `done` events as they are now (under the lock: a rank that
+// has not joined yet -- its thread still before bsa_comm_init_group -- has
+// none, and has read no slot either, so there is nothing to wait for)
+static void done_events(Group *g, hipEvent_t *ev) {
+  std::lock_guard<std::mutex> lk(g->m);
+  for (int q = 0; q < g->n; ++q) ev[q] = g->done[q];
+}
+
 // rank r publishes `bytes` from device `src` into its slot (after every rank
 // finished reading the previous collective's slots), then waits for all slots
 static int publish(Ctx *c, const void *src, size_t bytes) {
   Group *g = c->group;
   const int r = c->rank;
-  for (int q = 0; q < g->n; ++q) BSA_HIP(c, hipStreamWaitEvent(c->stream, g->done[q], 0));
+  hipEvent_t done[kMaxGroup];
+  done_events(g, done);
+  for (int q = 0; q < g->n; ++q)
+    if (done[q]) BSA_HIP(c, hipStreamWaitEvent(c->stream, done[q], 0));
   if (g->slot[r].bytes < bytes) {
-    for (int q = 0; q < g->n; ++q) BSA_HIP(c, hipEventSynchronize(g->done[q]));
+    for (int q = 0; q < g->n; ++q)
+      if (done[q]) BSA_HIP(c, hipEventSynchronize(done[q]));
     if (!ensure(c, g->slot[r], bytes, "group slot")) return -1;
   }
   if (bytes) BSA_HIP(c, hipMemcpyAsync(g->slot[r].p, src, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -367,10 +379,16 @@ int bsa_comm_init_group(bsa_ctx *cc, bsa_group *g, int rank) {
     if (g->ctx[rank]) return bsa::fail(c, "group rank %d already joined", rank);
     g->ctx[rank] = c;
   }
-  BSA_HIP(c, hipEventCreateWithFlags(&g->pub[rank], hipEventDisableTiming));
-  BSA_HIP(c, hipEventCreateWithFlags(&g->done[rank], hipEventDisableTiming));
-  BSA_HIP(c, hipEventRecord(g->pub[rank], c->stream));
-  BSA_HIP(c, hipEventRecord(g->done[rank], c->stream));
+  hipEvent_t pub = nullptr, done = nullptr;
+  BSA_HIP(c, hipEventCreateWithFlags(&pub, hipEventDisableTiming));
+  BSA_HIP(c, hipEventCreateWithFlags(&done, hipEventDisableTiming));
+  BSA_HIP(c, hipEventRecord(pub, c->stream));
+  BSA_HIP(c, hipEventRecord(done, c->stream));
+  {  // published under the lock (publish() of a rank already running reads them)
+    std::lock_guard<std::mutex> lk(g->m);
+    g->pub[rank] = pub;
+    g->done[rank] = done;
+  }
   c->group = g;
   c->nranks = g->n;
   c->rank = rank;

@@ -198,7 +198,7 @@ void bsa_destroy(bsa_ctx *c) {
   bsa::DevBuf *all[] = {&c->rowrec, &c->colrec, &c->pfrow, &c->pfcol, &c->counters, &c->cand,
                         &c->ckey, &c->cval, &c->ckey2, &c->cval2, &c->cpay, &c->kbuck, &c->lkey, &c->lkey2,
                         &c->out_ci, &c->out_cj, &c->out_li, &c->out_lj, &c->out_pay, &c->inconf,
-                        &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage, &c->mvp_pdv, &c->mvp_pfl,
+                        &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage, &c->mvp_pdv, &c->mvp_pfl, &c->mvp_rowdv,
                         &c->pfvrow, &c->pfvcol, &c->pfprow, &c->pfpcol, &c->key_r, &c->idx_r, &c->key_r2, &c->perm_r,
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
                         &c->gbox_r, &c->gbox_c, &c->sbox_c, &c->workq, &c->rowcnt, &c->rowoff,

@@ -17,10 +17,34 @@ __device__ __forceinline__ double np_min(double a, double b) {
   return (a <= b || a != a) ? a : b;
 }
 
+// fmod(a, 360) without the library's loop, exactly fmod's value: for
+// 360 <= |a| < 360 2^30, q = trunc(|a| / 360) is the true quotient or one
+// off (the division's error is < 2^-23 of one), q 360 is exact (9 significant
+// bits times < 2^30) and |a| - q 360 is exact by Sterbenz (q >= 1 and |a| in
+// [q 360 / 2, 2 q 360] for the true q and its neighbours that are tried), so
+// the remainder of the true quotient comes out exactly; fmod's sign is a's.
+// Anything else (huge, inf, NaN) goes to fmod.
+__device__ __forceinline__ double fmod360(double a) {
+  const double aa = fabs(a);
+  if (aa < 360.0) return a;
+  if (!(aa < 386547056640.0)) return fmod(a, 360.0);  // 360 * 2^30
+  double q = trunc(aa / 360.0);
+  double r = aa - q * 360.0;
+  if (r < 0.0) {
+    q -= 1.0;
+    r = aa - q * 360.0;
+  } else if (r >= 360.0) {
+    q += 1.0;
+    r = aa - q * 360.0;
+  }
+  return copysign(r, a);
+}
+
 // numpy.remainder for float64 (npy_divmod semantics), b > 0.  fmod is exact
-// and returns a itself when |a| < b, so that common case skips fmod's loop.
+// and returns a itself when |a| < b, so that common case skips fmod's loop
+// (and b = 360 takes fmod360).
 __device__ __forceinline__ double np_rem(double a, double b) {
-  double mod = (fabs(a) < b) ? a : fmod(a, b);
+  double mod = (fabs(a) < b) ? a : (b == 360.0 ? fmod360(a) : fmod(a, b));
   if (mod != 0.0) {
     if ((b < 0) != (mod < 0)) mod += b;
   } else {

@@ -211,7 +211,7 @@ struct Ctx {
   size_t trace_bytes = 0;
 
   // MVP / kinematics staging (host-buffer entry points)
-  DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl;
+  DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl, mvp_rowdv;
 
   // multi-GPU: comm is an ncclComm_t (one process per GPU) or group an
   // in-process group of contexts (bsa_comm.hip); at most one is set
@@ -284,6 +284,7 @@ struct Ctx {
   const bsa_mvp_params *fuse_mvp = nullptr;
   const double *fuse_gse = nullptr, *fuse_gsn = nullptr, *fuse_vs = nullptr, *fuse_alt = nullptr;
   bool fuse_done = false;  // the last detect_enqueue produced the per-pair vectors
+  bool fuse_rowdv = false;  // ... and folded them per row (k_rank_rows: mvp_rowdv)
 
   // standalone geo matrices (bsa_geo.hip)
   DevBuf geo_in, geo_pts, geo_out;

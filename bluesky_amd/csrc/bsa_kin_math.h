@@ -9,6 +9,7 @@
 // Every expression keeps numpy's evaluation order (compile with
 // -ffp-contract=off).
 #pragma once
+#include "bsa_geo_math.h"
 #include "bsa_internal.h"
 
 namespace bsa {
@@ -64,7 +65,7 @@ __device__ __forceinline__ double npsign(double x) {
 }
 // numpy.remainder for float64 (npy_divmod semantics)
 __device__ __forceinline__ double nprem(double a, double b) {
-  double mod = fmod(a, b);
+  double mod = b == 360.0 ? fmod360(a) : fmod(a, b);
   if (mod != 0.0) {
     if ((b < 0) != (mod < 0)) mod += b;
   } else {

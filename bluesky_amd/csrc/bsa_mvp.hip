@@ -95,7 +95,7 @@ int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned 
     BSA_HIP(c, hipGetLastError());
     seg = (const unsigned *)c->seg.p;
   }
-  MvpIn in;
+  MvpIn in{};
   in.ci = (const int *)c->out_ci.p;
   in.cj = (const int *)c->out_cj.p;
   in.pay = (const double *)c->out_pay.p;
@@ -122,6 +122,8 @@ int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned 
   in.o_tsolv = d.o_tsolv;
   in.pdv = (double4 *)c->mvp_pdv.p;
   in.pfl = (uint8_t *)c->mvp_pfl.p;
+  // K2 of the same detect folded each row's vectors (k_rank_rows)
+  in.rowdv = pairs_done && c->fuse_rowdv && resolve ? (const double4 *)c->mvp_rowdv.p : nullptr;
   in.gate = gate;
   in.sticky = sticky;
   in.inconf = inconf;

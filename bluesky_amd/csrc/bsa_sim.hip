@@ -54,57 +54,15 @@ struct PrepArgs {
   int mid, rec, n;
 };
 
-// one row of K4' (below)
+// one row of K4' (below).  The row's state is loaded before K3's part runs
+// (the loads overlap; K3 writes only the ASAS targets / asas.active, which
+// this lane then takes from its registers, MvpRowOut), so the row's memory
+// latency is paid about once instead of along a chain of dependent accesses.
 template <bool FUSE, bool PREP>
 __device__ __forceinline__ void pilot_kin_row(int rb, int k, double simdt, int winddim, double vwn, double vwe,
                                               const WindField &wf, const SimDev &d, const MvpIn &mv,
                                               const bsa_mvp_params &mp, const PrepArgs &pa) {
-  if (FUSE) mvp_row(rb, k - rb, mp, mv);
-  if (winddim == 2) {  // pilot.py:32 and traffic.py:463 read the field at the same pre-step position
-    kin::windfield_2d(wf, d.lat[k], d.lon[k], vwn, vwe);
-    winddim = 1;
-  }
-  const bool act = d.active[k] != 0;
-  const double ptrk = act ? d.atrk[k] : d.aptrk[k];   // pilot.py:41
   kin::In s;
-  double asastas = d.atas[k];                         // pilot.py:37-38: no wind, GS = TAS
-  if (winddim > 0) {                                  // pilot.py:31-35: ASAS GS -> TAS
-    const double atas = d.atas[k], atrk = d.atrk[k];
-    const double asastasnorth = atas * cos(atrk * kD2R) - vwn;
-    const double asastaseast = atas * sin(atrk * kD2R) - vwe;
-    asastas = sqrt(asastasnorth * asastasnorth + asastaseast * asastaseast);
-  }
-  s.ptas = act ? asastas : d.aptas[k];                // pilot.py:42
-  s.palt = act ? d.aalt[k] : d.apalt[k];              // pilot.py:43
-  s.pvs = fabs(act ? d.avs[k] : d.apvs[k]);           // pilot.py:44,48
-  if (winddim > 0) {                                  // pilot.py:51-61: wind correction
-    const double Vw = sqrt(vwn * vwn + vwe * vwe);
-    const double winddir = atan2(vwe, vwn);
-    const double drift = ptrk * kD2R - winddir;
-    const double steer = asin(kin::npmin(1.0, kin::npmax(-1.0, Vw * sin(drift) / kin::npmax(0.001, d.tas[k]))));
-    s.phdg = kin::nprem(ptrk + steer * kR2D, 360.);
-  } else {
-    s.phdg = kin::nprem(ptrk, 360.);                  // pilot.py:63
-  }
-  s.accel = d.accel[k];
-  if (d.atm) {  // Traffic.update's first statement: p, rho, Temp = vatmos(alt) (traffic.py:389)
-    double p, rho, T;
-    kin::vatmos(d.alt[k], p, rho, T);
-    d.atm[k] = p;
-    d.atm[d.n + k] = rho;
-    d.atm[2 * d.n + k] = T;
-  }
-  if (d.ptab) {  // OpenAP.update (perfoap.py:115-131) on the pre-step state, then applylimits
-    const double *row = d.ptab + (size_t)d.ptype[k] * kin::kPerfCols;
-    const int ph = kin::openap_phase(row[22], d.vs[k], d.alt[k]);
-    d.phase[k] = (uint8_t)ph;
-    kin::openap_limits(kin::openap_envelope(row, ph), d.ax[k], s.ptas, s.pvs, s.palt);
-    s.accel = ph == kin::kPhaseGD ? 2.0 : 0.5;  // OpenAP.acceleration (perfoap.py:271-280)
-  } else if (d.env) {  // Pilot.applylimits (pilot.py:65-68, OpenAP), traffic.py:404
-    const kin::Envelope e{d.env[k], d.env[d.n + k], d.env[2 * d.n + k], d.env[3 * d.n + k],
-                          d.env[4 * d.n + k], d.env[5 * d.n + k]};
-    kin::openap_limits(e, d.ax[k], s.ptas, s.pvs, s.palt);
-  }
   s.tas = d.tas[k];
   s.hdg = d.hdg[k];
   s.alt = d.alt[k];
@@ -113,6 +71,62 @@ __device__ __forceinline__ void pilot_kin_row(int rb, int k, double simdt, int w
   s.lon = d.lon[k];
   s.bank = d.bank[k];
   s.eps = d.eps[k];
+  s.accel = d.accel[k];
+  const double aptrk = d.aptrk[k], aptas = d.aptas[k], apalt = d.apalt[k], apvs = d.apvs[k];
+  double atrk = d.atrk[k], atas = d.atas[k], avs = d.avs[k], aalt = d.aalt[k];
+  bool act = d.active[k] != 0;
+  const double ax0 = (d.ptab || d.env) ? d.ax[k] : 0.0;
+  if (FUSE) {
+    const MvpRowOut o = mvp_row(rb, k - rb, mp, mv);
+    if (o.act_valid) act = o.active != 0;
+    if (o.valid) {
+      atrk = o.trk;
+      atas = o.tas;
+      avs = o.vs;
+      aalt = o.alt;
+    }
+  }
+  if (winddim == 2) {  // pilot.py:32 and traffic.py:463 read the field at the same pre-step position
+    kin::windfield_2d(wf, s.lat, s.lon, vwn, vwe);
+    winddim = 1;
+  }
+  const double ptrk = act ? atrk : aptrk;             // pilot.py:41
+  double asastas = atas;                              // pilot.py:37-38: no wind, GS = TAS
+  if (winddim > 0) {                                  // pilot.py:31-35: ASAS GS -> TAS
+    const double asastasnorth = atas * cos(atrk * kD2R) - vwn;
+    const double asastaseast = atas * sin(atrk * kD2R) - vwe;
+    asastas = sqrt(asastasnorth * asastasnorth + asastaseast * asastaseast);
+  }
+  s.ptas = act ? asastas : aptas;                     // pilot.py:42
+  s.palt = act ? aalt : apalt;                        // pilot.py:43
+  s.pvs = fabs(act ? avs : apvs);                     // pilot.py:44,48
+  if (winddim > 0) {                                  // pilot.py:51-61: wind correction
+    const double Vw = sqrt(vwn * vwn + vwe * vwe);
+    const double winddir = atan2(vwe, vwn);
+    const double drift = ptrk * kD2R - winddir;
+    const double steer = asin(kin::npmin(1.0, kin::npmax(-1.0, Vw * sin(drift) / kin::npmax(0.001, s.tas))));
+    s.phdg = kin::nprem(ptrk + steer * kR2D, 360.);
+  } else {
+    s.phdg = kin::nprem(ptrk, 360.);                  // pilot.py:63
+  }
+  if (d.atm) {  // Traffic.update's first statement: p, rho, Temp = vatmos(alt) (traffic.py:389)
+    double p, rho, T;
+    kin::vatmos(s.alt, p, rho, T);
+    d.atm[k] = p;
+    d.atm[d.n + k] = rho;
+    d.atm[2 * d.n + k] = T;
+  }
+  if (d.ptab) {  // OpenAP.update (perfoap.py:115-131) on the pre-step state, then applylimits
+    const double *row = d.ptab + (size_t)d.ptype[k] * kin::kPerfCols;
+    const int ph = kin::openap_phase(row[22], s.vs, s.alt);
+    d.phase[k] = (uint8_t)ph;
+    kin::openap_limits(kin::openap_envelope(row, ph), ax0, s.ptas, s.pvs, s.palt);
+    s.accel = ph == kin::kPhaseGD ? 2.0 : 0.5;  // OpenAP.acceleration (perfoap.py:271-280)
+  } else if (d.env) {  // Pilot.applylimits (pilot.py:65-68, OpenAP), traffic.py:404
+    const kin::Envelope e{d.env[k], d.env[d.n + k], d.env[2 * d.n + k], d.env[3 * d.n + k],
+                          d.env[4 * d.n + k], d.env[5 * d.n + k]};
+    kin::openap_limits(e, ax0, s.ptas, s.pvs, s.palt);
+  }
   const kin::Out o = kin::step(s, simdt, winddim, vwn, vwe);
   d.tas[k] = o.tas;
   d.hdg[k] = o.hdg;
