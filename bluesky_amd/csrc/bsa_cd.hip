@@ -185,7 +185,7 @@ constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
 // counting them with atomics, one per wave and block, cost 12 us at the 100k
 // box: the per-block words were hit by every wave of a block's rows at once.)
 constexpr int kRankRows = 512;
-constexpr int kRankLds = 1536;  // pairs per block folded from LDS (54 KB: 2 blocks per CU)
+constexpr int kRankLds = 1536;  // pairs per block folded from LDS (67 KB: 2 blocks per CU)
 __host__ __device__ __forceinline__ int rank_blocks(int nrows) { return (nrows + kRankRows - 1) / kRankRows; }
 __host__ __device__ __forceinline__ int rowcnt_words(int nrows) { return 2 * (nrows + 1) + 2 * rank_blocks(nrows); }
 
@@ -547,23 +547,33 @@ __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
     int nrt, int nct, int nrows, const TileBox *__restrict__ rb, const TileBox *__restrict__ rg,
     const TileBox *__restrict__ cb, int noprune, uint2 *__restrict__ out, unsigned long long cap,
     Counters *__restrict__ cnt, unsigned long long *__restrict__ icnt, const unsigned *__restrict__ build,
-    const uint8_t *__restrict__ present, int p0, int p1) {
+    const uint8_t *__restrict__ present, int p0, int p1, const TileBox *__restrict__ gbc) {
   if (build && !build[0]) return;
   __shared__ TileBox sgb[kSlicesPerTile];
   __shared__ unsigned wpre[4][kTPDirectThreads / 64];
   __shared__ unsigned long long bbase[2];
   const int rt = blockIdx.x;
+  // gbc (the resident step's prepped detect, no K0z launch): the tile boxes
+  // from the group boxes, as tile_from_groups would have written them (the
+  // rows are the columns then, so the row groups are the column groups)
+  auto tile_of = [&](int t) {
+    const int ng = (nrows + kGroup - 1) / kGroup;  // (all rows detected: nrows = n)
+    TileBox u = t * kGroupsPerTile < ng ? gbc[t * kGroupsPerTile] : empty_box();
+    for (int q = 1; q < kGroupsPerTile; ++q)
+      u = box_union(u, t * kGroupsPerTile + q < ng ? gbc[t * kGroupsPerTile + q] : empty_box());
+    return u;
+  };
   // every box load issued before the first barrier (one round trip)
-  TileBox bc = cb[min((int)threadIdx.x, nct - 1)];
+  TileBox bc = gbc ? tile_of(min((int)threadIdx.x, nct - 1)) : cb[min((int)threadIdx.x, nct - 1)];
   if (threadIdx.x < kSlicesPerTile && rt * kTile + (int)threadIdx.x * kGroup < nrows)
     sgb[threadIdx.x] = rg[rt * kSlicesPerTile + threadIdx.x];
-  const TileBox a = rb[rt];
+  const TileBox a = gbc ? tile_of(rt) : rb[rt];
   __syncthreads();
   for (int c0 = 0; c0 < nct; c0 += kTPDirectThreads) {
     const int ct = c0 + (int)threadIdx.x;
     bool kn = false, kf = false;
     unsigned sm = 0;
-    if (c0 > 0 && ct < nct) bc = cb[ct];
+    if (c0 > 0 && ct < nct) bc = gbc ? tile_of(ct) : cb[ct];
     if (ct < nct) sm = tp_classify(a, sgb, bc, rt, ct, nrows, noprune, present, p0, p1, cnt, kn, kf);
     tp_emit<kTPDirectThreads>(kn, kf, sm, rt, ct, out, cap, cnt, icnt, wpre, bbase);
     __syncthreads();  // wpre / bbase are rewritten by the next round
@@ -1431,12 +1441,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
       const unsigned oi = perm_r ? perm_r[p.x] : (unsigned)rb + p.x, oj = perm_c[p.y];
       if (perm_r ? oi != oj : oi != p.y) {
         PairResult o;
+#ifdef BSA_K1B_NOMATH  // diagnostic build (timing of K1b's memory chain alone; results are wrong)
+        {
+          const RowRec rr = R[p.x];
+          const ColRec cc = C[p.y];
+          o = PairResult{false, false, rr.lat, cc.lat, rr.lon, cc.lon, 0.0};
+        }
+#else
         if (MODE == kExactHome) {  // the records from the state arrays (rows = columns' slice)
           const ColRec ri = col_record(hs, hs, (int)oi), cj = col_record(hs, hs, (int)p.y);
           o = eval_pair<false>(reinterpret_cast<const RowRec &>(ri), cj, rpz, hpz, tla);
         } else {
           o = eval_pair<MODE == kExactKwik>(R[p.x], C[p.y], rpz, hpz, tla);
         }
+#endif
+#ifdef BSA_K1B_NOATOM  // diagnostic build (K1b without its per-row count atomics; results are wrong)
+        {
+          double *rq = cpay + idx * kPayStride;
+          rq[1] = o.qdr;
+          rq[2] = o.dist;
+          rq[3] = o.tcpa;
+          rq[4] = o.tin;
+          rq[5] = o.dcpa + (o.conf ? 1.0 : 0.0) + (o.los ? 2.0 : 0.0);
+        }
+        o.conf = o.los = false;
+#endif
         flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
         row = (int)oi - rb;
         // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
@@ -1448,11 +1477,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
           rec[3] = o.tcpa;
           rec[4] = o.tin;
           rec[5] = o.dcpa;
-          inconf[row] = 1;
-          // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
-          // positive tcpa can raise it, and positive doubles order as integers.
-          if (o.tcpa > 0.0)
-            atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
+          if (!B) {  // (row buckets: k_rank_rows writes both per row)
+            inconf[row] = 1;
+            // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
+            // positive tcpa can raise it, and positive doubles order as integers.
+            if (o.tcpa > 0.0)
+              atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
+          }
           if (B) {  // row bucket: (column, candidate) at the slot its count returned
             const unsigned s = atomicAdd(&rowcnt[row], 1u);
             if (s < (unsigned)B) kb[(size_t)row * B + s] = make_uint2(oj, (unsigned)idx);
@@ -1654,24 +1685,41 @@ __global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__
 
 __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
                                                          unsigned *__restrict__ rowoff,
-                                                         const unsigned *__restrict__ rowcnt,
+                                                         unsigned *__restrict__ rowcnt,
                                                          const uint2 *__restrict__ kb, int B,
                                                          const double *__restrict__ cpay, int rb,
                                                          int *__restrict__ ci, int *__restrict__ cj,
                                                          double *__restrict__ out, int *__restrict__ li,
                                                          int *__restrict__ lj, unsigned long long *__restrict__ stats,
                                                          unsigned long long *__restrict__ gate,
-                                                         const unsigned *__restrict__ build, MvpFuse mf) {
+                                                         const unsigned *__restrict__ build, MvpFuse mf,
+                                                         unsigned char *__restrict__ inconf,
+                                                         unsigned long long *__restrict__ tcpamax_bits,
+                                                         Counters *__restrict__ cnext,
+                                                         unsigned long long *__restrict__ wnext) {
   constexpr int W = kRankRows / 64;
   __shared__ unsigned red[4][W];
   __shared__ unsigned soff[2][kRankRows + 1];  // the block's rows' exclusive offsets (conf, LoS), + total
   // the block's MVP pair vectors for the fold (when they fit; else through pdv / pfl)
   __shared__ double4 sdv[kRankLds];
   __shared__ uint8_t sfl[kRankLds];
+  __shared__ double stc[kRankLds];  // ... and their tcpa (tcpamax)
   const int nb = rank_blocks(nrows), b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const unsigned *bcnt = rowcnt + 2 * (nrows + 1);
   const int r = b * kRankRows + t;
   const unsigned c = r < nrows ? rowcnt[r] : 0u, l = r < nrows ? rowcnt[nrows + 1 + r] : 0u;
+  // the next detect's per-row counts and counters start at zero (its K0z
+  // launch is skipped, detect_enqueue): this block's counts are read, the
+  // next detect's counter block (cnext / wnext, double-buffered) is idle
+  if (r < nrows) {
+    rowcnt[r] = 0u;
+    rowcnt[nrows + 1 + r] = 0u;
+  }
+  if (b == 0) {
+    constexpr int kWords = (int)(sizeof(Counters) / 8);
+    for (int k = t; k < kWords; k += kRankRows) reinterpret_cast<unsigned long long *>(cnext)[k] = 0ull;
+    for (int k = t; k < kWorkShards * kWorkStride; k += kRankRows) wnext[k] = 0ull;
+  }
   const bool ovf = cand_overflow(cnt, cap);
   // P / L = all conflict / LoS pairs, cb / lb = those of the blocks before b
   unsigned P = 0, L = 0, cb = 0, lb = 0;
@@ -1753,7 +1801,8 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
     rowoff[2 * nrows + 1] = P + L;
   }
   __syncthreads();
-  const bool lds_fold = mf.rowdv && tc <= (unsigned)kRankLds;
+  const bool lds = tc <= (unsigned)kRankLds;  // the block's conflict pairs fit the LDS arrays
+  const bool lds_fold = mf.rowdv && lds;
   for (unsigned x = t; x < tc + tl; x += kRankRows) {
     const bool conf = x < tc;
     const unsigned q = conf ? x : x - tc;
@@ -1780,6 +1829,7 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
         pay[f] = cpay[(size_t)e.y * kPayStride + 1 + f];
         out[(size_t)f * P + pos] = pay[f];
       }
+      if (lds) stc[so[lo] + rank] = pay[2];
       if (mf.pdv) {  // resident step: MVP's per-pair vector (MVP.py:33-56), folded below
         double4 dv;
         uint8_t fl;
@@ -1798,12 +1848,22 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
       lj[pos] = (int)e.x;
     }
   }
-  // K3's fold of each row's pairs, in order (MVP.py:44-61): from LDS, or
-  // from pdv / pfl (this workgroup's stores are visible to its lanes after
-  // the barrier)
-  if (!mf.rowdv) return;
+  // per row (this workgroup's stores are visible to its lanes after the
+  // barrier): inconf = any conflict (StateBasedCD.py:89), tcpamax =
+  // max_j(tcpa * swconfl) (:90) -- +0 or the largest positive tcpa, as K1b's
+  // atomics on the bit patterns made it -- and K3's fold of the row's pairs,
+  // in order (MVP.py:44-61), from LDS or from pdv / pfl
   __syncthreads();
-  if (r < nrows)
+  if (r >= nrows) return;
+  inconf[r] = c ? 1 : 0;
+  unsigned long long tm = 0ull;
+  for (unsigned k = 0; k < c; ++k) {
+    const double tq = lds ? stc[ec + k] : out[(size_t)2 * P + cb + ec + k];
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(tq);
+    if (tq > 0.0 && bits > tm) tm = bits;
+  }
+  tcpamax_bits[r] = tm;
+  if (mf.rowdv)
     mf.rowdv[r] = lds_fold ? mvp_fold(sdv, sfl, ec, ec + c) : mvp_fold(mf.pdv, mf.pfl, cb + ec, cb + ec + c);
 }
 
@@ -1955,6 +2015,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   c->last_flags = flags;
   c->last_conf = c->last_los = c->last_cand = 0;
   if (!ensure(c, c->counters, sizeof(Counters), "counters") ||
+      !ensure(c, c->counters2, sizeof(Counters), "next counters") ||
+      !ensure(c, c->workq2, kWorkShards * kWorkStride * 8, "next work counters") ||
       !ensure(c, c->stats, 8 * 8, "detect statistics") ||
       !ensure(c, c->inconf, (size_t)(nrows > 0 ? nrows : 1), "inconf") ||
       !ensure(c, c->tcpamax, (size_t)(nrows > 0 ? nrows : 1) * 8, "tcpamax") ||
@@ -2006,6 +2068,19 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        c->sim_prep_key[0] == rpz && c->sim_prep_key[1] == hpz && c->sim_prep_key[2] == tla &&
                        c->sim_prep_key[3] == (double)mid && c->sim_prep_n == n;
   c->sim_prepped = false;
+  // K0z skipped: the last detect's K2 (k_rank_rows) zeroed this detect's
+  // counter block (double-buffered), dequeue words and per-row counts, and
+  // writes inconf / tcpamax of every row itself; the prepped tile boxes are
+  // derived from the group boxes by K0d (direct form only)
+  static const bool tp_super = getenv("BSA_TP_SUPER") && atoi(getenv("BSA_TP_SUPER")) == 1;  // (A/B)
+  static const bool zero_env = getenv("BSA_K0Z") && atoi(getenv("BSA_K0Z")) == 1;           // (A/B)
+  const bool nozero = prepped && !zero_env && !tp_super && c->k2_bucket > 0 && c->zeroed_rows == nrows &&
+                      (n + kTile - 1) / kTile <= kTPDirectMax;
+  c->zeroed_rows = -1;
+  if (nozero) {
+    std::swap(c->counters, c->counters2);
+    std::swap(c->workq, c->workq2);
+  }
   // stage events of this detect: only one detect in ev_every is timed (each
   // record costs a ~5 us bubble before the next kernel, bsa_set_timing_sample)
   hipEvent_t *ev = nullptr;
@@ -2176,7 +2251,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                   {hp.zn[0], hp.zn[1], hp.zn[2]}};
   }
   if (prepped) {  // K0b + K0c ran in the previous step's K4': K0z + the tile boxes here
-    if (zero(false, nullptr, 0, true)) return -1;
+    if (!nozero && zero(false, nullptr, 0, true)) return -1;
   } else
   hipLaunchKernelGGL(k_prep_cols, dim3(halo ? (unsigned)(a1 - a0) : blocks_for(n, kTile)), dim3(kTile), 0,
                      c->stream, (int)n, perm_c, home ? 1 : 0, recs ? 1 : 0, own,
@@ -2213,12 +2288,11 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
   // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
   const unsigned long long icap = (unsigned long long)ntp * kSlicesPerTile;  // items: 8 slices per tile pair
-  static const bool tp_super = getenv("BSA_TP_SUPER") && atoi(getenv("BSA_TP_SUPER")) == 1;  // (A/B)
   if (nct <= kTPDirectMax && !tp_super)
     hipLaunchKernelGGL(k_tilepairs_direct, dim3((unsigned)nrt), dim3(kTPDirectThreads), 0, c->stream, nrt, nct,
                        (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
                        icap, dcnt, (unsigned long long *)c->workq.p, build, halo ? halo_present(c) : nullptr, a0,
-                       a1);
+                       a1, nozero ? (const TileBox *)c->gbox_c.p : (const TileBox *)nullptr);
   else
     hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
                        nrt, nct, (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune,
@@ -2329,10 +2403,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows)), dim3(64), 0, c->stream, (int)nrows,
                        (unsigned *)c->rowcnt.p);
     hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)rank_blocks((int)nrows)), dim3(kRankRows), 0, c->stream,
-                       (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p, (const unsigned *)c->rowcnt.p,
+                       (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
                        (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb, (int *)c->out_ci.p,
                        (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
-                       (unsigned long long *)c->stats.p, gate, build, mf);
+                       (unsigned long long *)c->stats.p, gate, build, mf, (unsigned char *)c->inconf.p,
+                       (unsigned long long *)c->tcpamax.p, (Counters *)c->counters2.p,
+                       (unsigned long long *)c->workq2.p);
+    c->zeroed_rows = nrows;
   } else {
     hipLaunchKernelGGL(k_rank, dim3(256 * 4), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
                        (const unsigned *)c->rowoff.p, (const unsigned long long *)c->ckey2.p,
@@ -2367,6 +2444,7 @@ int detect_finish(Ctx *c, bool *retry) {
     c->have_pairs = true;
     return 0;
   }
+  c->zeroed_rows = -1;  // (a retry zeroes everything again; so does any host-side recovery)
   if (h.k2_demand) {  // a K2 row bucket was full: nothing was written (the
     grow_k2_bucket(c, h.k2_demand);  // candidate list itself is complete: a reusable one stays valid)
     *retry = true;

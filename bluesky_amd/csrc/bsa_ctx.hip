@@ -201,7 +201,7 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->tcpamax, &c->sort_tmp, &c->seg, &c->mvp_stage, &c->kin_stage, &c->mvp_pdv, &c->mvp_pfl, &c->mvp_rowdv,
                         &c->pfvrow, &c->pfvcol, &c->pfprow, &c->pfpcol, &c->key_r, &c->idx_r, &c->key_r2, &c->perm_r,
                         &c->key_c, &c->idx_c, &c->key_c2, &c->perm_c, &c->tbox_r, &c->tbox_c,
-                        &c->gbox_r, &c->gbox_c, &c->sbox_c, &c->workq, &c->rowcnt, &c->rowoff,
+                        &c->gbox_r, &c->gbox_c, &c->sbox_c, &c->workq, &c->workq2, &c->counters2, &c->rowcnt, &c->rowoff,
                         &c->cflag, &c->stats,
                         &c->tilepairs, &c->scan_ws, &c->snap_build, &c->snap_cur, &c->reuse_ctl, &c->reuse_use,
                         &c->geo_in, &c->geo_pts, &c->geo_out, &c->wfield};

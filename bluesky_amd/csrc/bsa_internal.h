@@ -169,6 +169,8 @@ struct Ctx {
 
   // detect buffers
   DevBuf counters;           // Counters
+  DevBuf counters2, workq2;  // the next detect's counters / dequeue words (double-buffered, zeroed by K2)
+  int64_t zeroed_rows = -1;  // rows of the last detect whose K2 zeroed counters2 / workq2 / rowcnt, or -1
   DevBuf cand;               // uint2 (i, j)
   DevBuf cflag;              // per candidate: bit0 conflict, bit1 LoS
   unsigned long long cand_cap = 0;

@@ -496,6 +496,7 @@ static int sim_cd(Ctx *c, bool allow_defer) {
 // overflow re-runs the step here with unchanged buffers)
 static int grow_after_abort(Ctx *c, const unsigned long long *ctl) {
   c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
+  c->zeroed_rows = -1;     // ... and zeroes every per-detect buffer (an aborted K2 wrote no inconf / tcpamax)
   {
     Counters h;
     BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
