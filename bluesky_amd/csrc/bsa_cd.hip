@@ -558,17 +558,24 @@ __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
   // rows are the columns then, so the row groups are the column groups)
   auto tile_of = [&](int t) {
     const int ng = (nrows + kGroup - 1) / kGroup;  // (all rows detected: nrows = n)
-    TileBox u = t * kGroupsPerTile < ng ? gbc[t * kGroupsPerTile] : empty_box();
-    for (int q = 1; q < kGroupsPerTile; ++q)
-      u = box_union(u, t * kGroupsPerTile + q < ng ? gbc[t * kGroupsPerTile + q] : empty_box());
+    TileBox g[kGroupsPerTile];
+#pragma unroll
+    for (int q = 0; q < kGroupsPerTile; ++q) g[q] = gbc[min(t * kGroupsPerTile + q, ng - 1)];  // loads together
+    TileBox u = t * kGroupsPerTile < ng ? g[0] : empty_box();
+#pragma unroll
+    for (int q = 1; q < kGroupsPerTile; ++q) u = box_union(u, t * kGroupsPerTile + q < ng ? g[q] : empty_box());
     return u;
   };
   // every box load issued before the first barrier (one round trip)
   TileBox bc = gbc ? tile_of(min((int)threadIdx.x, nct - 1)) : cb[min((int)threadIdx.x, nct - 1)];
   if (threadIdx.x < kSlicesPerTile && rt * kTile + (int)threadIdx.x * kGroup < nrows)
     sgb[threadIdx.x] = rg[rt * kSlicesPerTile + threadIdx.x];
-  const TileBox a = gbc ? tile_of(rt) : rb[rt];
+  TileBox a = gbc ? empty_box() : rb[rt];
   __syncthreads();
+  if (gbc) {  // the row tile's groups are its slices (rows = columns): tile_from_groups' union from LDS
+    a = sgb[0];
+    for (int q = 1; q < kSlicesPerTile; ++q) a = box_union(a, rt * kTile + q * kGroup < nrows ? sgb[q] : empty_box());
+  }
   for (int c0 = 0; c0 < nct; c0 += kTPDirectThreads) {
     const int ct = c0 + (int)threadIdx.x;
     bool kn = false, kf = false;
