@@ -820,8 +820,11 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // K0d's items (complete before this launch): near ones from the front of
   // the list, the others from its back; each is `pieces` units
   // near items take kn.pnear units each, the others kn.pieces
-  const unsigned long long inear = work[1], unear = inear * (unsigned)kn.pnear;
-  const unsigned long long nunits = unear + work[2] * (unsigned)kn.pieces;
+  // (32-bit unit arithmetic, powers of two: the 64-bit forms with a run-time
+  // divisor expanded into ~50 scalar instructions per unit)
+  const unsigned lnear = (unsigned)__builtin_ctz((unsigned)kn.pnear), lpc = (unsigned)__builtin_ctz((unsigned)kn.pieces);
+  const unsigned inear = (unsigned)work[1], unear = inear << lnear;
+  const unsigned nunits = unear + ((unsigned)work[2] << lpc);
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
@@ -835,23 +838,26 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // shard counter) and continues there.  (The LDS stage-2 queue this replaces
   // waited on the previous flush's atomic at every flush: ~25 k flushes per
   // sweep, the densest items flushing every ~64 survivors.)
-  unsigned long long wpos = 0, wend = 0;
+  // (32-bit slot arithmetic: a shard's slots, and its counter until an
+  // overflowing detect is retried, stay far below 2^32)
+  const unsigned ccap32 = (unsigned)ccap;
+  unsigned wpos = 0, wend = 0;
   unsigned nemit = 0;  // candidates this wave wrote (statistics)
   auto emit = [&](unsigned long long mk, bool keep, uint2 v) {
     const unsigned c = (unsigned)__popcll(mk), pre = lane_prefix(mk);
-    const unsigned long long room = wend - wpos;
-    unsigned long long idx = wpos + pre;
+    const unsigned room = wend - wpos;
+    unsigned idx = wpos + pre;
     if (c > room) {
       unsigned long long r = 0;
       if (lane == 0) r = atomicAdd(cshard, (unsigned long long)PF_RES);
-      const unsigned long long nb = wave_bcast_u64(r);
+      const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)r);
       if (pre >= room) idx = nb + (pre - room);
       wpos = nb + (c - room);
       wend = nb + PF_RES;
     } else {
       wpos += c;
     }
-    if (keep && idx < ccap) ccand[idx] = v;
+    if (keep && idx < ccap32) ccand[idx] = v;
     nemit += c;
   };
 #ifdef BSA_PF_STAMPS
@@ -863,17 +869,17 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   unsigned tr_n = 0;
 #endif
   for (;;) {
-    unsigned long long item;
+    unsigned item;
     {
       unsigned long long m0 = 0;
       if (lane == 0) m0 = atomicAdd(wq, 1ull);
-      item = wave_bcast_u64(m0);
+      item = __builtin_amdgcn_readfirstlane((unsigned)m0);
     }
     // the unit of the shard's item-th dequeue: blocks of 8 consecutive units, 4
     // consecutive blocks to the 4 shards of one XCD (shard & 7 = the XCD of its
     // workgroups), so the items of a tile pair -- consecutive in the list -- are
     // swept on one XCD, close together in time: the column tile enters one L2
-    item = (((item >> 3) * kWorkShards + 4 * (shard & 7) + (shard >> 3)) << 3) | (item & 7ull);
+    item = (((item >> 3) * kWorkShards + 4 * (shard & 7) + (shard >> 3)) << 3) | (item & 7u);
     if (item >= nunits) break;
 #ifdef BSA_PF_TRACE
     const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
@@ -882,11 +888,12 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     do {  // one item; `break` ends it
     // the item: (row tile | slice << 22, column tile)
     const bool inr = item < unear;
-    const unsigned npc = (unsigned)(inr ? kn.pnear : kn.pieces);
-    const unsigned long long ui = inr ? item : item - unear;
-    const unsigned piece = (unsigned)(ui % npc);
-    const unsigned long long e = inr ? ui / npc : inear + ui / npc;
-    const uint2 it = items[e < inear ? e : icap - 1 - (e - inear)];
+    const unsigned ls = inr ? lnear : lpc;
+    const unsigned npc = 1u << ls;
+    const unsigned ui = inr ? item : item - unear;
+    const unsigned piece = ui & (npc - 1u);
+    const unsigned e = inr ? (ui >> ls) : inear + (ui >> ls);
+    const uint2 it = items[e < inear ? (unsigned long long)e : icap - 1 - (unsigned long long)(e - inear)];
     const uint2 rc = make_uint2(it.x & 0x3fffffu, it.y);
     const unsigned slice = it.x >> 22;
     // column sub-groups of this tile that may interact with the wave's row box:
@@ -1167,8 +1174,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 #endif
   }
   PF_STAMP(0);
-  for (unsigned long long k = wpos + lane; k < wend; k += 64)  // the last block's unused tail
-    if (k < ccap) ccand[k] = make_uint2(kCandHole, kCandHole);
+  for (unsigned k = wpos + lane; k < wend; k += 64)  // the last block's unused tail
+    if (k < ccap32) ccand[k] = make_uint2(kCandHole, kCandHole);
   // the roofline's sub-group count: one atomic per workgroup, spread over 32
   // lines (4096 waves adding to one word serialised at ~12 ns each, ~50 us of
   // the sweep's tail when the waves finish together)
