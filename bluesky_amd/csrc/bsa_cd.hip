@@ -1974,9 +1974,15 @@ static int next_events(Ctx *c, hipEvent_t **ev) {
 // reuse, BSA_FLAG_STAGE1_T0 or the BSA_STAGE1_T0 environment variable
 // home mode: K1b reads stored fp64 column records (else builds them from the
 // state arrays); BSA_HOME_REC=0/1 overrides (see detect_enqueue)
-bool home_records(const Ctx *c) {
+// By the rows of the detect: a rank's K1b on stored records runs 4 waves per
+// SIMD (on records rebuilt from the state, 2); writing the records costs its
+// K0b 128 B per column.  Measured per rank (tools/rowslice_probe.py,
+// BSA_HOME_REC): one rank of 8 at 1M 0.1415 -> 0.1377 ms and of 4 / 8 at the
+// 100k box -2.4 / -2.3 us with records; 500k and 1M rows slower with them.
+bool home_records(const Ctx *c, int64_t nrows) {
   static const int home_rec_env = getenv("BSA_HOME_REC") ? atoi(getenv("BSA_HOME_REC")) : -1;
-  return home_rec_env >= 0 ? home_rec_env == 1 : (c->n < (1 << 18) && c->nranks == 1);
+  (void)c;
+  return home_rec_env >= 0 ? home_rec_env == 1 : nrows <= 163840;
 }
 
 int stage1_mid(int flags, bool reuse, int kwik) {
@@ -2055,7 +2061,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // slice of several; with one rank below 2^18 aircraft the stored records
   // win (each aircraft is in ~5 candidates there: K1b 27 -> 18 us at 100k).
   // BSA_HOME_REC=0/1 overrides.
-  const bool recs = !home || home_records(c);
+  const bool recs = !home || home_records(c, nrows);
   if (home && (distinct || (rb % kTile != 0 && re > rb) || (flags & BSA_FLAG_KWIK)))  // (a rank without rows: rb = n)
     return fail(c, "home-order detect needs own == intruder, a %d-aligned row slice, no KWIK", kTile);
   const int kwik = (flags & BSA_FLAG_KWIK) ? 1 : 0;

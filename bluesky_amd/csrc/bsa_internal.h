@@ -367,7 +367,7 @@ void bk_release(Ctx *c);
 // their boxes), plan which tiles every rank needs, exchange them (mode 1) and
 // leave the flat list of this rank's halo tiles in h_hl (halo_hl slots, -1 =
 // unused) and its present mask in h_plan
-bool home_records(const Ctx *c);                  // home-mode detect stores fp64 column records
+bool home_records(const Ctx *c, int64_t nrows);   // home-mode detect (of nrows rows) stores fp64 column records
 int stage1_mid(int flags, bool reuse, int kwik);  // midpoint stage 1 for this detect?
 int halo_init_caps(Ctx *c);      // bsa_sim_init, several ranks: exact initial capacities (no exchange)
 int halo_grow(Ctx *c);           // after an aborted step, several ranks (collective)

@@ -653,7 +653,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
       bsa::PrepArgs pa{};
       if (prep) {
         const int64_t n = c->n;
-        pa.rec = bsa::home_records(c) ? 1 : 0;
+        pa.rec = bsa::home_records(c, n) ? 1 : 0;
         if ((pa.rec && !bsa::ensure(c, c->colrec, n * sizeof(bsa::ColRec), "column records")) ||
             !bsa::ensure(c, c->pfcol, n * sizeof(bsa::PFRec), "prefilter columns") ||
             !bsa::ensure(c, c->pfvcol, n * sizeof(bsa::PFVel), "prefilter column velocities") ||
