@@ -2369,14 +2369,16 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
-  // ---- K1b exact evaluation: grid-stride over the device-side count, one
-  // resident round (4 workgroups per CU at its register budget)
+  // ---- K1b exact evaluation: grid-stride over the device-side count; 2048
+  // workgroups (two resident rounds): the ~525 k slots of the 100k box's list
+  // (candidates + the tails of the waves' reserved blocks) in one stride
+  // (1024 workgroups: 24.7 -> 23.2 us with 2048, A/B on one box)
   // K2 row buckets (B pairs per row per list; a fuller row retries wider, then without)
   const int B = c->k2_bucket;
   if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * sizeof(uint2), "K2 row buckets")) return -1;
   {
     const auto KEX = !recs ? k_exact<kExactHome> : (kwik ? k_exact<kExactKwik> : k_exact<kExactRec>);
-    hipLaunchKernelGGL(KEX, dim3(256 * 4), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
+    hipLaunchKernelGGL(KEX, dim3(256 * 8), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
                        perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, own, cap, rpz, hpz, tla, (int)rb,
                        (int)nrows,
                        (unsigned char *)c->cflag.p, (double *)c->cpay.p,
