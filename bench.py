@@ -8,8 +8,9 @@ JSON line on rank 0; for N > 1 it is launched by ``torch.distributed.run``
 
 A step = one GPU-resident sim step of the synthetic 100k-aircraft
 density-matched box (BASELINE.json configs[3]) with ASAS every
-step: [RCCL all-gather] -> StateBased detect of the rank's ownship rows
-against all N intruders -> MVP -> pilot select + kinematics.  Inputs are
+step: [RCCL halo exchange of the column tiles the rank's rows can reach] ->
+StateBased detect of the rank's ownship rows against all N intruders -> MVP ->
+pilot select + kinematics.  Inputs are
 resident in HBM before the timed region.  Each step evaluates all N^2 pairs
 (diagonal included), so value = N^2 * K / time (whole job, all ranks);
 sim-steps/s = K / time.  Rows are partitioned, total work is fixed:

@@ -186,6 +186,7 @@ SIGNATURES.update({
     'bsa_sim_set_reso_lists': (ctypes.c_int, [_vp, _c_u8p, _c_u8p]),
     'bsa_sim_read_asas': (ctypes.c_int, [_vp, ctypes.POINTER(AsasOut)]),
     'bsa_sim_halo_stats': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_sim_set_halo_cap': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64]),
     'bsa_sim_set_atmos': (ctypes.c_int, [_vp, ctypes.c_int]),
     'bsa_sim_read_atmos': (ctypes.c_int, [_vp, _c_dp, _c_dp, _c_dp]),
 })
@@ -211,6 +212,8 @@ def load(path=None):
         except OSError as e:
             raise AccelUnavailable('cannot load %s: %s' % (p, e))
         for name, (res, args) in SIGNATURES.items():
+            if p != os.path.join(_HERE, 'libbsaccel.so') and not hasattr(lib, name):
+                continue   # an older build selected with BSACCEL_LIB for an A/B measurement
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args
@@ -508,6 +511,7 @@ class Context:
         if len(uid) != UNIQUE_ID_BYTES:
             raise ValueError('unique id must be %d bytes' % UNIQUE_ID_BYTES)
         self.check(self.lib.bsa_comm_init(self.h, int(nranks), int(rank), uid), 'bsa_comm_init')
+        self.comm_rank_world = (int(rank), int(nranks))
 
     def comm_init_group(self, group, rank):
         """Join an in-process Group as ``rank`` (call from this rank's thread)."""
@@ -710,6 +714,11 @@ class Context:
         v = np.zeros(4, np.int64)
         self.check(self.lib.bsa_sim_halo_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_halo_stats')
         return dict(rx_bytes=int(v[0]), tx_bytes=int(v[1]), tiles=int(v[2]), regrowths=int(v[3]))
+
+    def sim_set_halo_cap(self, sender, receiver, tiles):
+        """bsa_sim_set_halo_cap (testing aid): this rank's copy of one tile capacity."""
+        self.check(self.lib.bsa_sim_set_halo_cap(self.h, int(sender), int(receiver), int(tiles)),
+                   'bsa_sim_set_halo_cap')
 
     def sim_asas_stats(self):
         """ASAS bookkeeping counts after the last CD call (resume_nav on); the

@@ -44,6 +44,9 @@ RESOOFF lists, stack changes of ZONER / ZONEDH / DTLOOK between calls, and
 Traffic create / delete between calls (mirrored with ``bsa_sim_create`` /
 ``bsa_sim_delete``, which keep the bookkeeping of the other aircraft).  Any
 other CD / CR method raises ``NotImplementedError`` -- there is no CPU path.
+One rank only: BlueSky's ``ASAS.update`` is one process's call over the whole
+traffic, so a context joined to a communicator or group (several ranks, each
+holding only its rows' outputs) raises ``NotImplementedError``.
 """
 import collections.abc
 import warnings
@@ -159,6 +162,9 @@ class DeviceASAS:
     def __init__(self, asas, traf, ctx=None, history=False, waypoint_recovery=True):
         self.asas, self.traf = asas, traf
         self.ctx = ctx or _lib.default_context()
+        if getattr(self.ctx, 'comm_rank_world', (0, 1))[1] > 1:
+            raise NotImplementedError('ASAS drop-in: one rank only (this context is rank %d of %d; '
+                                      'the per-rank outputs cover only its rows)' % self.ctx.comm_rank_world)
         self.history = history
         self.waypoint_recovery = waypoint_recovery
         self._ids = None        # callsigns of the device's traffic, in index order

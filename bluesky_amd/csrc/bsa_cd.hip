@@ -184,8 +184,12 @@ constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
 // counts, so the row offsets need no scan with a look-back chain.  (K1b
 // counting them with atomics, one per wave and block, cost 12 us at the 100k
 // box: the per-block words were hit by every wave of a block's rows at once.)
-constexpr int kRankRows = 512;
-constexpr int kRankLds = 1536;  // pairs per block folded from LDS (67 KB: 2 blocks per CU)
+#ifndef BSA_RANK_ROWS
+#define BSA_RANK_ROWS 512
+#endif
+constexpr int kRankRows = BSA_RANK_ROWS;
+static_assert(kRankRows % 64 == 0 && kRankRows <= 1024, "whole waves per K2 block");
+constexpr int kRankLds = 3 * kRankRows;  // pairs per block folded from LDS (512 rows: 67 KB, 2 blocks per CU)
 __host__ __device__ __forceinline__ int rank_blocks(int nrows) { return (nrows + kRankRows - 1) / kRankRows; }
 __host__ __device__ __forceinline__ int rowcnt_words(int nrows) { return 2 * (nrows + 1) + 2 * rank_blocks(nrows); }
 
@@ -250,7 +254,8 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
   __shared__ TileBox fgb[kTile / 64];
   // K0z (fused): nothing here reads that state
   if (zs.cnt) zero_state(zs, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
-  int tile = tile_list ? tile_list[blockIdx.x] : tile_base + (int)blockIdx.x;
+  int tile = hu.count && blockIdx.x >= *hu.count ? -1
+             : (tile_list ? tile_list[blockIdx.x] : tile_base + (int)blockIdx.x);
   // halo exchange: this slot's received tile rows first (each thread writes
   // the row it prepares below), checked against this rank's plan
   if (hu.rbuf) tile = halo_unpack_tile(hu, (int)blockIdx.x, tile, hcnt);
@@ -543,11 +548,18 @@ __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, int 
 // union loads, its scan and its barrier were a third of K0d's chain there
 constexpr int kTPDirectThreads = 256;
 constexpr int kTPDirectMax = 1024;  // column tiles up to which K0d runs direct
+// Halo mode (hl != NULL): the columns are this rank's own tiles [p0, p1) and
+// the received halo tiles hl[0, nhl) (-1: an unused slot; *nhl_dev bounds the
+// list when set), not all nct tiles -- one rank of 8 at 1M holds ~300 of the
+// 1954 tiles.  Every other tile is still tested against the row tile, without
+// an append: a kept pair with a tile the halo plan did not deliver sets
+// Counters::halo_miss (the step fails loudly), as the full sweep did.
 __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
     int nrt, int nct, int nrows, const TileBox *__restrict__ rb, const TileBox *__restrict__ rg,
     const TileBox *__restrict__ cb, int noprune, uint2 *__restrict__ out, unsigned long long cap,
     Counters *__restrict__ cnt, unsigned long long *__restrict__ icnt, const unsigned *__restrict__ build,
-    const uint8_t *__restrict__ present, int p0, int p1, const TileBox *__restrict__ gbc) {
+    const uint8_t *__restrict__ present, int p0, int p1, const TileBox *__restrict__ gbc,
+    const int *__restrict__ hl, int nhl, const unsigned *__restrict__ nhl_dev) {
   if (build && !build[0]) return;
   __shared__ TileBox sgb[kSlicesPerTile];
   __shared__ unsigned wpre[4][kTPDirectThreads / 64];
@@ -566,8 +578,13 @@ __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
     for (int q = 1; q < kGroupsPerTile; ++q) u = box_union(u, t * kGroupsPerTile + q < ng ? g[q] : empty_box());
     return u;
   };
+  // column k of the sweep: tile k (all tiles), or own tile p0 + k / halo tile hl[k - (p1 - p0)]
+  const int nown = p1 - p0;
+  const int ncols = hl ? nown + (nhl_dev ? min(nhl, (int)*nhl_dev) : nhl) : nct;
+  auto col_of = [&](int k) { return k >= ncols ? -1 : (!hl ? k : (k < nown ? p0 + k : hl[k - nown])); };
   // every box load issued before the first barrier (one round trip)
-  TileBox bc = gbc ? tile_of(min((int)threadIdx.x, nct - 1)) : cb[min((int)threadIdx.x, nct - 1)];
+  int ct = col_of((int)threadIdx.x);
+  TileBox bc = gbc ? tile_of(max(ct, 0)) : cb[max(ct, 0)];
   if (threadIdx.x < kSlicesPerTile && rt * kTile + (int)threadIdx.x * kGroup < nrows)
     sgb[threadIdx.x] = rg[rt * kSlicesPerTile + threadIdx.x];
   TileBox a = gbc ? empty_box() : rb[rt];
@@ -576,15 +593,20 @@ __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
     a = sgb[0];
     for (int q = 1; q < kSlicesPerTile; ++q) a = box_union(a, rt * kTile + q * kGroup < nrows ? sgb[q] : empty_box());
   }
-  for (int c0 = 0; c0 < nct; c0 += kTPDirectThreads) {
-    const int ct = c0 + (int)threadIdx.x;
+  for (int c0 = 0; c0 < ncols; c0 += kTPDirectThreads) {
+    if (c0 > 0) {
+      ct = col_of(c0 + (int)threadIdx.x);
+      if (ct >= 0) bc = gbc ? tile_of(ct) : cb[ct];
+    }
     bool kn = false, kf = false;
     unsigned sm = 0;
-    if (c0 > 0 && ct < nct) bc = gbc ? tile_of(ct) : cb[ct];
-    if (ct < nct) sm = tp_classify(a, sgb, bc, rt, ct, nrows, noprune, present, p0, p1, cnt, kn, kf);
+    if (ct >= 0) sm = tp_classify(a, sgb, bc, rt, ct, nrows, noprune, present, p0, p1, cnt, kn, kf);
     tp_emit<kTPDirectThreads>(kn, kf, sm, rt, ct, out, cap, cnt, icnt, wpre, bbase);
     __syncthreads();  // wpre / bbase are rewritten by the next round
   }
+  if (hl)  // the tiles this rank does not hold: none may be reachable (no appends, no barriers)
+    for (int t = (int)threadIdx.x; t < nct; t += kTPDirectThreads)
+      if (!(t >= p0 && t < p1) && !present[t] && (noprune || boxes_may_interact(a, cb[t]))) cnt->halo_miss = 1;
 }
 
 __device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long v) {
@@ -681,13 +703,14 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
 #ifndef PF_Q1
 #define PF_Q1 512  // per-wave stage-1 queue: u16 (row_local << 6 | column slot)
 #endif
-// Refine survivors go straight to the wave's reserved block of PF_RES
-// candidate slots (one returning atomic per block; the unused tail of a wave's
-// last block is filled with kCandHole, which K1b skips)
+// Refine survivors are staged in the wave's LDS slot of PF_RES candidates; a
+// full slot is flushed to the candidate list (one returning atomic on the
+// shard counter per PF_RES candidates), and at the end of the sweep the four
+// waves of a workgroup flush what is left with ONE atomic together -- the list
+// is dense (no unused slots), so K1b runs every wave with all 64 lanes busy
 #ifndef PF_RES
 #define PF_RES 128
 #endif
-constexpr unsigned kCandHole = 0xffffffffu;  // candidate slot without a pair (both words)
 constexpr int PF_WROWS = 64;   // rows per wave (one per lane)
 constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 // Work distribution knob of the sweep (BSA_PF_SHARDS overrides it for
@@ -756,8 +779,9 @@ constexpr unsigned kTraceWave = 256;
 // per-lane counts).  The queue is drained after every batch (or when full)
 // with all 64 lanes busy through stage 2 (refine) on LDS-resident inputs (the
 // batch's staged columns, the item's staged rows, row unit vectors by
-// ds_bpermute).  Stage-2 survivors are written straight to the wave's
-// reserved block of candidate slots (one atomic on its shard per PF_RES slots).
+// ds_bpermute).  Stage-2 survivors are staged in the wave's LDS slot and
+// appended densely to the candidate list (one atomic per PF_RES candidates,
+// and one per workgroup at the end of the sweep).
 template <bool NOPRUNE>
 // 4 waves per SIMD = PF_BLOCKS_PER_CU resident workgroups: up to 128 VGPRs,
 // no spills (at 5 waves the 96-VGPR cap spilled to scratch, and every scratch
@@ -782,6 +806,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ float4 rsp[PF_WAVES][PF_WROWS];  //                    x y z sigma   (refine)
   __shared__ float4 rbs[PF_WAVES][PF_WROWS];  //                    x/rho y/rho rho - (refine basis)
   __shared__ unsigned char sgs[PF_WAVES][kSubsPerBatch];  // the next batch's sub-groups (tile-local)
+  __shared__ uint2 cst[PF_WAVES][PF_RES];   // staged candidates (row, column) of the wave
   if (build && !build[0]) return;  // reused candidate list
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned short *q1 = q1s[w];
@@ -832,32 +857,35 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   const unsigned long long ccap = cap / kCandShards;
   uint2 *ccand = cand + (unsigned long long)(shard % kCandShards) * ccap;
   unsigned long long *cshard = &cnt->cshard[shard % kCandShards][0];
-  // the wave's candidate slots [wpos, wend) (wave-uniform): a refine round's
-  // survivors (mask mk) take the next slots in lane order; a round that does
-  // not fit reserves the next PF_RES-slot block (one returning atomic on the
-  // shard counter) and continues there.  (The LDS stage-2 queue this replaces
-  // waited on the previous flush's atomic at every flush: ~25 k flushes per
-  // sweep, the densest items flushing every ~64 survivors.)
+  // the wave's staged candidates cst[w][0, nst) (wave-uniform count): a refine
+  // round's survivors (mask mk) take the next entries in lane order; a round
+  // that does not fit flushes the slot first (one returning atomic on the
+  // shard counter reserves exactly nst list slots).  Most waves never flush
+  // before the end of the sweep (the 100k box: ~37 candidates per wave), where
+  // the workgroup flushes its four slots with one atomic.  (Reserving blocks of
+  // PF_RES list slots directly left each wave's last block ~70 % unused: K1b
+  // ran ~524 k slots for ~153 k candidates.)
   // (32-bit slot arithmetic: a shard's slots, and its counter until an
   // overflowing detect is retried, stay far below 2^32)
   const unsigned ccap32 = (unsigned)ccap;
-  unsigned wpos = 0, wend = 0;
+  uint2 *stg = cst[w];
+  unsigned nst = 0;
   unsigned nemit = 0;  // candidates this wave wrote (statistics)
+  auto flush_stage = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long r = 0;
+    if (lane == 0) r = atomicAdd(cshard, (unsigned long long)nst);
+    const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)r);
+    for (unsigned k = lane; k < nst; k += 64)
+      if (nb + k < ccap32) ccand[nb + k] = stg[k];
+    nst = 0;
+    __builtin_amdgcn_wave_barrier();
+  };
   auto emit = [&](unsigned long long mk, bool keep, uint2 v) {
     const unsigned c = (unsigned)__popcll(mk), pre = lane_prefix(mk);
-    const unsigned room = wend - wpos;
-    unsigned idx = wpos + pre;
-    if (c > room) {
-      unsigned long long r = 0;
-      if (lane == 0) r = atomicAdd(cshard, (unsigned long long)PF_RES);
-      const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)r);
-      if (pre >= room) idx = nb + (pre - room);
-      wpos = nb + (c - room);
-      wend = nb + PF_RES;
-    } else {
-      wpos += c;
-    }
-    if (keep && idx < ccap32) ccand[idx] = v;
+    if (nst + c > (unsigned)PF_RES) flush_stage();
+    if (keep) stg[nst + pre] = v;
+    nst += c;
     nemit += c;
   };
 #ifdef BSA_PF_STAMPS
@@ -1174,23 +1202,33 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
 #endif
   }
   PF_STAMP(0);
-  for (unsigned k = wpos + lane; k < wend; k += 64)  // the last block's unused tail
-    if (k < ccap32) ccand[k] = make_uint2(kCandHole, kCandHole);
-  // the roofline's sub-group count: one atomic per workgroup, spread over 32
-  // lines (4096 waves adding to one word serialised at ~12 ns each, ~50 us of
-  // the sweep's tail when the waves finish together)
-  __shared__ unsigned wsubs[PF_WAVES], wcand[PF_WAVES];
+  // the workgroup's staged candidates with one atomic on its shard counter,
+  // and the roofline's sub-group count: one atomic per workgroup, spread over
+  // 32 lines (4096 waves adding to one word serialised at ~12 ns each, ~50 us
+  // of the sweep's tail when the waves finish together)
+  __shared__ unsigned wsubs[PF_WAVES], wcand[PF_WAVES], wst[PF_WAVES];
+  __shared__ unsigned wbase;
   if (lane == 0) {
     wsubs[w] = subs;
     wcand[w] = nemit;
+    wst[w] = nst;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned t = 0, tc = 0;
+    unsigned t = 0, tc = 0, ts = 0;
     for (int q = 0; q < PF_WAVES; ++q) t += wsubs[q];
     if (t) atomicAdd(&cnt->gpart[blockIdx.x & 31][0], (unsigned long long)t);
     for (int q = 0; q < PF_WAVES; ++q) tc += wcand[q];
-    if (tc) atomicAdd(&cnt->gpart[blockIdx.x & 31][1], (unsigned long long)tc);  // candidates (not slots)
+    if (tc) atomicAdd(&cnt->gpart[blockIdx.x & 31][1], (unsigned long long)tc);  // candidates
+    for (int q = 0; q < PF_WAVES; ++q) ts += wst[q];
+    wbase = ts ? (unsigned)atomicAdd(cshard, (unsigned long long)ts) : 0u;
+  }
+  __syncthreads();
+  {
+    unsigned o = wbase;
+    for (int q = 0; q < w; ++q) o += wst[q];
+    for (unsigned k = lane; k < nst; k += 64)
+      if (o + k < ccap32) ccand[o + k] = stg[k];
   }
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
@@ -1447,8 +1485,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
     const uint2 p = cand[(unsigned long long)sh * ccap + (idx - pre[sh])];
     unsigned char flag = 0;
     int row = 0;
-    // p.x == kCandHole: an unused reserved slot (the tail of a wave's last block)
-    if (p.x != kCandHole) {
+    {
       // home mode (perm_r == NULL, the resident sim): rows are the home slice
       // [rb, rb + nrows) of the columns; the key's row is the home row, its
       // column the aircraft index (so K2 orders each row's pairs by index)
@@ -2286,6 +2323,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
       FusedBoxes fb2 = fb;
       fb2.blk = nullptr;
+      hu.count = halo_list_count(c);
       hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)c->halo_hl), dim3(kTile), 0, c->stream, (int)n, perm_c, 1,
                          recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                          (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, 0,
@@ -2308,11 +2346,17 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
   // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
   const unsigned long long icap = (unsigned long long)ntp * kSlicesPerTile;  // items: 8 slices per tile pair
-  if (nct <= kTPDirectMax && !tp_super)
+  // halo mode: K0d sweeps the present column tiles only (own + received, the
+  // flat halo list; BSA_TP_HALO_ALL=1 sweeps all tiles for A/B)
+  static const bool tp_all = getenv("BSA_TP_HALO_ALL") && atoi(getenv("BSA_TP_HALO_ALL")) == 1;
+  const bool tp_list = halo && !tp_all && !tp_super;
+  if ((nct <= kTPDirectMax || tp_list) && !tp_super)
     hipLaunchKernelGGL(k_tilepairs_direct, dim3((unsigned)nrt), dim3(kTPDirectThreads), 0, c->stream, nrt, nct,
                        (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
                        icap, dcnt, (unsigned long long *)c->workq.p, build, halo ? halo_present(c) : nullptr, a0,
-                       a1, nozero ? (const TileBox *)c->gbox_c.p : (const TileBox *)nullptr);
+                       a1, nozero ? (const TileBox *)c->gbox_c.p : (const TileBox *)nullptr,
+                       tp_list ? (const int *)c->h_hl.p : (const int *)nullptr, (int)c->halo_hl,
+                       tp_list ? halo_list_count(c) : (const unsigned *)nullptr);
   else
     hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
                        nrt, nct, (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune,
@@ -2369,16 +2413,17 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
-  // ---- K1b exact evaluation: grid-stride over the device-side count; 2048
-  // workgroups (two resident rounds): the ~525 k slots of the 100k box's list
-  // (candidates + the tails of the waves' reserved blocks) in one stride
-  // (1024 workgroups: 24.7 -> 23.2 us with 2048, A/B on one box)
+  // ---- K1b exact evaluation: grid-stride over the device-side count of the
+  // dense candidate list; 2048 workgroups (524 k lanes: the 100k box's ~153 k
+  // candidates in one stride, the workgroups past the count exit at once;
+  // BSA_K1B_GRID overrides for A/B)
   // K2 row buckets (B pairs per row per list; a fuller row retries wider, then without)
   const int B = c->k2_bucket;
   if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * sizeof(uint2), "K2 row buckets")) return -1;
   {
     const auto KEX = !recs ? k_exact<kExactHome> : (kwik ? k_exact<kExactKwik> : k_exact<kExactRec>);
-    hipLaunchKernelGGL(KEX, dim3(256 * 8), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
+    static const int k1b_grid = getenv("BSA_K1B_GRID") ? atoi(getenv("BSA_K1B_GRID")) : 0;
+    hipLaunchKernelGGL(KEX, dim3(k1b_grid > 0 ? (unsigned)k1b_grid : 256u * 8u), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
                        perm_r, perm_c, (const uint2 *)c->cand.p, dcnt, own, cap, rpz, hpz, tla, (int)rb,
                        (int)nrows,
                        (unsigned char *)c->cflag.p, (double *)c->cpay.p,

@@ -47,6 +47,7 @@ struct Group {
   DevBuf slot[kMaxGroup];                 // each rank's published copy (its own device)
   hipEvent_t pub[kMaxGroup] = {}, done[kMaxGroup] = {};
   std::vector<double> host[kMaxGroup];    // host-value exchange
+  std::vector<size_t> hlen[kMaxGroup];    // comm_halo: each rank's send lengths and offsets (2 R)
 };
 
 // host barrier of the group; false (and the group marked broken) after 120 s
@@ -275,12 +276,40 @@ int comm_halo(Ctx *c, const void *send, const size_t *soff, const size_t *slen, 
     BSA_NCCL(c, ncclGroupEnd());
     return 0;
   }
+  // In-process group: rank q's region for this rank is copied out of q's
+  // published buffer.  RCCL's grouped send / recv needs every send length to
+  // equal its receive length (a mismatch hangs or truncates on 8 GPUs), so the
+  // lengths and offsets each rank sends with are compared here with what the
+  // receiver expects: a disagreement fails loudly on ONE GPU too.
   Group *g = c->group;
-  if (publish(c, send, stot)) return -1;
-  for (int q = 0; q < R; ++q)
-    if (q != me && rlen[q])
+  {
+    std::lock_guard<std::mutex> lk(g->m);
+    g->hlen[me].assign(slen, slen + R);
+    g->hlen[me].insert(g->hlen[me].end(), soff, soff + R);
+  }
+  if (publish(c, send, stot)) return -1;  // (its barrier: every rank's lengths are in place)
+  for (int q = 0; q < R; ++q) {
+    if (q == me) continue;
+    size_t qs = 0, qo = 0;
+    {
+      std::lock_guard<std::mutex> lk(g->m);
+      if (g->hlen[q].size() == (size_t)2 * R) {
+        qs = g->hlen[q][(size_t)me];
+        qo = g->hlen[q][(size_t)R + me];
+      }
+    }
+    if (qs != rlen[q] || (rlen[q] && qo != peer[q])) {
+      fail(c, "halo exchange: rank %d sends %zu B at %zu, rank %d expects %zu B at %zu", q, qs, qo, me, rlen[q],
+           peer[q]);
+      std::lock_guard<std::mutex> lk(g->m);
+      g->broken = true;  // the other ranks fail at their next barrier instead of waiting
+      g->cv.notify_all();
+      return -1;
+    }
+    if (rlen[q])
       BSA_HIP(c, hipMemcpyAsync((char *)recv + roff[q], (const char *)g->slot[q].p + peer[q], rlen[q],
                                 hipMemcpyDeviceToDevice, c->stream));
+  }
   return retire(c);
 }
 

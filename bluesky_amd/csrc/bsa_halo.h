@@ -43,6 +43,7 @@ struct HaloUnpack {
   HaloCaps cp;
   HaloFields fl;
   int R, n;
+  const unsigned *count;  // the probe's dense list: its length (device; slots past it are unused), or NULL
 };
 
 // returns the tile to prepare (-1: none)

@@ -137,13 +137,25 @@ __device__ void halo_lists_q(const ListArgs &a, const HaloCaps &cp, int q) {
     ovf = sc > cap;
   }
   const int t0 = q * a.tpr, t1 = min(a.nct, t0 + a.tpr);
-  const int cap = a.probe ? a.tpr : cp.rcap[q];
-  int *hl = a.hl + (a.probe ? (size_t)q * a.tpr : (size_t)cp.hoff[q]);
-  const int rc = block_compact(max(t1 - t0, 0), [&](int i) { return a.recv[t0 + i] != 0; },
-                               [&](int i, int k) { if (k < cap) hl[k] = t0 + i; });
+  auto wanted = [&](int i) { return a.recv[t0 + i] != 0; };
+  if (a.probe) {
+    // the probe's list is dense: source q's tiles at a base taken from the
+    // running total (dem[2R], which bounds the list for K0d and the halo K0b),
+    // in any source order -- the exchange's regions are per-source capacities
+    __shared__ unsigned pbase;
+    const int rc = block_compact(max(t1 - t0, 0), wanted, [](int, int) {});
+    if (threadIdx.x == 0) pbase = rc ? atomicAdd(&a.dem[2 * a.R], (unsigned)rc) : 0u;
+    __syncthreads();
+    int *hl = a.hl + pbase;
+    block_compact(max(t1 - t0, 0), wanted, [&](int i, int k) { hl[k] = t0 + i; });
+    return;  // (block_compact ends with a barrier: pbase is reused by the next q)
+  }
+  const int cap = cp.rcap[q];
+  int *hl = a.hl + (size_t)cp.hoff[q];
+  const int rc = block_compact(max(t1 - t0, 0), wanted, [&](int i, int k) { if (k < cap) hl[k] = t0 + i; });
   for (int k = rc + (int)threadIdx.x; k < cap; k += blockDim.x) hl[k] = -1;
   if (threadIdx.x == 0) {
-    if (!a.probe) a.dem[a.R + q] = (unsigned)rc;
+    a.dem[a.R + q] = (unsigned)rc;
     atomicAdd(&a.dem[2 * a.R], (unsigned)min(rc, cap));
     if (ovf || rc > cap) a.cnt->halo_ovf = 1;
   }
@@ -214,6 +226,11 @@ static size_t send_offsets(const Ctx *c, int s, int nf, unsigned long long *off)
 }
 
 const uint8_t *halo_present(const Ctx *c) { return (const uint8_t *)c->h_plan.p; }
+// the probe's dense halo list: its length on the device (the exchange's list
+// has per-source capacity regions, bounded by halo_hl on the host)
+const unsigned *halo_list_count(const Ctx *c) {
+  return c->halo_mode == 2 ? (const unsigned *)c->h_dem.p + c->halo_tot_word : nullptr;
+}
 
 // the plan's buffers: recv [nct] + send [R][tpr] flags, demands ([R] send,
 // [R] receive, the total received).  hp: the own-tile

@@ -373,6 +373,7 @@ int halo_init_caps(Ctx *c);      // bsa_sim_init, several ranks: exact initial c
 int halo_grow(Ctx *c);           // after an aborted step, several ranks (collective)
 void halo_release(Ctx *c);
 const uint8_t *halo_present(const Ctx *c);  // the received-tile mask of the last halo_mid
+const unsigned *halo_list_count(const Ctx *c);  // the probe's halo list length (device), else NULL
 // K0b over every column tile (fused boxes, no per-detect zeroing): the halo
 // plan's view of all tile boxes when every rank's state is on this GPU (bsa_cd.hip)
 int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla);

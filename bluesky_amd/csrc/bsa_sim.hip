@@ -691,7 +691,10 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
         c->sim_prep_n = c->n;
       }
       BSA_HIP(c, hipGetLastError());
-      c->sim_gs_derivable = true;  // every rank's rows now hold K4's gs / trk / gse / gsn
+      // every rank's rows now hold K4's gs / trk / gse / gsn: gse / gsn follow
+      // from gs / trk bitwise only without wind (with wind gs / trk derive from
+      // them, traffic.py:463-466, not the other way round)
+      c->sim_gs_derivable = c->simp.winddim == 0;
       c->sim_gathered = c->nranks == 1;
       c->sim_steps++;
     }
@@ -708,7 +711,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     c->sim_prepped = false;  // (an aborted K4' prepared nothing)
     const int64_t done = (int64_t)ctl[1];
     c->sim_steps = base + done;
-    c->sim_gs_derivable = derivable0 || done > 0;  // K4' ran for the completed steps only
+    c->sim_gs_derivable = done > 0 ? c->simp.winddim == 0 : derivable0;  // K4' ran for the completed steps only
     int64_t cds = 0;
     for (int64_t k = base; k < base + done; ++k) cds += (k % c->simp.cd_every == 0) ? 1 : 0;
     c->sim_cd_calls = base_cd + cds;
@@ -904,6 +907,17 @@ int bsa_sim_halo_stats(bsa_ctx *cc, int64_t *out4) {
   out4[1] = c->halo_tx;
   out4[2] = tiles;
   out4[3] = c->halo_grows;
+  return 0;
+}
+
+int bsa_sim_set_halo_cap(bsa_ctx *cc, int sender, int receiver, int64_t tiles) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  const int R = c->nranks;
+  if ((int64_t)c->halo_cap.size() != (int64_t)R * R) return bsa::fail(c, "no halo capacities (one rank, or no sim)");
+  if (sender < 0 || sender >= R || receiver < 0 || receiver >= R || sender == receiver || tiles < 0)
+    return bsa::fail(c, "bad halo capacity %d -> %d = %lld", sender, receiver, (long long)tiles);
+  c->halo_cap[(size_t)sender * R + receiver] = tiles;
   return 0;
 }
 

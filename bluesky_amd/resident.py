@@ -4,11 +4,12 @@ State lives in HBM across steps; the host only launches.  One step:
 CD + MVP every ``cd_every`` steps (asas.update, asas.py:473-504, with
 ``asas.active = inconf`` standing in for ResumeNav, or with ``resume_nav`` the
 device-side resopairs bookkeeping + ResumeNav), then Pilot.APorASAS
-(no wind) fused with the kinematic update (traffic.py:397-409).
-State is kept on the device in home order (the spatial order of the initial
-traffic); arrays cross the API in aircraft-index order.  With several ranks
-(one process per GPU) each rank owns a contiguous, spatially compact range of
-home rows and the replicated state is all-gathered over RCCL before each CD.
+(no wind, constant wind or a 2-D field) fused with the kinematic update
+(traffic.py:397-409).  State is kept on the device in home order (the spatial
+order of the initial traffic); arrays cross the API in aircraft-index order.
+With several ranks (one process per GPU) each rank owns a contiguous,
+spatially compact range of home rows; before each CD it receives, over RCCL,
+only the column tiles its rows can reach (the halo exchange).
 """
 import numpy as np
 

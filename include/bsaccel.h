@@ -272,11 +272,14 @@ int bsa_qdrdist(bsa_ctx *ctx, int64_t m, const double *lat1, const double *lon1,
 int bsa_geo_last_ms(bsa_ctx *ctx, double *ms);
 
 /* ---------------------------------------------------------------- multi-GPU
- * One process per GPU, one context per process.  Rank r owns the contiguous
- * ownship rows [r*ceil(n/R), min(n, (r+1)*ceil(n/R))) of the resident sim
- * (SURVEY.md 8e); state is replicated and re-synchronised with one RCCL
- * all-gather over xGMI before each CD step.  No reference equivalent (the
- * reference's only distributed backend, bluesky/network/ ZMQ, is out of scope). */
+ * One process per GPU, one context per process.  Rank r owns the home rows
+ * [r*rpr, min(n, (r+1)*rpr)) of the resident sim, rpr = ceil(n/R) rounded up
+ * to a multiple of 512 (a spatially compact chunk of the traffic, SURVEY.md
+ * 8e).  Before each CD step every rank receives only the column tiles its rows
+ * can reach (a halo exchange: box all-gather, then grouped RCCL send / recv of
+ * those tiles' state over xGMI), not the whole state.  No
+ * reference equivalent (the reference's only distributed backend,
+ * bluesky/network/ ZMQ, is out of scope). */
 #define BSA_UNIQUE_ID_BYTES 128
 /* Create a communicator id on one rank (ncclGetUniqueId); ship its 128 bytes
  * to the other ranks out of band. */
@@ -321,7 +324,7 @@ int bsa_gather_pairs(bsa_ctx *ctx, int root, const bsa_pairs_out *out);
 
 /* ---------------------------------------------------------------- GPU-resident sim
  * The synthetic sim step of SURVEY.md 8d with all state resident in HBM:
- *   every cd_every steps: [all-gather] -> detect (own rows) -> MVP (own rows,
+ *   every cd_every steps: [halo exchange] -> detect (own rows) -> MVP (own rows,
  *                         only if any rank has a conflict, asas.py:486-487)
  *                         -> asas.active = inconf, or (resume_nav = 1) the ASAS
  *                         bookkeeping + ResumeNav (asas.py:409-504) on the device
@@ -457,6 +460,13 @@ int bsa_sim_detect_rows(bsa_ctx *ctx, int64_t row_begin, int64_t row_end, int64_
  * bsa_sim_detect_rows, the tiles that rank share needs from other ranks --
  * and [3] capacity regrowths (aborted and re-run steps) since bsa_sim_init. */
 int bsa_sim_halo_stats(bsa_ctx *ctx, int64_t *out4);
+/* Testing aid: override this rank's copy of the tile capacity sender ->
+ * receiver (the capacities must agree on all ranks, and RCCL's grouped send /
+ * recv needs every send length to match its receive; the in-process group
+ * checks that agreement at every exchange and fails loudly, so a disagreement
+ * is caught on one GPU).  tiles >= 0; the next bsa_sim_init or regrowth
+ * recomputes the capacities. */
+int bsa_sim_set_halo_cap(bsa_ctx *ctx, int sender, int receiver, int64_t tiles);
 /* ASAS bookkeeping after the last CD call (resume_nav = 1; replaces
  * ASAS.update's Python sets, asas.py:490-502):
  * [0] |resopairs| of this rank's rows, [1] |confpairs_unique|,
@@ -470,7 +480,7 @@ int bsa_sim_asas_stats(bsa_ctx *ctx, int64_t *out6);
  * *count = total (call again with a larger buffer when *count > cap). */
 int bsa_sim_resopairs(bsa_ctx *ctx, int32_t *idx1, int32_t *idx2, int64_t cap, int64_t *count);
 
-/* One CD call of the resident sim WITHOUT the kinematics: [all-gather] ->
+/* One CD call of the resident sim WITHOUT the kinematics: [halo exchange] ->
  * detect -> resolver -> asas.active or the bookkeeping + ResumeNav, i.e. the
  * body of ASAS.update (asas.py:478-504), exactly the CD part of a
  * bsa_sim_step; the state does not move and the step count does not advance.

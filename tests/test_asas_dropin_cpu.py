@@ -195,3 +195,50 @@ def test_no_context_means_no_compute():
         pytest.skip('a HIP device is visible here')
     with pytest.raises(_lib.AccelUnavailable):
         gasas.install(asas_obj(), traffic(['A']))
+
+
+def test_several_ranks_are_refused():
+    """a context joined to a communicator holds only its rows'
+    outputs (and no global counts): the drop-in refuses it up front."""
+    ctx = RecCtx()
+    ctx.comm_rank_world = (1, 2)
+    with pytest.raises(NotImplementedError, match='one rank only'):
+        gasas.install(asas_obj(), traffic(['A', 'B']), ctx=ctx)
+
+
+class Route:
+    """ap.route[i] stand-in: records Route.direct calls (asas.py:459-462)."""
+
+    def __init__(self, log, act):
+        self.log, self.act, self.wpname = log, act, ['WP0', 'WP1', 'WP2']
+
+    def findact(self, i):
+        return self.act
+
+    def direct(self, i, name):
+        self.log.append((i, name))
+
+
+def test_waypoint_recovery_follows_the_device_drop_flags():
+    """ResumeNav's waypoint recovery (asas.py:459-462): route.direct to the
+    active waypoint for exactly the aircraft whose pair the device dropped
+    (bsa_sim_read_asas `dropped`, aircraft-index order), none without an active
+    waypoint, nothing with waypoint_recovery=False."""
+    class DropCtx(RecCtx):
+        def sim_read_asas(self):
+            o = super().sim_read_asas()
+            o['dropped'] = np.array([False, True, False, True, True])
+            return o
+
+    log = []
+    t = traffic(['A', 'B', 'C', 'D', 'E'])
+    t.ap.route = [Route(log, 1), Route(log, 2), Route(log, 0), Route(log, -1), Route(log, 0)]
+    a = asas_obj()
+    gasas.install(a, t, ctx=DropCtx())
+    run(a, t, 0.0)
+    assert log == [(1, 'WP2'), (4, 'WP0')]
+    log.clear()
+    a2 = asas_obj()
+    gasas.install(a2, t, ctx=DropCtx(), waypoint_recovery=False)
+    run(a2, t, 0.0)
+    assert log == []

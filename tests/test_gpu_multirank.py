@@ -334,6 +334,51 @@ def test_halo_requests_and_regrowth_equal_world1(ctx):
     assert max(h[-1]['regrowths'] for h in halo) > 0
 
 
+def test_halo_wind_then_calm_equal_world1(ctx):
+    """with wind K4' computes gs / trk FROM gseast / gsnorth
+    (traffic.py:463-466), so a receiver may not rebuild gseast / gsnorth as
+    gs sin / cos(trk).  Steps with a constant wind, then set_params without
+    wind: the first calm exchange must still carry all 8 fields (only rows K4'
+    wrote without wind are derivable), and the run stays bitwise equal to the
+    one-rank run (state, gathered pair lists) at every step."""
+    t = synth.box(3000, 100.0, seed=97)
+    windy = resident.params(simdt=1.0, wind=(9.0, -14.0))
+    calm = resident.params(simdt=1.0)
+
+    def between(k, sim):
+        if k == 3:
+            sim.set_params(calm)
+
+    halo, exp = sharded_vs_world1(ctx, t, windy, 2, 6, between=between)
+    assert len(exp[3]['pairs']['ci']) > 0
+    # 8 fields per halo row up to the first calm CD call (its state is still
+    # K4' with wind), 6 from the next one on (rx_bytes: the capacities' regions)
+    for h in halo:
+        if h[4]['rx_bytes'] and h[3]['regrowths'] == h[4]['regrowths']:
+            assert h[3]['rx_bytes'] > h[4]['rx_bytes'] == h[5]['rx_bytes'], h
+
+
+def test_halo_capacity_disagreement_fails_loudly():
+    """RCCL's grouped send / recv hangs or truncates when a send
+    length differs from its receive length, which only 8 GPUs would show.  The
+    in-process group checks every (sender, receiver) region length against the
+    receiver's expectation at each exchange: one rank with a different copy of
+    one tile capacity fails loudly on one GPU, and its peer does not hang."""
+    t = synth.box(3000, 100.0, seed=97)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=1.0)
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=2, group=g)
+        sim.step(1)
+        if r == 1:
+            c.sim_set_halo_cap(0, 1, 0)
+        sim.step(1)
+
+    with pytest.raises(AssertionError, match='halo exchange: rank 0 sends'):
+        run_ranks(2, rank, timeout=200)
+
+
 def test_halo_probe_shares_equal_full_detect(ctx):
     """bsa_sim_detect_rows as one rank of 8 computes its share (own tiles, halo
     plan, halo tiles only) at the 100k bench workload: the 8 shares' pairs
