@@ -109,6 +109,49 @@ def dropin_detect_line(ctx, t, reps=3):
                      'h2d / detect / d2h / tuples / total in ms, median of %d' % reps)
 
 
+def asas_update_line(ctx, t, calls=6):
+    """the user-facing ``ASAS.update`` drop-in
+    (bluesky_amd.asas.DeviceASAS.update, asas.py:473-504) at 100k, history off,
+    MVP: wall time per phase of one call -- upload of the host simulator's
+    traffic (bsa_sim_update), the device CD call (detect + MVP + resopairs +
+    ResumeNav + unique / cumulative counts, bsa_sim_cd), the pair lists and
+    per-row outputs (bsa_fetch_pairs), the ASAS outputs and counts -- median of
+    ``calls`` after the first (which initialises the device sim).  Between
+    calls the host traffic moves by one 1 s step (positions along the track),
+    as BlueSky's own kinematics would have moved it."""
+    import types
+    from bluesky_amd import asas as gasas, mvp, statebased
+    n = t.ntraf
+    st = resident.initial_state(t)
+    traf = types.SimpleNamespace(id=['AC%d' % k for k in range(n)], ntraf=n)
+    for k in ('lat', 'lon', 'trk', 'gs', 'alt', 'vs', 'tas', 'hdg', 'gseast', 'gsnorth', 'selalt'):
+        setattr(traf, k, np.array(st[k]))
+    traf.ap = types.SimpleNamespace(trk=st['ap_trk'].copy(), tas=st['ap_tas'].copy(), alt=st['ap_alt'].copy(),
+                                    vs=st['ap_vs'].copy())
+    a = types.SimpleNamespace(swasas=True, tasas=0.0, dtasas=1.0, asaseval=False, noresolst=[], resoofflst=[],
+                              swnoreso=False, swresooff=False, priocode='FF1', R=synth.RPZ, dh=synth.HPZ,
+                              dtlookahead=synth.TLOOKAHEAD, Rm=synth.RPZ * 1.05, dhm=synth.HPZ * 1.05,
+                              vmin=200.0 * 1852 / 3600., vmax=500.0 * 1852 / 3600., vsmin=-3000. / 60. * 0.3048,
+                              vsmax=3000. / 60. * 0.3048, swresohoriz=True, swresospd=False, swresohdg=False,
+                              swresovert=False, swprio=False, resopairs=set(), confpairs_all=[], lospairs_all=[],
+                              cd=statebased, cr=mvp, alt=np.array(st['asas_alt']))
+    dev = gasas.install(a, traf, ctx=ctx)
+    tt = []
+    for k in range(calls + 1):
+        dev.update(float(k))
+        if k:
+            tt.append(dev.timings)
+        dn = traf.gsnorth / 6371000.0 * 57.29577951308232
+        traf.lat = traf.lat + dn
+        traf.lon = traf.lon + traf.gseast / (6371000.0 * np.cos(np.radians(traf.lat))) * 57.29577951308232
+    med = {key: float(np.median([x[key] for x in tt])) * 1e3 for key in tt[0]}
+    return dict(n=n, ms=med, n_conf=len(a.confpairs), n_los=len(a.lospairs), resopairs=len(a.resopairs),
+                confpairs_all=len(a.confpairs_all),
+                note='wall time of bluesky_amd.asas.DeviceASAS.update (ASAS.update drop-in, MVP, resume_nav, '
+                     'history off); upload / cd / pairs / asas_outputs / waypoints / total in ms, median of %d'
+                     % calls)
+
+
 def global1m_line(ctx, rank, world, warmup=2, steps=5):
     """BASELINE configs[4]: 1M aircraft uniform on the globe (|lat| <= 70 deg),
     the resident step (ASAS every step) row-sharded over the ranks -- the base
@@ -335,6 +378,8 @@ def main():
             d = dropin_detect_line(ctx, t)
             d['speedup_vs_cpu_detect'] = out['cpu_baseline']['detect_s_extrapolated'] * 1e3 / d['ms']['total']
             out['dropin_detect'] = d
+    if rank == 0 and world == 1 and not args.no_variants and args.workload == 'box100k':
+        out['asas_update'] = asas_update_line(ctx, t)
     if rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -49,6 +49,7 @@ traffic, so a context joined to a communicator or group (several ranks, each
 holding only its rows' outputs) raises ``NotImplementedError``.
 """
 import collections.abc
+import time
 import warnings
 
 import numpy as np
@@ -172,6 +173,7 @@ class DeviceASAS:
         self._reso = None       # the resopairs object last set on asas (reset detection)
         self._base = [0, 0]     # confpairs_all / lospairs_all counted before the last re-init
         self._prev_unique = (set(), set())   # history=True: last call's unique sets
+        self.timings = {}       # wall time [s] of the last call's phases (bench.py's asas_update line)
 
     # ------------------------------------------------------------- plumbing
     def _reso_mode(self):
@@ -274,6 +276,7 @@ class DeviceASAS:
         a.tasas += a.dtasas
         if not traf.ntraf:
             return
+        tm = [time.perf_counter()]
         self._check_cd()
         reso = self._reso_mode()
         p = self._params(reso)
@@ -288,7 +291,9 @@ class DeviceASAS:
         if noreso is not None or resooff is not None or self._lists:
             ctx.sim_set_reso_lists(noreso, resooff)
             self._lists = noreso is not None or resooff is not None
+        tm.append(time.perf_counter())
         ctx.sim_cd()
+        tm.append(time.perf_counter())
         st = ctx.sim_stats()
         o = ctx.fetch_pairs(st['n_conf'], st['n_los'])
         ids = self._idarr
@@ -296,6 +301,7 @@ class DeviceASAS:
         a.lospairs = PairList(ids, o['li'], o['lj'])
         a.inconf = o['inconf'].astype(bool)
         a.tcpamax, a.qdr, a.dist, a.tcpa, a.tLOS = o['tcpamax'], o['qdr'], o['dist'], o['tcpa'], o['tinconf']
+        tm.append(time.perf_counter())
         out = ctx.sim_read_asas()
         if len(a.confpairs):   # asas.py:486-487: the resolver ran
             if reso:
@@ -321,6 +327,7 @@ class DeviceASAS:
             a.confpairs_all = PairHistory(self._base[0] + bk['confpairs_all'])
             a.lospairs_all = PairHistory(self._base[1] + bk['lospairs_all'])
         a.resopairs = self._reso = ResoPairs(bk['resopairs'], self._resopairs)
+        tm.append(time.perf_counter())
         if self.waypoint_recovery and out['dropped'].any():
             routes = getattr(traf.ap, 'route', None)
             if routes is not None:   # asas.py:459-462
@@ -328,6 +335,9 @@ class DeviceASAS:
                     iwpid = routes[i].findact(i)
                     if iwpid != -1:
                         routes[i].direct(i, routes[i].wpname[iwpid])
+        tm.append(time.perf_counter())
+        self.timings = dict(upload=tm[1] - tm[0], cd=tm[2] - tm[1], pairs=tm[3] - tm[2],
+                            asas_outputs=tm[4] - tm[3], waypoints=tm[5] - tm[4], total=tm[5] - tm[0])
 
     _lists = False
 

@@ -263,6 +263,7 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
   const int k = tile * kTile + (int)threadIdx.x;
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
+  PFRec pk{};              // this lane's record (the fused boxes take it from registers)
   if (k < cnt) {
     const int o = presorted ? k : (int)perm[k];
     const double tlap = tla > 0.0 ? tla : 0.0;
@@ -327,6 +328,7 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
     if (shared && !(cosl > 1e-2)) v.flags = 1u;
     PC[k] = p;
     PV[k] = v;
+    pk = p;
   }
   if (rz.build) {  // one store per wave, no atomics
     const unsigned long long ob = __ballot(over);
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
     }
   }
   // K0c (fused): this thread wrote PC[k] above, every thread reaches the barrier
-  if (fb.gbox) tile_boxes(cnt, tile, PC, fgb, fb.sbox, fb.gbox, fb.tbox);
+  if (fb.gbox) tile_boxes_v(cnt, tile, pk, fgb, fb.sbox, fb.gbox, fb.tbox);
   if (fb.blk && threadIdx.x == 0) fb.blk[tile - fb.blk_base] = fb.tbox[tile];  // (written by this thread)
 }
 
@@ -1522,6 +1524,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
         // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
         double *rec = cpay + idx * kPayStride;
         if (flag && !B) rec[0] = __longlong_as_double((long long)(((unsigned long long)oi << 32) | oj));
+        // row buckets: word 0 carries the column's sorted (home) position, so
+        // K2's fused MVP reads the intruder's state without an id2h lookup
+        if (o.conf && B) rec[0] = __longlong_as_double((long long)p.y);
         if (o.conf) {
           rec[1] = o.qdr;
           rec[2] = o.dist;
@@ -1880,11 +1885,18 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
         pay[f] = cpay[(size_t)e.y * kPayStride + 1 + f];
         out[(size_t)f * P + pos] = pay[f];
       }
+      const unsigned jh = (unsigned)__double_as_longlong(cpay[(size_t)e.y * kPayStride]);  // (K1b: home column)
       if (lds) stc[so[lo] + rank] = pay[2];
       if (mf.pdv) {  // resident step: MVP's per-pair vector (MVP.py:33-56), folded below
         double4 dv;
         uint8_t fl;
-        mvp_pair(mf.p, mf.in, rb + row, (int)e.x, pay[0], pay[1], pay[2], pay[3], dv, fl);
+        MvpPairIn in = mf.in;
+        int j = (int)e.x;
+        if (in.id2h) {  // home order: the intruder's home position as K1b stored it
+          j = (int)jh;
+          in.id2h = nullptr;
+        }
+        mvp_pair(mf.p, in, rb + row, j, pay[0], pay[1], pay[2], pay[3], dv, fl);
         if (lds_fold) {
           sdv[so[lo] + rank] = dv;
           sfl[so[lo] + rank] = fl;

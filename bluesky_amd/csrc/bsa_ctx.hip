@@ -100,36 +100,147 @@ int download_pairs(Ctx *c, HostPairs &h) {
 // sort of the pairs by their row's index gives np.where's row-major order
 // (StateBasedCD.py:93-95); the per-row outputs of homes rb.. follow their
 // rows' ascending indices.
+// Linear in P + R (a comparison sort of the ~1.5e5 pairs took milliseconds):
+// the rows' ascending-index order is known up front -- the sim's rows are
+// [sim_rb, sim_re) with lpos_h, any other home slice is ordered once by a
+// counting pass over its indices -- so each row's contiguous segment is moved
+// to its row's place in that order.
 void home_pairs_to_ids(const Ctx *c, int64_t rb, HostPairs &h) {
   const unsigned *H = c->h2id_h.data();
-  std::vector<uint32_t> ord;
-  auto sort_rows = [&](std::vector<int32_t> &ri) {
-    for (auto &x : ri) x = (int32_t)H[x];
-    ord.resize(ri.size());
-    for (size_t k = 0; k < ord.size(); ++k) ord[k] = (uint32_t)k;
-    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return ri[a] < ri[b]; });
-  };
-  auto apply = [&](auto &v, size_t stride, size_t fields) {
-    auto w = v;
-    const size_t m = ord.size();
-    for (size_t f = 0; f < fields; ++f)
-      for (size_t k = 0; k < m; ++k) v[f * stride + k] = w[f * stride + ord[k]];
-  };
   const size_t P = h.ci.size(), L = h.li.size(), R = h.inconf.size();
-  sort_rows(h.ci);
-  apply(h.ci, P, 1);
-  apply(h.cj, P, 1);
-  apply(h.pay, P, 5);
-  sort_rows(h.li);
-  apply(h.li, L, 1);
-  apply(h.lj, L, 1);
-  std::vector<int32_t> rid(R);
-  for (size_t r = 0; r < R; ++r) rid[r] = (int32_t)H[rb + (int64_t)r];
-  ord.resize(R);
-  for (size_t k = 0; k < R; ++k) ord[k] = (uint32_t)k;
-  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return rid[a] < rid[b]; });
-  apply(h.inconf, R, 1);
-  apply(h.tcpamax, R, 1);
+  // byidx[k] = the home row (0..R-1, relative to rb) with the k-th smallest index
+  std::vector<uint32_t> byidx(R);
+  if (rb == c->sim_rb && (int64_t)R == c->sim_re - c->sim_rb && c->lpos_h.size() == R) {
+    for (size_t r = 0; r < R; ++r) byidx[c->lpos_h[r]] = (uint32_t)r;
+  } else {
+    std::vector<std::pair<uint32_t, uint32_t>> ir(R);
+    for (size_t r = 0; r < R; ++r) ir[r] = {H[rb + (int64_t)r], (uint32_t)r};
+    std::sort(ir.begin(), ir.end());
+    for (size_t k = 0; k < R; ++k) byidx[k] = ir[k].second;
+  }
+  // one list: segments by home row, then laid out in byidx order
+  auto reorder = [&](std::vector<int32_t> &ri, size_t m, auto &&move) {
+    std::vector<uint32_t> start(R + 1, 0u);
+    for (size_t k = 0; k < m; ++k) start[(size_t)(ri[k] - rb) + 1]++;
+    for (size_t r = 0; r < R; ++r) start[r + 1] += start[r];
+    size_t at = 0;
+    for (size_t k = 0; k < R; ++k) {
+      const uint32_t r = byidx[k];
+      for (uint32_t q = start[r]; q < start[r + 1]; ++q) move(at++, q);
+    }
+  };
+  {
+    std::vector<int32_t> ci(h.ci), cj(h.cj);
+    std::vector<double> pay(h.pay);
+    reorder(ci, P, [&](size_t to, uint32_t from) {
+      h.ci[to] = (int32_t)H[ci[from]];
+      h.cj[to] = cj[from];
+      for (size_t f = 0; f < 5; ++f) h.pay[f * P + to] = pay[f * P + from];
+    });
+  }
+  {
+    std::vector<int32_t> li(h.li), lj(h.lj);
+    reorder(li, L, [&](size_t to, uint32_t from) {
+      h.li[to] = (int32_t)H[li[from]];
+      h.lj[to] = lj[from];
+    });
+  }
+  std::vector<uint8_t> inc(h.inconf);
+  std::vector<double> tm(h.tcpamax);
+  for (size_t k = 0; k < R; ++k) {
+    h.inconf[k] = inc[byidx[k]];
+    h.tcpamax[k] = tm[byidx[k]];
+  }
+}
+
+// fetch_pairs of the resident sim's last CD call over this rank's rows: the
+// lists are put into aircraft-index order on the device (rows in ascending
+// index order, each row's contiguous segment moved whole), so the host copies
+// them out once -- no host-side re-ordering pass over ~8 MB at 100k.
+// k_fetch_lens: per row in index order its conflict / LoS segment lengths
+// (then scanned into the new offsets) and its inconf / tcpamax.
+__global__ __launch_bounds__(256) void k_fetch_lens(int R, const unsigned *__restrict__ byidx,
+                                                    const unsigned *__restrict__ rowoff, unsigned *__restrict__ lens,
+                                                    const uint8_t *__restrict__ inconf,
+                                                    const unsigned long long *__restrict__ tcpamax,
+                                                    uint8_t *__restrict__ o_inconf,
+                                                    unsigned long long *__restrict__ o_tcpamax) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > R) return;
+  if (k == R) {
+    lens[R] = 0u;
+    lens[2 * R + 1] = 0u;
+    return;
+  }
+  const unsigned r = byidx[k];
+  lens[k] = rowoff[r + 1] - rowoff[r];
+  lens[R + 1 + k] = rowoff[R + 2 + r] - rowoff[R + 1 + r];
+  o_inconf[k] = inconf[r];
+  o_tcpamax[k] = tcpamax[r];
+}
+// one lane per row in index order: its segments to their new offsets, home
+// rows mapped to aircraft indices
+__global__ __launch_bounds__(256) void k_fetch_scatter(int R, int rb, const unsigned *__restrict__ byidx,
+                                                       const unsigned *__restrict__ h2id,
+                                                       const unsigned *__restrict__ rowoff,
+                                                       const unsigned *__restrict__ noff, const int *__restrict__ cj,
+                                                       const double *__restrict__ pay, const int *__restrict__ lj,
+                                                       int *__restrict__ o_ci, int *__restrict__ o_cj,
+                                                       double *__restrict__ o_pay, int *__restrict__ o_li,
+                                                       int *__restrict__ o_lj) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= R) return;
+  const unsigned r = byidx[k];
+  const unsigned P = rowoff[R];
+  const int id = (int)h2id[rb + (int)r];
+  const unsigned s0 = rowoff[r], s1 = rowoff[r + 1], d0 = noff[k];
+  for (unsigned s = s0; s < s1; ++s) {
+    const unsigned d = d0 + (s - s0);
+    o_ci[d] = id;
+    o_cj[d] = cj[s];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) o_pay[(size_t)f * P + d] = pay[(size_t)f * P + s];
+  }
+  const unsigned l0 = rowoff[R + 1 + r] - P, l1 = rowoff[R + 2 + r] - P, e0 = noff[R + 1 + k] - P;
+  for (unsigned s = l0; s < l1; ++s) {
+    o_li[e0 + (s - l0)] = id;
+    o_lj[e0 + (s - l0)] = lj[s];
+  }
+}
+
+static int fetch_home_device(Ctx *c, int32_t *ci, int32_t *cj, double *const dst5[5], int32_t *li, int32_t *lj,
+                             uint8_t *inconf, double *tcpamax) {
+  const int64_t P = c->last_conf, L = c->last_los, R = c->last_re - c->last_rb;
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t o_ci = 0, o_cj = o_ci + al(P * 4), o_pay = o_cj + al(P * 4), o_li = o_pay + al(P * 40),
+               o_lj = o_li + al(L * 4), o_inc = o_lj + al(L * 4), o_tm = o_inc + al(R), o_len = o_tm + al(R * 8),
+               o_off = o_len + al(2 * (R + 1) * 4), total = o_off + al(2 * (R + 1) * 4);
+  if (!ensure(c, c->fetch_stage, total, "fetch staging")) return -1;
+  char *st = (char *)c->fetch_stage.p;
+  const unsigned *rowoff = (const unsigned *)c->rowoff.p;
+  hipLaunchKernelGGL(k_fetch_lens, dim3((unsigned)((R + 1 + 255) / 256)), dim3(256), 0, c->stream, (int)R,
+                     (const unsigned *)c->lbyidx.p, rowoff, (unsigned *)(st + o_len), (const uint8_t *)c->inconf.p,
+                     (const unsigned long long *)c->tcpamax.p, (uint8_t *)(st + o_inc),
+                     (unsigned long long *)(st + o_tm));
+  BSA_HIP(c, hipGetLastError());
+  if (scan_excl(c, (const unsigned *)(st + o_len), (unsigned *)(st + o_off), (int)(2 * (R + 1)))) return -1;
+  hipLaunchKernelGGL(k_fetch_scatter, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, c->stream, (int)R,
+                     (int)c->last_rb, (const unsigned *)c->lbyidx.p, (const unsigned *)c->h2id.p, rowoff,
+                     (const unsigned *)(st + o_off), (const int *)c->out_cj.p, (const double *)c->out_pay.p,
+                     (const int *)c->out_lj.p, (int *)(st + o_ci), (int *)(st + o_cj), (double *)(st + o_pay),
+                     (int *)(st + o_li), (int *)(st + o_lj));
+  BSA_HIP(c, hipGetLastError());
+  auto cp = [&](void *dst, size_t off, size_t bytes) -> int {
+    if (dst && bytes) BSA_HIP(c, hipMemcpyAsync(dst, st + off, bytes, hipMemcpyDeviceToHost, c->stream));
+    return 0;
+  };
+  if (cp(ci, o_ci, P * 4) || cp(cj, o_cj, P * 4) || cp(li, o_li, L * 4) || cp(lj, o_lj, L * 4) ||
+      cp(inconf, o_inc, R) || cp(tcpamax, o_tm, R * 8))
+    return -1;
+  for (int f = 0; f < 5; ++f)
+    if (cp(dst5[f], o_pay + (size_t)f * P * 8, P * 8)) return -1;
+  BSA_HIP(c, hipStreamSynchronize(c->stream));
+  return 0;
 }
 
 static int upload6(Ctx *c, DevBuf *dst, int64_t n, const double *const src[6]) {
@@ -294,7 +405,12 @@ int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *d
   };
   const double *pay = (const double *)c->out_pay.p;
   if (dcpa && !(c->last_flags & BSA_FLAG_WITH_DCPA)) return bsa::fail(c, "dcpa requested without BSA_FLAG_WITH_DCPA");
-  if (c->last_home) {  // resident sim: rows are home positions, translated on the host
+  if (c->last_home && c->last_rb == c->sim_rb && c->last_re == c->sim_re && c->lbyidx.p &&
+      c->last_re > c->last_rb) {  // the sim's own rows: re-ordered on the device
+    double *dst5[5] = {qdr, dist, tcpa, tinconf, dcpa};
+    return bsa::fetch_home_device(c, ci, cj, dst5, li, lj, inconf, tcpamax);
+  }
+  if (c->last_home) {  // another home slice (bsa_sim_detect_rows): translated on the host
     bsa::HostPairs h;
     if (bsa::download_pairs(c, h)) return -1;
     bsa::home_pairs_to_ids(c, c->last_rb, h);

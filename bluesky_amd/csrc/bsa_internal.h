@@ -214,6 +214,7 @@ struct Ctx {
 
   // MVP / kinematics staging (host-buffer entry points)
   DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl, mvp_rowdv;
+  DevBuf xfer_stage;  // batched home-order transfers (bsa_sim.hip: HomeBatch), index-order staging
 
   // multi-GPU: comm is an ncclComm_t (one process per GPU) or group an
   // in-process group of contexts (bsa_comm.hip); at most one is set
@@ -233,6 +234,8 @@ struct Ctx {
   bool det_home = false;              // detect_enqueue: home-ordered state (set by sim_cd)
   bool last_home = false;             // the last detect's ci / li are home rows (fetch translates)
   DevBuf h2id, id2h;                  // u32, device
+  DevBuf lbyidx;                      // u32, device: this rank's home rows (relative) in ascending index order
+  DevBuf fetch_stage;                 // fetch_pairs of a home-order detect: the lists re-ordered on the device
   std::vector<unsigned> h2id_h, id2h_h, lpos_h;  // host copies
   bool sim_ready = false;
   bool mvp_deferred = false;            // this step's K3 rows run inside K4' (sim_cd -> bsa_sim_step)

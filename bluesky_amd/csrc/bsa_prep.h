@@ -147,9 +147,9 @@ struct PrepOut {
   PFVel *PV;
   float4 *PP;
 };
-__device__ __forceinline__ void prep_home_record(int k, double la, double lo, double trk, double gs, double alt,
-                                                 double vs, double rpz, double hpz, double tla, int mid, int rec,
-                                                 const PrepOut &out) {
+__device__ __forceinline__ PFRec prep_home_record(int k, double la, double lo, double trk, double gs, double alt,
+                                                  double vs, double rpz, double hpz, double tla, int mid, int rec,
+                                                  const PrepOut &out) {
   const double tlap = tla > 0.0 ? tla : 0.0;
   const ColRec c = col_record_v(la, lo, trk, gs, alt, vs, la);
   if (rec) out.C[k] = c;
@@ -169,6 +169,7 @@ __device__ __forceinline__ void prep_home_record(int k, double la, double lo, do
   v.flags = (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) || !(cosl > 1e-2)) ? 1u : 0u;
   out.PC[k] = p;
   out.PV[k] = v;
+  return p;
 }
 
 __device__ __forceinline__ float xmin(float v, int o) { return fminf(v, __shfl_xor(v, o)); }
@@ -176,16 +177,17 @@ __device__ __forceinline__ float xmax(float v, int o) { return fmaxf(v, __shfl_x
 
 // Boxes of one kGroup-record group g (one wave, lane = record): its kSub-record
 // sub-group boxes to sbox (nullable) and the group box to gbox[g]; returns
-// the group box (lane 0).
-__device__ __forceinline__ TileBox group_boxes(int cnt, int g, const PFRec *__restrict__ P,
-                                               TileBox *__restrict__ sbox, TileBox *__restrict__ gbox) {
+// the group box (lane 0).  The lane's record p is passed in registers by the
+// lane that just computed it (reading it back from memory put a store ->
+// load round trip into K0b and K4'); lanes past cnt pass anything.
+__device__ __forceinline__ TileBox group_boxes_v(int cnt, int g, const PFRec &p, TileBox *__restrict__ sbox,
+                                                 TileBox *__restrict__ gbox) {
   const int lane = threadIdx.x & 63;
   const int k = g * kGroup + lane;
   const int ngroups = (cnt + kGroup - 1) / kGroup;
   float lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   float smax = 0.f;
   if (k < cnt) {
-    const PFRec p = P[k];
     lo[0] = hi[0] = p.x;
     lo[1] = hi[1] = p.y;
     lo[2] = hi[2] = p.z;
@@ -227,6 +229,13 @@ __device__ __forceinline__ TileBox group_boxes(int cnt, int g, const PFRec *__re
   if (lane == 0 && g < ngroups) gbox[g] = b;
   return b;
 }
+__device__ __forceinline__ TileBox group_boxes(int cnt, int g, const PFRec *__restrict__ P,
+                                               TileBox *__restrict__ sbox, TileBox *__restrict__ gbox) {
+  const int k = g * kGroup + (threadIdx.x & 63);
+  PFRec p{};
+  if (k < cnt) p = P[k];
+  return group_boxes_v(cnt, g, p, sbox, gbox);
+}
 
 // the empty box (the identity of box_union)
 __device__ __forceinline__ TileBox empty_box() {
@@ -247,11 +256,11 @@ __device__ __forceinline__ TileBox empty_box() {
 // Boxes of one kTile-record tile (workgroup = kTile lanes, one wave per
 // group): group_boxes, then their union to tbox[tile] (in group order).
 // Shared by k_boxes and the fused K0b+K0c path of k_prep_cols.
-__device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__restrict__ P, TileBox *gb,
-                                           TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
-                                           TileBox *__restrict__ tbox) {
+__device__ __forceinline__ void tile_boxes_v(int cnt, int tile, const PFRec &p, TileBox *gb,
+                                             TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
+                                             TileBox *__restrict__ tbox) {
   const int w = threadIdx.x >> 6;
-  const TileBox b = group_boxes(cnt, tile * kGroupsPerTile + w, P, sbox, gbox);
+  const TileBox b = group_boxes_v(cnt, tile * kGroupsPerTile + w, p, sbox, gbox);
   if ((threadIdx.x & 63) == 0) gb[w] = b;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -259,6 +268,14 @@ __device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__res
     for (int q = 1; q < kGroupsPerTile; ++q) u = box_union(u, gb[q]);
     tbox[tile] = u;
   }
+}
+__device__ __forceinline__ void tile_boxes(int cnt, int tile, const PFRec *__restrict__ P, TileBox *gb,
+                                           TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
+                                           TileBox *__restrict__ tbox) {
+  const int k = tile * kTile + (int)threadIdx.x;
+  PFRec p{};
+  if (k < cnt) p = P[k];
+  tile_boxes_v(cnt, tile, p, gb, sbox, gbox, tbox);
 }
 
 // tbox[t] from the group boxes of tile t (K0z after a K4' that wrote the group

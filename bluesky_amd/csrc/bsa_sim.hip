@@ -59,9 +59,9 @@ struct PrepArgs {
 // this lane then takes from its registers, MvpRowOut), so the row's memory
 // latency is paid about once instead of along a chain of dependent accesses.
 template <bool FUSE, bool PREP>
-__device__ __forceinline__ void pilot_kin_row(int rb, int k, double simdt, int winddim, double vwn, double vwe,
-                                              const WindField &wf, const SimDev &d, const MvpIn &mv,
-                                              const bsa_mvp_params &mp, const PrepArgs &pa) {
+__device__ __forceinline__ PFRec pilot_kin_row(int rb, int k, double simdt, int winddim, double vwn, double vwe,
+                                               const WindField &wf, const SimDev &d, const MvpIn &mv,
+                                               const bsa_mvp_params &mp, const PrepArgs &pa) {
   kin::In s;
   s.tas = d.tas[k];
   s.hdg = d.hdg[k];
@@ -140,7 +140,8 @@ __device__ __forceinline__ void pilot_kin_row(int rb, int k, double simdt, int w
   d.gsn[k] = o.gsnorth;
   d.altprev[k] = s.alt;
   d.ax[k] = o.ax;
-  if (PREP) prep_home_record(k, o.lat, o.lon, o.trk, o.gs, o.alt, o.vs, pa.rpz, pa.hpz, pa.tla, pa.mid, pa.rec, pa.out);
+  if (PREP) return prep_home_record(k, o.lat, o.lon, o.trk, o.gs, o.alt, o.vs, pa.rpz, pa.hpz, pa.tla, pa.mid, pa.rec, pa.out);
+  return PFRec{};
 }
 
 // Pilot.APorASAS (pilot.py:28-63; no wind, constant wind or a 2-D field) +
@@ -168,9 +169,10 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   }
   const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
-  if (PREP) {  // every lane reaches the wave's group reduction
-    if (k < re) pilot_kin_row<FUSE, PREP>(rb, k, simdt, winddim, vwn, vwe, wf, d, mv, mp, pa);
-    group_boxes(pa.n, k / kGroup, pa.out.PC, pa.sbox, pa.gbox);
+  if (PREP) {  // every lane reaches the wave's group reduction (its record from registers)
+    PFRec p{};
+    if (k < re) p = pilot_kin_row<FUSE, PREP>(rb, k, simdt, winddim, vwn, vwe, wf, d, mv, mp, pa);
+    group_boxes_v(pa.n, k / kGroup, p, pa.sbox, pa.gbox);
     return;
   }
   if (k >= re) return;
@@ -326,7 +328,8 @@ void sim_release(Ctx *c) {
                    &c->s_apalt, &c->s_apvs, &c->s_selalt, &c->s_bank, &c->s_eps, &c->s_accel,
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
                    &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env,
-                   &c->s_ptab, &c->s_ptype, &c->s_phase, &c->s_noreso, &c->s_resooff, &c->s_dropped, &c->s_atm};
+                   &c->s_ptab, &c->s_ptype, &c->s_phase, &c->s_noreso, &c->s_resooff, &c->s_dropped, &c->s_atm,
+                   &c->xfer_stage, &c->lbyidx, &c->fetch_stage};
   for (auto *b : all) release(*b);
   bk_release(c);
   halo_release(c);
@@ -341,6 +344,82 @@ static void by_size(size_t esz, F f) {
   else if (esz == 4) f((const uint32_t *)nullptr);
   else f((const uint8_t *)nullptr);
 }
+
+// Batched home-order transfers of whole arrays (h in [0, n)): the host
+// arrays cross PCIe as they are, in aircraft-index order (one async copy
+// each into a device staging area), and ONE kernel permutes every field on
+// the device -- dst[h] = stage[h2id[h]] on upload, stage[h2id[h]] = src[h] on
+// download -- with one stream synchronisation per batch.  (Per array, the
+// host-side permutation loop and a synchronisation each cost the ASAS drop-in
+// ~0.2 ms per array at 100k aircraft.)
+constexpr int kXferMax = 24;
+struct XferFields {
+  void *dev[kXferMax];
+  unsigned long long off[kXferMax];  // byte offset of the field in the staging area
+  int esz[kXferMax];
+  int nf, up;
+};
+__global__ __launch_bounds__(256) void k_home_xfer(int n, XferFields f, const unsigned *__restrict__ h2id,
+                                                   unsigned char *__restrict__ stage) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= n) return;
+  const unsigned i = h2id[h];
+  for (int q = 0; q < f.nf; ++q) {
+    unsigned char *sp = stage + f.off[q];
+    unsigned char *dp = (unsigned char *)f.dev[q];
+    if (f.esz[q] == 8) {
+      if (f.up) ((unsigned long long *)dp)[h] = ((const unsigned long long *)sp)[i];
+      else ((unsigned long long *)sp)[i] = ((const unsigned long long *)dp)[h];
+    } else if (f.esz[q] == 4) {
+      if (f.up) ((unsigned *)dp)[h] = ((const unsigned *)sp)[i];
+      else ((unsigned *)sp)[i] = ((const unsigned *)dp)[h];
+    } else {
+      if (f.up) dp[h] = sp[i];
+      else sp[i] = dp[h];
+    }
+  }
+}
+
+struct HomeBatch {
+  Ctx *c;
+  bool up;
+  XferFields f{};
+  const void *hsrc[kXferMax] = {};
+  void *hdst[kXferMax] = {};
+  size_t bytes = 0;
+  HomeBatch(Ctx *cc, bool upload) : c(cc), up(upload) { f.up = upload ? 1 : 0; }
+  // upload: device array dev <- host src (index order); download: host dst <- dev
+  int add(void *dev, const void *hsrc_, void *hdst_, int esz) {
+    if (f.nf == kXferMax && run()) return -1;
+    const int q = f.nf++;
+    f.dev[q] = dev;
+    f.esz[q] = esz;
+    f.off[q] = bytes;
+    hsrc[q] = hsrc_;
+    hdst[q] = hdst_;
+    bytes += ((size_t)c->n * esz + 255) / 256 * 256;
+    return 0;
+  }
+  int run() {
+    const int64_t n = c->n;
+    if (f.nf == 0 || n <= 0) return 0;
+    if (!ensure(c, c->xfer_stage, bytes, "transfer staging")) return -1;
+    unsigned char *st = (unsigned char *)c->xfer_stage.p;
+    if (up)
+      for (int q = 0; q < f.nf; ++q)
+        BSA_HIP(c, hipMemcpyAsync(st + f.off[q], hsrc[q], (size_t)n * f.esz[q], hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_home_xfer, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, (int)n, f,
+                       (const unsigned *)c->h2id.p, st);
+    BSA_HIP(c, hipGetLastError());
+    if (!up)
+      for (int q = 0; q < f.nf; ++q)
+        BSA_HIP(c, hipMemcpyAsync(hdst[q], st + f.off[q], (size_t)n * f.esz[q], hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+    f.nf = 0;
+    bytes = 0;
+    return 0;
+  }
+};
 
 // dst[h] (device) = src[h2id[h]] (host), h in [0, n)
 static int put_home(Ctx *c, void *dst, const void *src, size_t esz, std::vector<char> &tmp) {
@@ -387,6 +466,8 @@ int set_home_maps(Ctx *c) {
   std::sort(ord.begin(), ord.end(), [&](unsigned a, unsigned b) { return c->h2id_h[rb + a] < c->h2id_h[rb + b]; });
   c->lpos_h.assign((size_t)nr, 0u);
   for (int64_t k = 0; k < nr; ++k) c->lpos_h[ord[(size_t)k]] = (unsigned)k;
+  if (!ensure(c, c->lbyidx, (size_t)std::max<int64_t>(nr, 1) * 4, "rows by index")) return -1;
+  if (nr) BSA_HIP(c, hipMemcpyAsync(c->lbyidx.p, ord.data(), (size_t)nr * 4, hipMemcpyHostToDevice, c->stream));
   if (!ensure(c, c->h2id, (size_t)n * 4, "home -> index") || !ensure(c, c->id2h, (size_t)n * 4, "index -> home"))
     return -1;
   BSA_HIP(c, hipMemcpyAsync(c->h2id.p, c->h2id_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
@@ -808,7 +889,7 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
             {s->asas_alt, c->s_aalt.p}};
   // the replicated CD inputs are rewritten on every rank (in the sim's home order)
   bool any_cd = false, all_rep = true;
-  std::vector<char> tmp;
+  bsa::HomeBatch hb(c, true);
   for (int k = 0; k < 19; ++k) {
     const bool rep = k < 6 || k == 8 || k == 9;  // the arrays the all-gather replicates
     if (!cp[k].src) {
@@ -816,8 +897,9 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
       continue;
     }
     if (k < 10) any_cd = true;
-    if (bsa::put_home(c, cp[k].dst, cp[k].src, 8, tmp)) return -1;
+    if (hb.add(cp[k].dst, cp[k].src, nullptr, 8)) return -1;
   }
+  if (hb.run()) return -1;
   c->sim_prepped = false;  // prepared records are of the old state
   if (any_cd) {
     // every rank passed the same full arrays: the replicas are consistent only
@@ -847,10 +929,10 @@ int bsa_sim_read(bsa_ctx *cc, bsa_sim_out *o) {
             {o->gsnorth, c->s_gsn.p, 8},   {o->asas_trk, c->s_atrk.p, 8}, {o->asas_tas, c->s_atas.p, 8},
             {o->asas_vs, c->s_avs.p, 8},   {o->asas_alt, c->s_aalt.p, 8},
             {o->active, c->s_active.p, 1}};
-  std::vector<char> tmp;
+  bsa::HomeBatch hb(c, false);
   for (auto &e : cp)
-    if (e.dst && bsa::get_home(c, e.dst, e.src, e.esz, 0, c->n, tmp)) return -1;
-  return 0;
+    if (e.dst && hb.add(const_cast<void *>(e.src), nullptr, e.dst, (int)e.esz)) return -1;
+  return hb.run();
 }
 
 int bsa_sim_stats(bsa_ctx *cc, int64_t *out6) {
@@ -1053,6 +1135,12 @@ int bsa_sim_read_asas(bsa_ctx *cc, bsa_asas_out *o) {
   } cp[] = {{o->trk, c->s_atrk.p, 8},   {o->tas, c->s_atas.p, 8},     {o->vs, c->s_avs.p, 8},
             {o->alt, c->s_aalt.p, 8},   {o->asase, c->s_ase.p, 4},    {o->asasn, c->s_asn.p, 4},
             {o->active, c->s_active.p, 1}, {o->dropped, c->s_dropped.p, 1}};
+  if (c->sim_rb == 0 && c->sim_re == c->n) {  // one rank: every row, one batch
+    bsa::HomeBatch hb(c, false);
+    for (auto &e : cp)
+      if (e.dst && hb.add(const_cast<void *>(e.src), nullptr, e.dst, (int)e.esz)) return -1;
+    return hb.run();
+  }
   std::vector<char> tmp;
   for (auto &e : cp)
     if (e.dst && bsa::get_home(c, e.dst, e.src, e.esz, c->sim_rb, c->sim_re, tmp)) return -1;

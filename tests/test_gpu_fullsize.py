@@ -2,6 +2,8 @@
 configs[4] global 1M) -- the cases the golden fixtures are too small for.
 
 * box10k: the whole detect against the oracle (10^8 pairs, ~15-30 s of CPU).
+* box100k: the whole detect against the oracle's (10^10 pairs, evaluated on
+  the CPU of the build container by tools/make_fullrows.py into a fixture).
 * Exact-safety of the culling at full size: the pruned detect (fp32 stage 1 +
   CPA refine) must equal the unpruned one
   (BSA_FLAG_NOPRUNE: every pair of the rows evaluated in fp64), bitwise, for
@@ -52,6 +54,36 @@ def test_box10k_full_vs_oracle(ctx):
     util.assert_detect_equal(got, exp, RPZ, TLA)
     # the survey's probe count for this recipe at seed 7
     assert (len(got['ci']), len(got['li'])) == (14317, 2228)
+
+
+def test_box100k_every_row_vs_oracle_fixture(ctx):
+    """BASELINE configs[3] against the ORACLE over every row:
+    tests/golden/full_box100k.npz holds the oracle's StateBasedCD.detect of the
+    whole 100k box (1e10 pairs, evaluated on the CPU by tools/make_fullrows.py):
+    the HIP detect's conflict / LoS pair lists equal it pair for pair and in
+    order, inconf exactly, and qdr / dist / tcpa / tinconf / dcpa / tcpamax
+    within 1e-9 relative (tests/util.py)."""
+    import hashlib
+    path = util.golden('full_box100k.npz')
+    assert path, 'tests/golden/full_box100k.npz missing (python tools/make_fullrows.py)'
+    z = dict(np.load(path[0], allow_pickle=False))
+    t = synth.workload('box100k')
+    h = hashlib.sha256()
+    for f in ('lat', 'lon', 'trk', 'gs', 'alt', 'vs'):
+        h.update(np.ascontiguousarray(getattr(t, f), dtype=np.float64).tobytes())
+    assert h.hexdigest() == str(z['state_sha256']), 'the synthetic box100k differs from the fixture\'s'
+    got = statebased.detect_indices(t, t, float(z['rpz']), float(z['hpz']), float(z['tla']), ctx=ctx,
+                                    with_dcpa=True)
+    n = int(z['n'])
+    inconf = np.unpackbits(z['inconf_bits'])[:n].astype(bool)
+    tcpamax = np.zeros(n)
+    tcpamax[inconf] = z['tcpamax_inconf']
+    exp = dict(ci=z['ci'], cj=z['cj'], li=z['li'], lj=z['lj'], qdr=z['qdr'], dist=z['dist'], tcpa=z['tcpa'],
+               tinconf=z['tinconf'], inconf=inconf, tcpamax=tcpamax)
+    util.assert_detect_equal(got, exp, RPZ, TLA)
+    ok, msg = util.close(got['dcpa'], z['dcpa'], RPZ)
+    assert ok, 'dcpa: %s' % msg
+    assert len(exp['ci']) > 100000 and len(exp['li']) > 10000
 
 
 def test_noprune_row_sweep_100k_bitwise(ctx):

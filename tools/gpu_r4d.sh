@@ -1,0 +1,20 @@
+# Round 4, pass d: parity of the fetch / K2 changes, K1b grid A/B, bench line with asas_update.
+set -u
+OUT=gpurun_out/r4d
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_gpu_asas_dropin.py tests/test_gpu_sim.py tests/test_gpu_trace.py tests/test_gpu_multirank.py tests/test_gpu_detect.py tests/test_gpu_mvp_kin.py tests/test_gpu_feed.py tests/test_gpu_reuse.py -m "gpu" -k "not 8ranks and not key_blocks" -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
+[ $rc -eq 0 ] || exit $rc
+for G in 0 600 1200 0 600 1200; do
+  BSA_K1B_GRID=$G timeout -k 10 200 python bench.py --steps 40 --warmup 5 --no-cpu --no-variants > $OUT/bench_g$G.json 2> $OUT/bench_g$G.err || { tail -3 $OUT/bench_g$G.err; exit 1; }
+  python -c "
+import json; d=json.load(open('$OUT/bench_g$G.json'))
+print('grid $G ms/step %.4f' % d['ms_per_step'], {k: round(v, 4) if isinstance(v, float) else v for k, v in d['kernels_ms_rank0'].items()})"
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- \
+    python bench.py --steps 20 --warmup 3 --no-cpu --no-variants > $OUT/prof_stats.log 2>&1
+rc=$?; echo "stats rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu > $OUT/bench_full.json 2> $OUT/bench_full.err
+rc=$?; echo "bench rc=$rc"; python -c "
+import json; d=json.load(open('$OUT/bench_full.json')); print('asas_update', d.get('asas_update')); print('dropin', d.get('dropin_detect'))"
