@@ -36,9 +36,18 @@ OPS_PER_PAIR = 110           # algorithmic fp64 ops per pair-eval
 PF_FLOPS_PER_PAIR = 9        # prefilter stage-1 fp32 flops per tested pair:
                              # acc = K + k (1) + 3 FMA (6); lo - hi, hi - lo (2)
 KIN_BYTES_PER_AC = 234       # K4 algorithmic HBM bytes per aircraft-step
-PREP_BYTES_PER_AC = 128 + 32 + 16 + 16 + 48 / 8 + 48 / 64   # K4' also writing the next detect's column
-                             # records (fp64 128 B when stored, PFRec, PFVel, position) and sub-group /
-                             # group boxes (one rank)
+PREP_BYTES_PER_AC = 32 + 16 + 16 + 48 / 8 + 48 / 64   # K4' also writing the next detect's column
+                             # records (PFRec, PFVel, position) and sub-group / group boxes (one rank,
+                             # DESIGN.md 3.7) ...
+PREP_REC_BYTES = 128         # ... plus the 128-B fp64 record when the library stores it (home_records:
+                             # rows <= 163840 unless BSA_HOME_REC overrides, bsa_cd.hip)
+
+
+def prep_bytes_per_ac(n):
+    """K4''s next-detect bytes per aircraft for a one-rank sim of n aircraft."""
+    env = os.environ.get('BSA_HOME_REC')
+    rec = (env == '1') if env in ('0', '1') else n <= 163840
+    return PREP_BYTES_PER_AC + (PREP_REC_BYTES if rec else 0)
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E (spec)
 PMC_JSON = os.path.join(REPO, 'profiles', 'pmc_latest.json')
 TIMING_SAMPLE = 8            # detects per HIP-event-timed detect (bsa_set_timing_sample; each timed one
@@ -285,6 +294,7 @@ def main():
     ctx.allreduce_max([0.0])     # barrier
     ctx.sync()
     ctx.timing_reset()
+    tr0 = ctx.tile_reuse_stats()
     t0 = time.perf_counter()
     sim.step(args.steps)         # one batch: no host synchronisation between steps
     ctx.sync()
@@ -294,6 +304,9 @@ def main():
     tm, ts = ctx.timing_summary()
     st = sim.stats()
     counts = ctx.allreduce_sum([st['n_conf'], st['n_los'], ts['candidates'] / max(ts['detects'], 1)])
+    tr = ctx.tile_reuse_stats()   # tile-pair list (K0d) builds / detects of this run
+    tile_reuse = dict(builds=tr['builds'] - tr0['builds'], detects=tr['detects'] - tr0['detects'],
+                      note='K0d tile-pair list rebuilt on the device when a record left its drift budget')
 
     cd_steps = sum(1 for k in range(args.warmup, args.warmup + args.steps) if k % args.cd_every == 0)
     pairs = float(n) * n * cd_steps
@@ -321,10 +334,10 @@ def main():
     if kin.get('dur_ns'):
         nrows_r0 = (n + world - 1) // world
         prep = world == 1 and not args.reuse and os.environ.get('BSA_SIM_PREP', '1') != '0'
-        alg = int((KIN_BYTES_PER_AC + (PREP_BYTES_PER_AC if prep else 0)) * nrows_r0)
+        pb = prep_bytes_per_ac(n) if prep else 0
+        alg = int((KIN_BYTES_PER_AC + pb) * nrows_r0)
         propagation = dict(kernel='k_sim_pilot_kin', bound='hbm', algorithmic_bytes=alg, from_profile=prov,
-                           bytes_per_aircraft=dict(kinematics=KIN_BYTES_PER_AC,
-                                                   next_detect_records=PREP_BYTES_PER_AC if prep else 0),
+                           bytes_per_aircraft=dict(kinematics=KIN_BYTES_PER_AC, next_detect_records=pb),
                            duration_us_profiled=kin['dur_ns'] * 1e-3,
                            achieved_GBps=alg / kin['dur_ns'], peak_GBps=HBM_PEAK_GBPS,
                            frac=alg / kin['dur_ns'] / HBM_PEAK_GBPS,
@@ -351,6 +364,7 @@ def main():
                                      k2_sort=tm['sort'], detect_total=tm['total'],
                                      timed_detects='1 in %d' % TIMING_SAMPLE),
                prefilter_pair_tests_rank0=tested,
+               tile_reuse_rank0=tile_reuse,
                tile_pairs_rank0=ts['tiles'] / max(ts['detects'], 1),
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),

@@ -57,6 +57,8 @@ SIGNATURES = {
     'bsa_last_tiles': (ctypes.c_int, [_vp, _c_i64p, _c_i64p, _c_i64p]),
     'bsa_set_candidate_reuse': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_double]),
     'bsa_reuse_stats': (ctypes.c_int, [_vp, _c_i64p, _c_i64p]),
+    'bsa_set_tile_reuse': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_double]),
+    'bsa_tile_reuse_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_reuse_budget_use': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_timing_reset': (ctypes.c_int, [_vp]),
@@ -436,6 +438,17 @@ class Context:
         every aircraft's drift stays inside its budgets (exact either way)."""
         self.check(self.lib.bsa_set_candidate_reuse(self.h, int(bool(on)), float(sigma_h), float(sigma_v)),
                    'bsa_set_candidate_reuse')
+
+    def set_tile_reuse(self, on=True, sigma_h=2016.0, sigma_v=300.0):
+        """bsa_set_tile_reuse: keep the resident detect's tile-pair list (K0d) while
+        every prefilter record stays within the budgets of its build-time record."""
+        self.check(self.lib.bsa_set_tile_reuse(self.h, int(bool(on)), float(sigma_h), float(sigma_v)),
+                   'bsa_set_tile_reuse')
+
+    def tile_reuse_stats(self):
+        v = np.zeros(2, np.int64)
+        self.check(self.lib.bsa_tile_reuse_stats(self.h, ptr(v, _c_i64p)), 'bsa_tile_reuse_stats')
+        return dict(builds=int(v[0]), detects=int(v[1]))
 
     def reuse_stats(self):
         b, d = ctypes.c_int64(), ctypes.c_int64()

@@ -42,4 +42,28 @@ __device__ __forceinline__ bool boxes_may_interact(const TileBox &a, const TileB
   return !(d2 >= st * st) && (b.vlo < a.vhi) && (b.vhi > a.vlo);
 }
 
+// Tile-pair list reuse: a box grown by dx in every unit-vector
+// axis, ds in reach and dv vertically (plus a rounding margin far above one
+// fp32 ulp of the values), and the matching per-record test -- a record within
+// (dx, ds, dv) of its record at the build lies inside every box grown from a
+// box that held the build record, so every pair the boxes of the current
+// records could keep, the grown boxes of the build kept (boxes_may_interact is
+// monotone in the extents).  NaN fails the test (a rebuild), never passes it.
+constexpr float kTprPad = 1e-6f;   // chord / reach units (fp32 ulp of a unit vector ~6e-8)
+constexpr float kTprPadV = 1.0f;   // m (fp32 ulp at 20 km ~2e-3)
+__device__ __forceinline__ TileBox box_grow(TileBox b, float dx, float ds, float dv) {
+  for (int q = 0; q < 3; ++q) {
+    b.lo[q] -= dx + kTprPad;
+    b.hi[q] += dx + kTprPad;
+  }
+  b.smax += ds + kTprPad;
+  b.vlo -= dv + kTprPadV;
+  b.vhi += dv + kTprPadV;
+  return b;
+}
+__device__ __forceinline__ bool pf_within(const PFRec &p, const PFRec &b, float dx, float ds, float dv) {
+  return fabsf(p.x - b.x) <= dx && fabsf(p.y - b.y) <= dx && fabsf(p.z - b.z) <= dx && p.s <= b.s + ds &&
+         p.lo >= b.lo - dv && p.hi <= b.hi + dv;
+}
+
 }  // namespace bsa

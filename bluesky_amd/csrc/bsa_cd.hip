@@ -550,6 +550,18 @@ __global__ __launch_bounds__(kTPThreads) void k_tilepairs(int nrt, int nct, int 
 // union loads, its scan and its barrier were a third of K0d's chain there
 constexpr int kTPDirectThreads = 256;
 constexpr int kTPDirectMax = 1024;  // column tiles up to which K0d runs direct
+// Tile-pair list reuse: ctl == NULL -> off (the list is this
+// detect's own); else K0d builds (grown boxes, snapshot of the records) only
+// when forced by the host or flagged by the records' preparer (ctl[0]), and
+// the prefilter publishes the built list's item counts (ctl[1], ctl[2])
+struct TprArgs {
+  unsigned long long *ctl;
+  int force;
+  float dx, ds, dv;
+  const PFRec *pc;  // this detect's column records (rows = columns)
+  PFRec *snap;
+};
+
 // Halo mode (hl != NULL): the columns are this rank's own tiles [p0, p1) and
 // the received halo tiles hl[0, nhl) (-1: an unused slot; *nhl_dev bounds the
 // list when set), not all nct tiles -- one rank of 8 at 1M holds ~300 of the
@@ -561,8 +573,15 @@ __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
     const TileBox *__restrict__ cb, int noprune, uint2 *__restrict__ out, unsigned long long cap,
     Counters *__restrict__ cnt, unsigned long long *__restrict__ icnt, const unsigned *__restrict__ build,
     const uint8_t *__restrict__ present, int p0, int p1, const TileBox *__restrict__ gbc,
-    const int *__restrict__ hl, int nhl, const unsigned *__restrict__ nhl_dev) {
+    const int *__restrict__ hl, int nhl, const unsigned *__restrict__ nhl_dev, TprArgs tp) {
   if (build && !build[0]) return;
+  // tile-pair list reuse: no build this detect -> the kept
+  // list's item counts into the dequeue words, nothing else
+  const bool grow = tp.ctl != nullptr;
+  if (grow && !(tp.force || tp.ctl[0] != 0ull)) {
+    if (blockIdx.x == 0 && threadIdx.x < 2) icnt[1 + threadIdx.x] = tp.ctl[1 + threadIdx.x];
+    return;
+  }
   __shared__ TileBox sgb[kSlicesPerTile];
   __shared__ unsigned wpre[4][kTPDirectThreads / 64];
   __shared__ unsigned long long bbase[2];
@@ -590,15 +609,27 @@ __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
   if (threadIdx.x < kSlicesPerTile && rt * kTile + (int)threadIdx.x * kGroup < nrows)
     sgb[threadIdx.x] = rg[rt * kSlicesPerTile + threadIdx.x];
   TileBox a = gbc ? empty_box() : rb[rt];
+  if (grow) {  // a build: the snapshot of this row tile's records (rows = columns here)
+    for (int k = rt * kTile + (int)threadIdx.x; k < min(nrows, (rt + 1) * kTile); k += kTPDirectThreads)
+      tp.snap[k] = tp.pc[k];
+  }
   __syncthreads();
   if (gbc) {  // the row tile's groups are its slices (rows = columns): tile_from_groups' union from LDS
     a = sgb[0];
     for (int q = 1; q < kSlicesPerTile; ++q) a = box_union(a, rt * kTile + q * kGroup < nrows ? sgb[q] : empty_box());
   }
+  if (grow) {  // the list outlives this detect: every box grown by the drift budgets
+    a = box_grow(a, tp.dx, tp.ds, tp.dv);
+    bc = box_grow(bc, tp.dx, tp.ds, tp.dv);
+    __syncthreads();  // (every lane has read sgb above)
+    if (threadIdx.x < kSlicesPerTile) sgb[threadIdx.x] = box_grow(sgb[threadIdx.x], tp.dx, tp.ds, tp.dv);
+    __syncthreads();
+  }
   for (int c0 = 0; c0 < ncols; c0 += kTPDirectThreads) {
     if (c0 > 0) {
       ct = col_of(c0 + (int)threadIdx.x);
       if (ct >= 0) bc = gbc ? tile_of(ct) : cb[ct];
+      if (grow) bc = box_grow(bc, tp.dx, tp.ds, tp.dv);
     }
     bool kn = false, kf = false;
     unsigned sm = 0;
@@ -606,9 +637,26 @@ __global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
     tp_emit<kTPDirectThreads>(kn, kf, sm, rt, ct, out, cap, cnt, icnt, wpre, bbase);
     __syncthreads();  // wpre / bbase are rewritten by the next round
   }
-  if (hl)  // the tiles this rank does not hold: none may be reachable (no appends, no barriers)
-    for (int t = (int)threadIdx.x; t < nct; t += kTPDirectThreads)
-      if (!(t >= p0 && t < p1) && !present[t] && (noprune || boxes_may_interact(a, cb[t]))) cnt->halo_miss = 1;
+  if (hl) {  // the tiles this rank does not hold: none may be reachable (no appends, no barriers;
+             // 4 tiles' loads per lane issued together, not one dependent round trip per tile)
+    bool miss = false;
+    for (int t0 = (int)threadIdx.x; t0 < nct; t0 += 4 * kTPDirectThreads) {
+      TileBox b[4];
+      uint8_t pr[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = min(t0 + u * kTPDirectThreads, nct - 1);
+        b[u] = cb[t];
+        pr[u] = present[t];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * kTPDirectThreads;
+        miss |= t < nct && !(t >= p0 && t < p1) && !pr[u] && (noprune || boxes_may_interact(a, b[u]));
+      }
+    }
+    if (miss) cnt->halo_miss = 1;
+  }
 }
 
 __device__ __forceinline__ unsigned long long wave_bcast_u64(unsigned long long v) {
@@ -796,7 +844,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const uint2 *__restrict__ items, unsigned long long icap,
     Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
-    uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn, int diag) {
+    uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn, int diag,
+    TprArgs tp) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
   __shared__ float4 cen[PF_WAVES][32];      //                      e e' n n'     (stage 1)
@@ -810,6 +859,15 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ unsigned char sgs[PF_WAVES][kSubsPerBatch];  // the next batch's sub-groups (tile-local)
   __shared__ uint2 cst[PF_WAVES][PF_RES];   // staged candidates (row, column) of the wave
   if (build && !build[0]) return;  // reused candidate list
+  if (tp.ctl && blockIdx.x == 0 && threadIdx.x == 0) {  // tile-pair list reuse: K0d is complete here
+    if (tp.force || tp.ctl[0] != 0ull) {  // it built: keep the list's counts, clear the flag
+      tp.ctl[1] = work[1];
+      tp.ctl[2] = work[2];
+      tp.ctl[0] = 0ull;
+      tp.ctl[3] += 1ull;
+    }
+    tp.ctl[4] += 1ull;
+  }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned short *q1 = q1s[w];
   float *ska = (float *)cka[w];
@@ -1872,9 +1930,25 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
     const unsigned k = q - so[lo], m = so[lo + 1] - so[lo];
     const int row = b * kRankRows + lo;
     const uint2 *bk = kb + ((size_t)(conf ? 0 : nrows) + row) * B;
-    const uint2 e = bk[k];
+    uint2 e;
     unsigned rank = 0;
-    for (unsigned y = 0; y < m; ++y) rank += (bk[y].x < e.x) ? 1u : 0u;
+    if (B == 8) {  // the whole bucket (one 64-B line, always allocated) in 4 loads issued together,
+                   // not one dependent round trip per entry of the row
+      uint4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = reinterpret_cast<const uint4 *>(bk)[u];
+      const unsigned col[8] = {q[0].x, q[0].z, q[1].x, q[1].z, q[2].x, q[2].z, q[3].x, q[3].z};
+      const unsigned cid[8] = {q[0].y, q[0].w, q[1].y, q[1].w, q[2].y, q[2].w, q[3].y, q[3].w};
+      e = make_uint2(0u, 0u);
+#pragma unroll
+      for (unsigned y = 0; y < 8; ++y)
+        if (y == k) e = make_uint2(col[y], cid[y]);
+#pragma unroll
+      for (unsigned y = 0; y < 8; ++y) rank += (y < m && col[y] < e.x) ? 1u : 0u;
+    } else {
+      e = bk[k];
+      for (unsigned y = 0; y < m; ++y) rank += (bk[y].x < e.x) ? 1u : 0u;
+    }
     if (conf) {
       const unsigned pos = cb + so[lo] + rank;
       ci[pos] = rb + row;
@@ -2362,13 +2436,39 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // flat halo list; BSA_TP_HALO_ALL=1 sweeps all tiles for A/B)
   static const bool tp_all = getenv("BSA_TP_HALO_ALL") && atoi(getenv("BSA_TP_HALO_ALL")) == 1;
   const bool tp_list = halo && !tp_all && !tp_super;
+  // tile-pair list reuse: the resident step's detects of all
+  // rows whose records K4' prepared (and checked against the last build's);
+  // any other detect of this context invalidates the kept list
+  static const bool tpr_env = !(getenv("BSA_TPR") && atoi(getenv("BSA_TPR")) == 0);
+  TprArgs tp{};
+  const bool tpr = tpr_env && c->tpr_on && prepped && nct <= kTPDirectMax && !tp_super && !tp_list;
+  if (tpr) {
+    if (!ensure(c, c->tpr_snap, (size_t)n * sizeof(PFRec), "tile-pair list snapshot")) return -1;
+    const bool fresh = !c->tpr_ctl.p;
+    if (!ensure(c, c->tpr_ctl, 64, "tile-pair list control")) return -1;
+    if (fresh) BSA_HIP(c, hipMemsetAsync(c->tpr_ctl.p, 0, 64, c->stream));
+    const double key[4] = {rpz, hpz, tla, (double)mid};
+    const bool valid = c->tpr_valid && c->tpr_n == n && memcmp(key, c->tpr_key, sizeof key) == 0;
+    static const double sh_env = getenv("BSA_TPR_SH") ? atof(getenv("BSA_TPR_SH")) : 0.0;  // (A/B) [m]
+    if (sh_env > 0.0) {
+      c->tpr_dx = (float)(sh_env / 6.3e6);
+      c->tpr_ds = (float)(sh_env / 6.3e6 / 20);
+    }
+    tp = TprArgs{(unsigned long long *)c->tpr_ctl.p, valid ? 0 : 1, c->tpr_dx, c->tpr_ds, c->tpr_dv,
+                 (const PFRec *)c->pfcol.p, (PFRec *)c->tpr_snap.p};
+    c->tpr_valid = true;  // (an aborted step clears it: grow_after_abort)
+    memcpy(c->tpr_key, key, sizeof key);
+    c->tpr_n = n;
+  } else {
+    c->tpr_valid = false;
+  }
   if ((nct <= kTPDirectMax || tp_list) && !tp_super)
     hipLaunchKernelGGL(k_tilepairs_direct, dim3((unsigned)nrt), dim3(kTPDirectThreads), 0, c->stream, nrt, nct,
                        (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
                        icap, dcnt, (unsigned long long *)c->workq.p, build, halo ? halo_present(c) : nullptr, a0,
                        a1, nozero ? (const TileBox *)c->gbox_c.p : (const TileBox *)nullptr,
                        tp_list ? (const int *)c->h_hl.p : (const int *)nullptr, (int)c->halo_hl,
-                       tp_list ? halo_list_count(c) : (const unsigned *)nullptr);
+                       tp_list ? halo_list_count(c) : (const unsigned *)nullptr, tp);
   else
     hipLaunchKernelGGL(k_tilepairs, dim3((unsigned)((nrt + kSuper - 1) / kSuper)), dim3(kTPThreads), 0, c->stream,
                        nrt, nct, (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune,
@@ -2416,13 +2516,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, TprArgs{});
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, tp);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count of the

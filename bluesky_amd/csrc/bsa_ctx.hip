@@ -472,6 +472,33 @@ int bsa_set_candidate_reuse(bsa_ctx *c, int on, double sigma_h, double sigma_v) 
   return 0;
 }
 
+int bsa_set_tile_reuse(bsa_ctx *c, int on, double sigma_h, double sigma_v) {
+  if (!c) return -1;
+  if (on && !(sigma_h > 0.0 && sigma_h < 1e5 && sigma_v > 0.0 && sigma_v < 1e4))
+    return bsa::fail(c, "tile reuse budgets must be positive (sigma_h < 100 km, sigma_v < 10 km)");
+  c->tpr_on = on != 0;
+  if (on) {
+    c->tpr_dx = (float)(sigma_h / 6.3e6);       // chord units (a unit-vector axis moves <= its chord)
+    c->tpr_ds = (float)(sigma_h / 6.3e6 / 20);  // reach: |V| T/2 changes with the speed, slowly
+    c->tpr_dv = (float)sigma_v;
+  }
+  c->tpr_valid = false;  // the next detect builds
+  return 0;
+}
+
+int bsa_tile_reuse_stats(bsa_ctx *c, int64_t *out2) {
+  if (!c || !out2) return -1;
+  unsigned long long w[8] = {0};
+  if (c->tpr_ctl.p) {
+    BSA_HIP(c, hipSetDevice(c->device));
+    BSA_HIP(c, hipMemcpyAsync(w, c->tpr_ctl.p, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+    BSA_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  out2[0] = (int64_t)w[3];
+  out2[1] = (int64_t)w[4];
+  return 0;
+}
+
 int bsa_reuse_stats(bsa_ctx *c, int64_t *builds, int64_t *detects) {
   if (!c || !builds || !detects) return -1;
   unsigned long long st[8] = {0};

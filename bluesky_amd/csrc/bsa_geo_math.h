@@ -18,17 +18,18 @@ __device__ __forceinline__ double np_min(double a, double b) {
 }
 
 // fmod(a, 360) without the library's loop, exactly fmod's value: for
-// 360 <= |a| < 360 2^30, q = trunc(|a| / 360) is the true quotient or one
-// off (the division's error is < 2^-23 of one), q 360 is exact (9 significant
-// bits times < 2^30) and |a| - q 360 is exact by Sterbenz (q >= 1 and |a| in
-// [q 360 / 2, 2 q 360] for the true q and its neighbours that are tried), so
-// the remainder of the true quotient comes out exactly; fmod's sign is a's.
-// Anything else (huge, inf, NaN) goes to fmod.
+// 360 <= |a| < 360 2^30, q = trunc(|a| (1/360)) is the true quotient or one
+// off (the product's error is < 2^-22 of one: two roundings of 2^-53 relative
+// on a quotient below 2^30; no division needed), q 360 is exact (9
+// significant bits times < 2^30) and |a| - q 360 is exact by Sterbenz (|a| in
+// [q 360 / 2, 2 q 360] for the true q and its neighbours that are tried, q = 0
+// only for |a| < 720), so the remainder of the true quotient comes out
+// exactly; fmod's sign is a's.  Anything else (huge, inf, NaN) goes to fmod.
 __device__ __forceinline__ double fmod360(double a) {
   const double aa = fabs(a);
   if (aa < 360.0) return a;
   if (!(aa < 386547056640.0)) return fmod(a, 360.0);  // 360 * 2^30
-  double q = trunc(aa / 360.0);
+  double q = trunc(aa * (1.0 / 360.0));
   double r = aa - q * 360.0;
   if (r < 0.0) {
     q -= 1.0;

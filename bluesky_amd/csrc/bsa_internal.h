@@ -201,6 +201,19 @@ struct Ctx {
   void *reuse_candp = nullptr;
   DevBuf snap_build, snap_cur, reuse_ctl, reuse_use;  // ctl: [0] build flag, [1] detects since build
 
+  // tile-pair list reuse: K0d's item list, built on boxes
+  // inflated by (tpr_dx chord, tpr_ds reach, tpr_dv m), is kept while every
+  // aircraft's prefilter record stays within those distances of its record at
+  // the build (checked by whoever prepares the records: K4' / K0b); a record
+  // outside raises tpr_ctl[0] and the next detect rebuilds on the device
+  bool tpr_on = true;                  // resident home-order detects of all rows (BSA_TPR=0: off)
+  bool tpr_valid = false;              // a list + snapshot exist for tpr_key / tpr_n
+  double tpr_key[4] = {0, 0, 0, 0};    // rpz hpz tla mid of the list
+  int64_t tpr_n = -1;
+  float tpr_dx = 3.2e-4f, tpr_ds = 1.6e-5f, tpr_dv = 300.f;  // ~2 km, ~100 m of reach, 300 m
+  DevBuf tpr_snap;                     // PFRec per aircraft at the last build
+  DevBuf tpr_ctl;                      // u64: [0] build flag, [1] near items, [2] far items, [3] builds, [4] detects
+
   // detect timing: one set of 5 events per detect since the last reset
   std::vector<hipEvent_t> evpool;
   int ev_sets = 0, ev_last = 0;

@@ -30,7 +30,7 @@ static_assert(kGroup % kSub == 0 && (kSub & (kSub - 1)) == 0, "sub-groups tile a
 // s >= 0.5 (a reach beyond ~3000 km) or non-finite -> INF (never pruned
 // horizontally); the bound also caps the magnitudes in the fp32 test (kPlaneMargin).
 __device__ __forceinline__ float reach_h(double rpz, double gs, double tlap) {
-  const double s = ((0.5 * rpz + (fabs(gs) + 0.5e-3) * tlap) * (1.0 + 1e-5)) / 6.3e6 + 1e-6;
+  const double s = ((0.5 * rpz + (fabs(gs) + 0.5e-3) * tlap) * (1.0 + 1e-5)) * (1.0 / 6.3e6) + 1e-6;
   return (s < 0.5) ? (float)s : INFINITY;
 }
 // vertical half-bound [m]: kept iff |dalt| < h_i + h_j
@@ -38,6 +38,9 @@ __device__ __forceinline__ double reach_v(double hpz, double vs, double alt, dou
   return (0.5 * hpz + (fabs(vs) + 0.5e-6) * tlap) * (1.0 + 1e-5) + 0.5 + 1e-6 * fabs(alt);
 }
 
+// (Divisions by the constant radii are products with their reciprocals: one
+// more rounding, 2^-53 relative, inside the 1e-5 relative and 1e-6 chord
+// margins of every bound below; a quarter-rate fp64 division chain fewer each.)
 // Prefilter record from the fp64 unit vector, reach and altitude.
 // lo / hi = alt -/+ h rounded to fp32 (error
 // <= 1e-3 m at flight levels, inside h's 0.5 m + 1e-6 |alt| margin); a
@@ -87,15 +90,15 @@ __device__ __forceinline__ PFRec make_pf_mid(double px, double py, double pz, do
                                              double alt, double vs, double rpz, double hpz, double tlap) {
   const double ag = fabs(gs) + 0.5e-3;
   const double ht = 0.5 * tlap;
-  const double cmax = (rpz + (ag + kVcap + 0.5e-3) * tlap) * (1.0 + 1e-5) / 6.35e6;
+  const double cmax = (rpz + (ag + kVcap + 0.5e-3) * tlap) * (1.0 + 1e-5) * (1.0 / 6.35e6);
   const double rhop = cosl - cmax;
   double mx = px, my = py, mz = pz;
   float s = INFINITY;
   if (fabs(gs) <= kVcap && isfinite(u) && isfinite(v) && rhop >= 0.05 && cmax <= 0.1) {
     const double kb = 1.5707963267948966 + 2.5707963267948966 / rhop;
     const double sm = ((0.5 * rpz + ag * ht) * (1.0 + 1e-5) + 0.012 * (0.5 * rpz + ag * tlap) +
-                       ag * ht * kb * cmax) / 6.3e6 + 0.25 * cmax * cmax + 1e-6;
-    const double f = ht / 6371000.0;
+                       ag * ht * kb * cmax) * (1.0 / 6.3e6) + 0.25 * cmax * cmax + 1e-6;
+    const double f = ht * (1.0 / 6371000.0);
     mx = px + f * (-u * sinlo - v * sinl * coslo);
     my = py + f * (u * coslo - v * sinl * sinlo);
     mz = pz + f * (v * cosl);

@@ -52,6 +52,11 @@ struct PrepArgs {
   TileBox *sbox, *gbox;  // (the tile boxes follow from the group boxes in the detect's K0z)
   double rpz, hpz, tla;
   int mid, rec, n;
+  // tile-pair list reuse: the last build's records; a record
+  // outside its budgets raises tpr_ctl[0] (the next detect rebuilds), or NULL
+  const PFRec *snap;
+  unsigned long long *tpr_ctl;
+  float dx, ds, dv;
 };
 
 // one row of K4' (below).  The row's state is loaded before K3's part runs
@@ -170,9 +175,14 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
   const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
   if (PREP) {  // every lane reaches the wave's group reduction (its record from registers)
-    PFRec p{};
+    PFRec p{}, b{};
+    if (pa.snap && k < re) b = pa.snap[k];  // (issued with the row's other loads)
     if (k < re) p = pilot_kin_row<FUSE, PREP>(rb, k, simdt, winddim, vwn, vwe, wf, d, mv, mp, pa);
     group_boxes_v(pa.n, k / kGroup, p, pa.sbox, pa.gbox);
+    if (pa.snap) {
+      const bool out = k < re && !pf_within(p, b, pa.dx, pa.ds, pa.dv);
+      if (__ballot(out) && (threadIdx.x & 63) == 0) pa.tpr_ctl[0] = 1ull;
+    }
     return;
   }
   if (k >= re) return;
@@ -329,7 +339,7 @@ void sim_release(Ctx *c) {
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
                    &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env,
                    &c->s_ptab, &c->s_ptype, &c->s_phase, &c->s_noreso, &c->s_resooff, &c->s_dropped, &c->s_atm,
-                   &c->xfer_stage, &c->lbyidx, &c->fetch_stage};
+                   &c->xfer_stage, &c->lbyidx, &c->fetch_stage, &c->tpr_snap, &c->tpr_ctl};
   for (auto *b : all) release(*b);
   bk_release(c);
   halo_release(c);
@@ -752,6 +762,13 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
         pa.tla = c->simp.tla;
         pa.mid = bsa::stage1_mid(0, false, 0);
         pa.n = (int)n;
+        if (c->tpr_valid && c->tpr_snap.p && c->tpr_ctl.p && c->tpr_n == n) {  // the kept list's budgets
+          pa.snap = (const bsa::PFRec *)c->tpr_snap.p;
+          pa.tpr_ctl = (unsigned long long *)c->tpr_ctl.p;
+          pa.dx = c->tpr_dx;
+          pa.ds = c->tpr_ds;
+          pa.dv = c->tpr_dv;
+        }
       }
       const int blk = k4b;  // (PREP: whole waves = whole groups, rb = 0)
       const int64_t nb = std::max<int64_t>(1, (re - rb + blk - 1) / blk);

@@ -147,6 +147,19 @@ int bsa_reuse_stats(bsa_ctx *ctx, int64_t *builds, int64_t *detects);
 /* Largest fraction of its horizontal [0] / vertical [1] budget any aircraft
  * had used at the last detect (> 1 triggered a build; 0 after a forced one). */
 int bsa_reuse_budget_use(bsa_ctx *ctx, double *use2);
+/* Tile-pair list reuse in the resident sim step (on by
+ * default): the detect's coarse cull -- which (512-row tile, 512-column tile,
+ * 64-row slice) items the prefilter sweeps (K0d) -- is built on boxes grown by
+ * sigma_h [m] horizontally (and proportionally in reach) and sigma_v [m]
+ * vertically, and kept while every aircraft's prefilter record stays within
+ * those distances of its record at the build (K4' checks each record it
+ * prepares; the first one outside makes the next detect rebuild on the
+ * device).  Every pair is still tested and evaluated at every detect, so the
+ * results are identical with it on or off.  off: every detect builds. */
+int bsa_set_tile_reuse(bsa_ctx *ctx, int on, double sigma_h, double sigma_v);
+/* [0] tile-pair list builds, [1] detects that used the kept or a fresh list,
+ * since the sim's first such detect (device counters). */
+int bsa_tile_reuse_stats(bsa_ctx *ctx, int64_t *out2);
 
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
  * bounding-box cull, the total number of tile pairs, and the number of

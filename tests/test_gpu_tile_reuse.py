@@ -1,0 +1,72 @@
+"""Tile-pair list reuse of the resident step: K0d's item
+list is built on boxes grown by the drift budgets and kept while every
+aircraft's prefilter record stays inside them (K4' checks; the first record
+outside makes the next detect rebuild on the device).  It only changes which
+detects rebuild the coarse cull -- every pair is still tested and evaluated --
+so the sim with it is BITWISE the sim without it: state arrays and pair lists
+after every step, with MVP manoeuvres, large steps that force rebuilds, budgets
+tiny enough to rebuild every step, and cd_every > 1."""
+import numpy as np
+import pytest
+
+from bluesky_amd import _lib, resident, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def run(ctx, init, p, steps, tile):
+    if tile is None:
+        ctx.set_tile_reuse(False)
+    else:
+        ctx.set_tile_reuse(True, *tile)
+    try:
+        sim = resident.ResidentSim(init, p, ctx=ctx)
+        out = []
+        for _ in range(steps):
+            sim.step(1)
+            st = sim.stats()
+            out.append((sim.read(), ctx.fetch_pairs(st['n_conf'], st['n_los'])))
+        return out, ctx.tile_reuse_stats()
+    finally:
+        ctx.set_tile_reuse(True)
+
+
+def same(a, b):
+    for k, (sa, pa) in enumerate(a):
+        sb, pb = b[k]
+        for f in sa:
+            assert np.array_equal(sa[f], sb[f]), 'step %d %s' % (k, f)
+        for f in ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'li', 'lj', 'inconf', 'tcpamax'):
+            assert np.array_equal(pa[f], pb[f]), 'step %d %s' % (k, f)
+
+
+@pytest.mark.parametrize('simdt, tile, cd_every', [
+    (0.05, (2016.0, 300.0), 1),     # the bench's cadence and default budgets: few builds
+    (1.0, (2016.0, 300.0), 1),      # 250 m per step: rebuilds every few steps
+    (1.0, (1.0, 1.0), 1),           # budgets below one step's drift: a rebuild at every detect
+    (0.5, (2016.0, 300.0), 3),      # K4' prepares (and checks) only before CD steps
+])
+def test_tile_reuse_is_bitwise_the_full_cull(ctx, simdt, tile, cd_every):
+    t = synth.box(20000, 300.0, seed=101)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=simdt, cd_every=cd_every, swresohoriz=False)   # horizontal + vertical MVP
+    exp, _ = run(ctx, init, p, 24, None)
+    got, st = run(ctx, init, p, 24, tile)
+    same(got, exp)
+    assert sum(len(x[1]['ci']) for x in exp) > 0
+    assert st['builds'] >= 1
+
+
+def test_tile_reuse_builds_rarely_at_the_bench_cadence(ctx):
+    """At simdt 0.05 s the list survives many detects (the point of keeping
+    it), and a budget below one step's drift rebuilds every time."""
+    t = synth.box(20000, 300.0, seed=103)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=0.05)
+    _, a0 = run(ctx, init, p, 0, (2016.0, 300.0))
+    _, a = run(ctx, init, p, 30, (2016.0, 300.0))
+    builds, detects = a['builds'] - a0['builds'], a['detects'] - a0['detects']
+    assert detects == 29 and 1 <= builds <= 8, a        # (the first detect is K0b's: no list)
+    _, b0 = run(ctx, init, resident.params(simdt=1.0), 0, (1.0, 1.0))
+    _, b = run(ctx, init, resident.params(simdt=1.0), 10, (1.0, 1.0))
+    assert b['builds'] - b0['builds'] == b['detects'] - b0['detects'] == 9, b

@@ -125,3 +125,28 @@ def test_geo_operand_forms_and_result_types():
         geo.qdrdist_matrix(np.asmatrix(a), a, a, a, ctx=ctx)
     with pytest.raises(ValueError):
         geo.qdrdist_matrix(np.ones((2, 3)), np.ones((2, 3)), np.ones((2, 3)), np.ones((2, 3)), ctx=ctx)
+
+
+def test_fmod360_reciprocal_quotient_is_exact():
+    """bsa_geo_math.h fmod360: q = trunc(|a| * (1/360)), then one neighbour
+    tried, gives fmod(a, 360) bitwise (the device function's arithmetic,
+    restated in numpy fp64: every operation is IEEE, no contraction) on 2e6
+    values: random magnitudes up to 360 * 2^30, the multiples of 360 and their
+    ulp neighbours, the range bounds."""
+    rng = np.random.default_rng(3)
+    a = np.concatenate([rng.uniform(-1, 1, 10 ** 6) * 10 ** rng.uniform(2.5, 11.5, 10 ** 6),
+                        rng.uniform(-720, 720, 10 ** 5)])
+    k = rng.integers(1, 2 ** 30, 3 * 10 ** 5).astype(np.float64) * 360.0
+    a = np.concatenate([a, k, np.nextafter(k, 0), np.nextafter(k, np.inf), -k, [360.0, 720.0, 359.99999999999994,
+                                                                                 360 * 2.0 ** 30 - 1]])
+    aa = np.abs(a)
+    m = (aa >= 360.0) & (aa < 386547056640.0)
+    aa = aa[m]
+    q = np.trunc(aa * (1.0 / 360.0))
+    r = aa - q * 360.0
+    lo, hi = r < 0.0, r >= 360.0
+    q = np.where(lo, q - 1.0, np.where(hi, q + 1.0, q))
+    r = aa - q * 360.0
+    got = np.copysign(r, a[m])
+    exp = np.fmod(a[m], 360.0)
+    assert np.array_equal(got.view(np.uint64), exp.view(np.uint64))

@@ -3,7 +3,7 @@ set -u
 OUT=gpurun_out/r4d
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_asas_dropin.py tests/test_gpu_sim.py tests/test_gpu_trace.py tests/test_gpu_multirank.py tests/test_gpu_detect.py tests/test_gpu_mvp_kin.py tests/test_gpu_feed.py tests/test_gpu_reuse.py -m "gpu" -k "not 8ranks and not key_blocks" -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fullsize.py::test_box100k_every_row_vs_oracle_fixture tests/test_gpu_fullsize.py::test_noprune_row_sweep_100k_bitwise tests/test_stage1_bound.py tests/test_gpu_asas_dropin.py tests/test_gpu_sim.py tests/test_gpu_trace.py tests/test_gpu_multirank.py tests/test_gpu_detect.py tests/test_gpu_mvp_kin.py tests/test_gpu_feed.py tests/test_gpu_reuse.py -m "gpu" -k "not 8ranks and not key_blocks" -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || exit $rc
 for G in 0 600 1200 0 600 1200; do
