@@ -190,6 +190,16 @@ constexpr int kWorkStride = 16;  // u64 words between counters (128 B apart)
 constexpr int kRankRows = BSA_RANK_ROWS;
 static_assert(kRankRows % 64 == 0 && kRankRows <= 1024, "whole waves per K2 block");
 constexpr int kRankLds = 3 * kRankRows;  // pairs per block folded from LDS (512 rows: 67 KB, 2 blocks per CU)
+// lanes per workgroup of k_rank_rows: its rows take one lane each, its pairs
+// (~1.7 per row at the 100k box) one lane each.  Two lanes per row place a
+// block's pairs in one pass instead of two, but the 1024-lane workgroup caps
+// the kernel at 128 VGPRs (7 spilled): K2 27.7 -> 29.0 us at the 100k box
+// (A/B on one box, round 4), so one
+#ifndef BSA_RANK_LANES_PER_ROW
+#define BSA_RANK_LANES_PER_ROW 1
+#endif
+constexpr int kRankThreads = BSA_RANK_LANES_PER_ROW * kRankRows;
+static_assert(kRankThreads <= 1024, "K2 workgroup size");
 __host__ __device__ __forceinline__ int rank_blocks(int nrows) { return (nrows + kRankRows - 1) / kRankRows; }
 __host__ __device__ __forceinline__ int rowcnt_words(int nrows) { return 2 * (nrows + 1) + 2 * rank_blocks(nrows); }
 
@@ -1797,7 +1807,7 @@ __global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__
   }
 }
 
-__global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
+__global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
                                                          unsigned *__restrict__ rowoff,
                                                          unsigned *__restrict__ rowcnt,
                                                          const uint2 *__restrict__ kb, int B,
@@ -1811,7 +1821,7 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
                                                          unsigned long long *__restrict__ tcpamax_bits,
                                                          Counters *__restrict__ cnext,
                                                          unsigned long long *__restrict__ wnext) {
-  constexpr int W = kRankRows / 64;
+  constexpr int W = kRankThreads / 64;
   __shared__ unsigned red[4][W];
   __shared__ unsigned soff[2][kRankRows + 1];  // the block's rows' exclusive offsets (conf, LoS), + total
   // the block's MVP pair vectors for the fold (when they fit; else through pdv / pfl)
@@ -1820,7 +1830,8 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
   __shared__ double stc[kRankLds];  // ... and their tcpa (tcpamax)
   const int nb = rank_blocks(nrows), b = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
   const unsigned *bcnt = rowcnt + 2 * (nrows + 1);
-  const int r = b * kRankRows + t;
+  const bool rowlane = t < kRankRows;  // lanes past the block's rows only place pairs
+  const int r = rowlane ? b * kRankRows + t : nrows;
   const unsigned c = r < nrows ? rowcnt[r] : 0u, l = r < nrows ? rowcnt[nrows + 1 + r] : 0u;
   // the next detect's per-row counts and counters start at zero (its K0z
   // launch is skipped, detect_enqueue): this block's counts are read, the
@@ -1831,13 +1842,13 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
   }
   if (b == 0) {
     constexpr int kWords = (int)(sizeof(Counters) / 8);
-    for (int k = t; k < kWords; k += kRankRows) reinterpret_cast<unsigned long long *>(cnext)[k] = 0ull;
-    for (int k = t; k < kWorkShards * kWorkStride; k += kRankRows) wnext[k] = 0ull;
+    for (int k = t; k < kWords; k += kRankThreads) reinterpret_cast<unsigned long long *>(cnext)[k] = 0ull;
+    for (int k = t; k < kWorkShards * kWorkStride; k += kRankThreads) wnext[k] = 0ull;
   }
   const bool ovf = cand_overflow(cnt, cap);
   // P / L = all conflict / LoS pairs, cb / lb = those of the blocks before b
   unsigned P = 0, L = 0, cb = 0, lb = 0;
-  for (int q = t; q < nb; q += kRankRows) {
+  for (int q = t; q < nb; q += kRankThreads) {
     const unsigned x = bcnt[q], y = bcnt[nb + q];
     P += x;
     L += y;
@@ -1900,8 +1911,10 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
   }
   if (ovf) return;
   const unsigned ec = wc + xc - c, el = wl + xl - l;  // exclusive, within the block
-  soff[0][t] = ec;
-  soff[1][t] = el;
+  if (rowlane) {
+    soff[0][t] = ec;
+    soff[1][t] = el;
+  }
   if (t == 0) {
     soff[0][kRankRows] = tc;
     soff[1][kRankRows] = tl;
@@ -1917,7 +1930,7 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
   __syncthreads();
   const bool lds = tc <= (unsigned)kRankLds;  // the block's conflict pairs fit the LDS arrays
   const bool lds_fold = mf.rowdv && lds;
-  for (unsigned x = t; x < tc + tl; x += kRankRows) {
+  for (unsigned x = t; x < tc + tl; x += kRankThreads) {
     const bool conf = x < tc;
     const unsigned q = conf ? x : x - tc;
     const unsigned *so = soff[conf ? 0 : 1];
@@ -1991,7 +2004,7 @@ __global__ __launch_bounds__(kRankRows) void k_rank_rows(int nrows, Counters *__
   // atomics on the bit patterns made it -- and K3's fold of the row's pairs,
   // in order (MVP.py:44-61), from LDS or from pdv / pfl
   __syncthreads();
-  if (r >= nrows) return;
+  if (!rowlane || r >= nrows) return;
   inconf[r] = c ? 1 : 0;
   unsigned long long tm = 0ull;
   for (unsigned k = 0; k < c; ++k) {
@@ -2581,7 +2594,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (B) {
     hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows)), dim3(64), 0, c->stream, (int)nrows,
                        (unsigned *)c->rowcnt.p);
-    hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)rank_blocks((int)nrows)), dim3(kRankRows), 0, c->stream,
+    hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)rank_blocks((int)nrows)), dim3(kRankThreads), 0, c->stream,
                        (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
                        (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb, (int *)c->out_ci.p,
                        (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
