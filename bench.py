@@ -184,16 +184,25 @@ def global1m_line(ctx, rank, world, warmup=2, steps=5):
                 candidates_rank0=ts['candidates'] / max(ts['detects'], 1))
 
 
-def halo_line(ctx, sim):
-    """Bytes each rank exchanged per CD call (max over ranks; collective)."""
+def halo_line(ctx, sim, cd_steps=None):
+    """Bytes each rank exchanged per CD call (max over ranks; collective), and
+    the stream-ordered collectives of the timed region per CD step (calls and
+    payload bytes, max over ranks: bsa_sim_comm_stats)."""
     h = sim.halo_stats()
-    mx = ctx.allreduce_max([h['rx_bytes'], h['tx_bytes'], h['tiles'], h['regrowths']])
+    cs = ctx.sim_comm_stats()
+    mx = ctx.allreduce_max([h['rx_bytes'], h['tx_bytes'], h['tiles'], h['regrowths'], cs['calls'],
+                            cs['tx_bytes'], cs['rx_bytes']])
     tot = ctx.allreduce_sum([h['rx_bytes']])
-    return dict(rx_bytes_per_cd_max_rank=int(mx[0]), tx_bytes_per_cd_max_rank=int(mx[1]),
-                rx_bytes_per_cd_all_ranks=int(tot[0]), tiles_received_max_rank=int(mx[2]),
-                regrowths=int(mx[3]),
-                note='halo exchange (grouped RCCL send/recv of the column tiles a rank\'s rows can reach) '
-                     'instead of the full-state all-gather; 512 aircraft x 6 or 8 fp64 per tile')
+    out = dict(rx_bytes_per_cd_max_rank=int(mx[0]), tx_bytes_per_cd_max_rank=int(mx[1]),
+               rx_bytes_per_cd_all_ranks=int(tot[0]), tiles_received_max_rank=int(mx[2]),
+               regrowths=int(mx[3]),
+               note='halo exchange (grouped RCCL send/recv of the column tiles a rank\'s rows can reach) '
+                    'instead of the full-state all-gather; 512 aircraft x 6 or 8 fp64 per tile')
+    if cd_steps:
+        out['collectives_per_cd_step'] = dict(
+            calls=mx[4] / cd_steps, tx_bytes_max_rank=mx[5] / cd_steps, rx_bytes_max_rank=mx[6] / cd_steps,
+            note='box all-gather + grouped halo send/recv + 16-B gate all-reduce per CD step (RCCL over xGMI)')
+    return out
 
 
 def timed_steps(ctx, sim, warmup, steps):
@@ -371,7 +380,7 @@ def main():
                propagation=propagation, exact_fp64=exact_fp64,
                build=dict(lib_path=os.path.relpath(lib_path, REPO), lib_sha256=lib_sha))
     if world > 1:   # the halo exchange that replaced the full-state all-gather
-        out['halo'] = halo_line(ctx, sim)
+        out['halo'] = halo_line(ctx, sim, cd_steps)
     if world > 1:   # C2: the last CD call's pair lists of all ranks to rank 0's host
         g0 = time.perf_counter()
         gp = sim.gather_pairs(root=0)

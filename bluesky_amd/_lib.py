@@ -189,6 +189,7 @@ SIGNATURES.update({
     'bsa_sim_read_asas': (ctypes.c_int, [_vp, ctypes.POINTER(AsasOut)]),
     'bsa_sim_halo_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_set_halo_cap': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64]),
+    'bsa_sim_comm_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_set_atmos': (ctypes.c_int, [_vp, ctypes.c_int]),
     'bsa_sim_read_atmos': (ctypes.c_int, [_vp, _c_dp, _c_dp, _c_dp]),
 })
@@ -727,6 +728,12 @@ class Context:
         v = np.zeros(4, np.int64)
         self.check(self.lib.bsa_sim_halo_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_halo_stats')
         return dict(rx_bytes=int(v[0]), tx_bytes=int(v[1]), tiles=int(v[2]), regrowths=int(v[3]))
+
+    def sim_comm_stats(self):
+        """bsa_sim_comm_stats: collectives since the last timing_reset (calls, bytes sent / received)."""
+        v = np.zeros(3, np.int64)
+        self.check(self.lib.bsa_sim_comm_stats(self.h, ptr(v, _c_i64p)), 'bsa_sim_comm_stats')
+        return dict(calls=int(v[0]), tx_bytes=int(v[1]), rx_bytes=int(v[2]))
 
     def sim_set_halo_cap(self, sender, receiver, tiles):
         """bsa_sim_set_halo_cap (testing aid): this rank's copy of one tile capacity."""

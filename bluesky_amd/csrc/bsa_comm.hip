@@ -121,11 +121,18 @@ __global__ void k_max_u64_slots(unsigned long long *out, int count, int nq, Slot
 
 bool comm_multi(const Ctx *c) { return c->nranks > 1 && (c->comm || c->group); }
 
+static void account(Ctx *c, size_t tx, size_t rx) {
+  c->comm_calls++;
+  c->comm_tx += (int64_t)tx;
+  c->comm_rx += (int64_t)rx;
+}
+
 int comm_allgather(Ctx *c, const void *send, void *recv, size_t bytes) {
   if (!comm_multi(c)) {
     if (bytes && recv != send) BSA_HIP(c, hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, c->stream));
     return 0;
   }
+  account(c, bytes, bytes * (size_t)(c->nranks - 1));
   if (c->comm) {
     BSA_NCCL(c, ncclAllGather(send, recv, bytes, ncclUint8, (ncclComm_t)c->comm, c->stream));
     return 0;
@@ -145,6 +152,7 @@ int comm_allgather(Ctx *c, const void *send, void *recv, size_t bytes) {
 // unpacked).  RCCL: nf in-place ncclAllGather fused in one group.
 int comm_allgather_inplace(Ctx *c, double *const *f, int nf, size_t rpr) {
   if (!comm_multi(c) || rpr == 0 || nf <= 0) return 0;
+  account(c, rpr * 8 * nf, rpr * 8 * nf * (size_t)(c->nranks - 1));
   if (c->comm) {
     BSA_NCCL(c, ncclGroupStart());
     for (int k = 0; k < nf; ++k)
@@ -173,6 +181,7 @@ int comm_allgather_inplace(Ctx *c, double *const *f, int nf, size_t rpr) {
 int comm_allreduce_max_u64(Ctx *c, unsigned long long *buf, int count) {
   if (!comm_multi(c) || count <= 0) return 0;
   if (count > 256) return fail(c, "device max all-reduce of %d words", count);
+  account(c, (size_t)count * 8, (size_t)count * 8);
   if (c->comm) {
     BSA_NCCL(c, ncclAllReduce(buf, buf, (size_t)count, ncclUint64, ncclMax, (ncclComm_t)c->comm, c->stream));
     return 0;
@@ -261,6 +270,15 @@ int comm_halo(Ctx *c, const void *send, const size_t *soff, const size_t *slen, 
               const size_t *roff, const size_t *rlen, const size_t *peer) {
   if (!comm_multi(c)) return 0;
   const int R = c->nranks, me = c->rank;
+  {
+    size_t tx = 0, rx = 0;
+    for (int q = 0; q < R; ++q)
+      if (q != me) {
+        tx += slen[q];
+        rx += rlen[q];
+      }
+    account(c, tx, rx);
+  }
   if (c->comm) {
     bool any = false;
     for (int q = 0; q < R; ++q) any = any || (q != me && (slen[q] || rlen[q]));

@@ -472,6 +472,14 @@ int bsa_set_candidate_reuse(bsa_ctx *c, int on, double sigma_h, double sigma_v) 
   return 0;
 }
 
+int bsa_sim_comm_stats(bsa_ctx *c, int64_t *out3) {
+  if (!c || !out3) return -1;
+  out3[0] = c->comm_calls;
+  out3[1] = c->comm_tx;
+  out3[2] = c->comm_rx;
+  return 0;
+}
+
 int bsa_set_tile_reuse(bsa_ctx *c, int on, double sigma_h, double sigma_v) {
   if (!c) return -1;
   if (on && !(sigma_h > 0.0 && sigma_h < 1e5 && sigma_v > 0.0 && sigma_v < 1e4))
@@ -564,6 +572,7 @@ int bsa_timing_reset(bsa_ctx *c) {
   c->ev_sets = 0;
   c->ev_count = 0;
   c->ev_valid = false;
+  c->comm_calls = c->comm_tx = c->comm_rx = 0;
   if (!bsa::ensure(c, c->stats, 8 * 8, "detect statistics")) return -1;
   BSA_HIP(c, hipMemsetAsync(c->stats.p, 0, 8 * 8, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));

@@ -235,6 +235,10 @@ struct Ctx {
   struct Group *group = nullptr;
   int nranks = 1, rank = 0;
   DevBuf red;  // small reduction scratch
+  // stream-ordered collectives this rank issued since the last bsa_timing_reset
+  // (bsa_sim_comm_stats): calls and the bytes it sends / receives (payload,
+  // as RCCL would move them; the in-process group's staging copies aside)
+  int64_t comm_calls = 0, comm_tx = 0, comm_rx = 0;
   DevBuf pg_send, pg_recv;  // C2 pair gather staging (bsa_gather_pairs)
 
   // GPU-resident sim (bsa_sim.hip).  Its state lives in HOME order: home

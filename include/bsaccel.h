@@ -473,6 +473,12 @@ int bsa_sim_detect_rows(bsa_ctx *ctx, int64_t row_begin, int64_t row_end, int64_
  * bsa_sim_detect_rows, the tiles that rank share needs from other ranks --
  * and [3] capacity regrowths (aborted and re-run steps) since bsa_sim_init. */
 int bsa_sim_halo_stats(bsa_ctx *ctx, int64_t *out4);
+/* Stream-ordered collectives (RCCL or the in-process group) this rank issued
+ * since the last bsa_timing_reset: [0] calls, [1] payload bytes it sent,
+ * [2] payload bytes it received (as RCCL moves them).  Per CD step of the
+ * sharded sim: the box all-gather, the halo send / recv, the 16-B gate
+ * all-reduce (+ the pair-key all-gather with resume_nav). */
+int bsa_sim_comm_stats(bsa_ctx *ctx, int64_t *out3);
 /* Testing aid: override this rank's copy of the tile capacity sender ->
  * receiver (the capacities must agree on all ranks, and RCCL's grouped send /
  * recv needs every send length to match its receive; the in-process group
