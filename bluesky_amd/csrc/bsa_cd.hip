@@ -245,6 +245,15 @@ struct FusedBoxes {
   int blk_base;
 };
 
+// Plan reuse (several ranks / the probe): the own-tile K0b
+// compares each record it writes with the last build's and raises the rank's
+// rebuild flag on the first one outside the budgets (snap == NULL: off)
+struct TprCheck {
+  const PFRec *snap;
+  unsigned *flag;
+  float dx, ds, dv;
+};
+
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
 // Workgroup = kTile lanes (one tile of sorted records).  rec = 0 (the
 // resident sim's home order): the fp64 records are not stored -- K1b builds
@@ -260,7 +269,7 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
                                                      PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
                                                      ReuseParams rz, FusedBoxes fb, ZeroArgs zs, int tile_base,
                                                      const int *__restrict__ tile_list, HaloUnpack hu,
-                                                     Counters *__restrict__ hcnt) {
+                                                     Counters *__restrict__ hcnt, TprCheck tck) {
   __shared__ TileBox fgb[kTile / 64];
   // K0z (fused): nothing here reads that state
   if (zs.cnt) zero_state(zs, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
@@ -273,7 +282,8 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
   const int k = tile * kTile + (int)threadIdx.x;
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
-  PFRec pk{};              // this lane's record (the fused boxes take it from registers)
+  PFRec pk{}, pb{};        // this lane's record (the fused boxes take it from registers), its build's
+  if (tck.snap && k < cnt) pb = tck.snap[k];
   if (k < cnt) {
     const int o = presorted ? k : (int)perm[k];
     const double tlap = tla > 0.0 ? tla : 0.0;
@@ -352,6 +362,10 @@ __global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__
       rz.use[2 * wv] = use_h;
       rz.use[2 * wv + 1] = use_v;
     }
+  }
+  if (tck.snap) {  // plan reuse: one flag store per wave whose records left their budgets
+    const bool out = k < cnt && !pf_within(pk, pb, tck.dx, tck.ds, tck.dv);
+    if (__ballot(out) && (threadIdx.x & 63) == 0) *tck.flag = 1u;
   }
   // K0c (fused): this thread wrote PC[k] above, every thread reaches the barrier
   if (fb.gbox) tile_boxes_v(cnt, tile, pk, fgb, fb.sbox, fb.gbox, fb.tbox);
@@ -2149,7 +2163,7 @@ int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla) {
   hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)nct), dim3(kTile), 0, c->stream, (int)n,
                      (const unsigned *)c->h2id.p, 1, 0, own, own, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, stage1_mid(0, false, 0),
-                     ReuseParams{}, fb, zs, 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr);
+                     ReuseParams{}, fb, zs, 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, TprCheck{});
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -2267,6 +2281,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       if (halo_pre(c, rb, re, &hp)) return -1;
       for (int r = 0; r < 3; ++r)
         if (hp.zn[r]) BSA_HIP(c, hipMemsetAsync(hp.z[r], 0, (size_t)hp.zn[r] * 4, c->stream));
+      // (its plan-reuse flag stays clear: it holds no records that could drift)
+      if (unsigned *f = halo_flag_word(c)) BSA_HIP(c, hipMemsetAsync(f, 0, 4, c->stream));
       if (halo_mid(c, rb, re, &hu)) return -1;
     }
     if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
@@ -2394,12 +2410,53 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
       !ensure(c, c->tilepairs, (size_t)ntp * kSlicesPerTile * sizeof(uint2), "prefilter items"))
     return -1;
+  // halo mode: K0d sweeps the present column tiles only (own + received, the
+  // flat halo list; BSA_TP_HALO_ALL=1 sweeps all tiles for A/B)
+  static const bool tp_all = getenv("BSA_TP_HALO_ALL") && atoi(getenv("BSA_TP_HALO_ALL")) == 1;
+  const bool tp_list = halo && !tp_all && !tp_super;
+  // tile-pair list reuse: the resident step's detects of a
+  // rank's rows -- one rank: records prepared (and checked) by K4'; several
+  // ranks or the probe: the halo plan is kept with the list, checked by the
+  // own-tile K0b and decided from flags gathered with the boxes.  Any other
+  // detect of this context invalidates the kept list.
+  static const bool tpr_env = !(getenv("BSA_TPR") && atoi(getenv("BSA_TPR")) == 0);
+  TprArgs tp{};
+  HaloTpr ht{};
+  const bool tpr = tpr_env && c->tpr_on && home && !reuse && flags == 0 && !tp_super &&
+                   ((!halo && prepped && nct <= kTPDirectMax) || tp_list);
+  if (tpr) {
+    if (!ensure(c, c->tpr_snap, (size_t)n * sizeof(PFRec), "tile-pair list snapshot")) return -1;
+    const bool fresh = !c->tpr_ctl.p;
+    if (!ensure(c, c->tpr_ctl, 64, "tile-pair list control")) return -1;
+    if (fresh) BSA_HIP(c, hipMemsetAsync(c->tpr_ctl.p, 0, 64, c->stream));
+    static const double sh_env = getenv("BSA_TPR_SH") ? atof(getenv("BSA_TPR_SH")) : 0.0;  // (A/B) [m]
+    if (sh_env > 0.0) {
+      c->tpr_dx = (float)(sh_env / 6.3e6);
+      c->tpr_ds = (float)(sh_env / 6.3e6 / 20);
+    }
+    const double key[6] = {rpz, hpz, tla, (double)mid, (double)rb, (double)re};
+    const bool valid = c->tpr_valid && c->tpr_n == n && memcmp(key, c->tpr_key, sizeof key) == 0;
+    ht = HaloTpr{halo ? 1 : 0, valid ? 0 : 1, c->tpr_dx, c->tpr_ds, c->tpr_dv, (unsigned long long *)c->tpr_ctl.p,
+                 nullptr};
+    c->tpr_valid = true;  // (an aborted step or any state change clears it)
+    memcpy(c->tpr_key, key, sizeof key);
+    c->tpr_n = n;
+  } else {
+    c->tpr_valid = false;
+  }
   FusedBoxes fb{nullptr, nullptr, nullptr, nullptr, 0};
   ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
   // halo mode: the plan's buffers are zeroed and the own tile boxes written
   // into the exchanged block by this K0b (no memset / copy launches)
   HaloPre hp{};
-  if (halo && halo_pre(c, rb, re, &hp)) return -1;
+  if (halo && halo_pre(c, rb, re, &hp, tpr ? &ht : nullptr)) return -1;
+  // plan reuse: the own K0b checks its records against the last build's and
+  // raises this rank's flag (not at a forced rebuild: it rebuilds anyway)
+  TprCheck tck{};
+  if (tpr && halo) {
+    ht.myflag = halo_flag_word(c);
+    if (!ht.force) tck = TprCheck{(const PFRec *)c->tpr_snap.p, ht.myflag, c->tpr_dx, c->tpr_ds, c->tpr_dv};
+  }
   if (!reuse) {
     fb = FusedBoxes{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, hp.blk, hp.blk_base};
     zs = ZeroArgs{(int)nrows, 1, 0, dcnt, (unsigned long long *)c->workq.p, (unsigned char *)c->inconf.p,
@@ -2413,11 +2470,11 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      c->stream, (int)n, perm_c, home ? 1 : 0, recs ? 1 : 0, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs,
-                     halo ? a0 : 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr);
+                     halo ? a0 : 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, tck);
   BSA_HIP(c, hipGetLastError());
   if (halo) {
     HaloUnpack hu{};
-    if (halo_mid(c, rb, re, &hu)) return -1;
+    if (halo_mid(c, rb, re, &hu, tpr ? &ht : nullptr)) return -1;
     if (c->halo_hl > 0) {  // the received tiles: unpacked (exchange), records and boxes (no zeroing here)
       const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
       FusedBoxes fb2 = fb;
@@ -2426,7 +2483,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)c->halo_hl), dim3(kTile), 0, c->stream, (int)n, perm_c, 1,
                          recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                          (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, 0,
-                         (const int *)c->h_hl.p, hu, dcnt);
+                         (const int *)c->h_hl.p, hu, dcnt, TprCheck{});
       BSA_HIP(c, hipGetLastError());
     }
   }
@@ -2445,36 +2502,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, build, dcnt);
   // ~1024 workgroups' worth of candidates per thread-chunk (one at 100k, several at 1M)
   const unsigned long long icap = (unsigned long long)ntp * kSlicesPerTile;  // items: 8 slices per tile pair
-  // halo mode: K0d sweeps the present column tiles only (own + received, the
-  // flat halo list; BSA_TP_HALO_ALL=1 sweeps all tiles for A/B)
-  static const bool tp_all = getenv("BSA_TP_HALO_ALL") && atoi(getenv("BSA_TP_HALO_ALL")) == 1;
-  const bool tp_list = halo && !tp_all && !tp_super;
-  // tile-pair list reuse: the resident step's detects of all
-  // rows whose records K4' prepared (and checked against the last build's);
-  // any other detect of this context invalidates the kept list
-  static const bool tpr_env = !(getenv("BSA_TPR") && atoi(getenv("BSA_TPR")) == 0);
-  TprArgs tp{};
-  const bool tpr = tpr_env && c->tpr_on && prepped && nct <= kTPDirectMax && !tp_super && !tp_list;
-  if (tpr) {
-    if (!ensure(c, c->tpr_snap, (size_t)n * sizeof(PFRec), "tile-pair list snapshot")) return -1;
-    const bool fresh = !c->tpr_ctl.p;
-    if (!ensure(c, c->tpr_ctl, 64, "tile-pair list control")) return -1;
-    if (fresh) BSA_HIP(c, hipMemsetAsync(c->tpr_ctl.p, 0, 64, c->stream));
-    const double key[4] = {rpz, hpz, tla, (double)mid};
-    const bool valid = c->tpr_valid && c->tpr_n == n && memcmp(key, c->tpr_key, sizeof key) == 0;
-    static const double sh_env = getenv("BSA_TPR_SH") ? atof(getenv("BSA_TPR_SH")) : 0.0;  // (A/B) [m]
-    if (sh_env > 0.0) {
-      c->tpr_dx = (float)(sh_env / 6.3e6);
-      c->tpr_ds = (float)(sh_env / 6.3e6 / 20);
-    }
-    tp = TprArgs{(unsigned long long *)c->tpr_ctl.p, valid ? 0 : 1, c->tpr_dx, c->tpr_ds, c->tpr_dv,
-                 (const PFRec *)c->pfcol.p, (PFRec *)c->tpr_snap.p};
-    c->tpr_valid = true;  // (an aborted step clears it: grow_after_abort)
-    memcpy(c->tpr_key, key, sizeof key);
-    c->tpr_n = n;
-  } else {
-    c->tpr_valid = false;
-  }
+  if (tpr)  // (after halo_mid, which may have forced the rebuild)
+    tp = TprArgs{(unsigned long long *)c->tpr_ctl.p, ht.force, c->tpr_dx, c->tpr_ds, c->tpr_dv,
+                 (const PFRec *)c->pfcol.p + roff, (PFRec *)c->tpr_snap.p + roff};
   if ((nct <= kTPDirectMax || tp_list) && !tp_super)
     hipLaunchKernelGGL(k_tilepairs_direct, dim3((unsigned)nrt), dim3(kTPDirectThreads), 0, c->stream, nrt, nct,
                        (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,

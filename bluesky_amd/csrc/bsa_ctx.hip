@@ -349,6 +349,7 @@ int bsa_set_state(bsa_ctx *c, int64_t n, const double *lat, const double *lon, c
   BSA_HIP(c, hipSetDevice(c->device));
   c->sim_ready = false;  // a new state replaces any resident sim
   c->sim_prepped = false;
+  c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
   c->home = false;       // ... and its home order: aircraft-index order again
   const double *src[6] = {lat, lon, trk, gs, alt, vs};
   if (n == 0) {

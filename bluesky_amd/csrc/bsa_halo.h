@@ -72,8 +72,24 @@ __device__ __forceinline__ int halo_unpack_tile(const HaloUnpack &u, int j, int 
   return got;
 }
 
+// Tile-pair list reuse across the halo plan: the plan,
+// its lists and K0d's list are rebuilt only when forced by the host or when
+// some rank flags it -- a record of its own rows outside its drift budget
+// (own K0b) or a resopairs request for a tile it does not hold (k_halo_req)
+// -- the flags travelling with the box all-gather, so every rank takes the
+// same decision (ctl[0]) from the same gathered words.  A rebuild plans on
+// grown boxes.  tpr = 0: every detect plans (round-3 behaviour).
+struct HaloTpr {
+  int tpr, force;
+  float dx, ds, dv;
+  unsigned long long *ctl;  // tile-pair list control (Ctx::tpr_ctl): [0] the decision, read by K0d
+  unsigned *myflag;         // this rank's flag word (in the box block; the probe: a control word)
+};
+
 // host side (bsa_halo.hip)
-int halo_pre(Ctx *c, int64_t rb, int64_t re, HaloPre *hp);  // buffers; no launches
-int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu);  // plan (+ exchange); hu->rbuf set in mode 1
+int halo_pre(Ctx *c, int64_t rb, int64_t re, HaloPre *hp, const HaloTpr *ht = nullptr);  // buffers; no launches
+int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu,
+             HaloTpr *ht = nullptr);  // plan (+ exchange); hu->rbuf set in mode 1 (may force ht)
+unsigned *halo_flag_word(Ctx *c);  // this rank's rebuild flag word (box block, or the probe's control word)
 
 }  // namespace bsa

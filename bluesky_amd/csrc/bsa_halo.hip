@@ -54,26 +54,36 @@ static inline size_t region_bytes(int cap, int nf) {
 }
 
 // requests: the tiles of this rank's resopairs' intruders outside its own tiles
+// (with plan reuse: a requested tile this rank does not hold -- present, the
+// kept plan's mask -- raises its rebuild flag, so the next plan delivers it)
 __global__ __launch_bounds__(256) void k_halo_req(int nrows, const unsigned *__restrict__ rptr,
                                                   const unsigned *__restrict__ rcol, const unsigned *__restrict__ id2h,
-                                                  int a0, int a1, unsigned *__restrict__ req) {
+                                                  int a0, int a1, unsigned *__restrict__ req,
+                                                  const uint8_t *__restrict__ present, unsigned *__restrict__ flag) {
   const unsigned total = rptr[nrows];
   for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < total; k += gridDim.x * blockDim.x) {
     const unsigned j = rcol[k];
     if (j == kDangling) continue;
     const int t = (int)(id2h[j] / (unsigned)kTile);
-    if (t < a0 || t >= a1) atomicOr(&req[t >> 5], 1u << (t & 31));
+    if (t < a0 || t >= a1) {
+      atomicOr(&req[t >> 5], 1u << (t & 31));
+      if (flag && !present[t]) *flag = 1u;
+    }
   }
 }
 
 struct PlanArgs {
   int nct, tpr, R, me, a0, a1;
   const TileBox *tbox;        // own tile boxes (probe: every tile's)
-  const unsigned char *gblk;  // gathered blocks [R][tpr boxes | request words], or NULL (probe)
+  const unsigned char *gblk;  // gathered blocks [R][tpr boxes | request words | flag word], or NULL (probe)
   size_t bb;                  // block bytes
   TileBox *tbox_out;          // exchange: the gathered boxes of other ranks' tiles -> tbox_c
   uint8_t *recv;              // [nct] tiles this rank needs (the present mask besides its own)
   uint8_t *send;              // [R][tpr] own tiles each rank needs (exchange), else NULL
+  int W;                      // request words per block
+  HaloTpr ht;                 // plan reuse (ht.tpr = 0: plan every detect)
+  unsigned *dem;              // demand words (zeroed here at a rebuild with reuse), 2 Rd + 1
+  int ndem;
 };
 
 __device__ __forceinline__ const TileBox &plan_box(const PlanArgs &a, int t) {
@@ -169,14 +179,35 @@ __device__ void halo_lists_q(const ListArgs &a, const HaloCaps &cp, int q) {
 // tiles.  (Ordering the lists in the last workgroup to finish, behind a
 // release fence per workgroup, took longer than the separate k_halo_lists
 // launch: 16.8 us against 4.5 + 4.4 at 1M, R = 8.)
+// plan reuse: every rank's flag word (gathered; the probe: its own) decides
+__device__ __forceinline__ bool plan_rebuild(const PlanArgs &a) {
+  if (!a.ht.tpr || a.ht.force) return true;
+  if (!a.gblk) return *a.ht.myflag != 0u;
+  bool any = false;
+  for (int q = 0; q < a.R; ++q)
+    any |= reinterpret_cast<const unsigned *>(a.gblk + (size_t)q * a.bb + (size_t)a.tpr * sizeof(TileBox))[a.W] != 0u;
+  return any;
+}
+
 __global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a, int ny) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int na = a.a1 - a.a0, y = blockIdx.y;
+  if (a.ht.tpr) {
+    const bool rb = plan_rebuild(a);
+    if (t == 0 && y == 0) {  // (every block reads the words first: the flag is cleared after this launch)
+      a.ht.ctl[0] = rb ? 1ull : 0ull;
+    }
+    if (!rb) return;
+    if (t == 0 && y == 0)
+      for (int k = 0; k < a.ndem; ++k) a.dem[k] = 0u;  // the lists kernel writes them next
+  }
+  // grown boxes when the plan is kept for later detects (symmetric: both sides grow alike)
+  auto gr = [&](const TileBox &b) { return a.ht.tpr ? box_grow(b, a.ht.dx, a.ht.ds, a.ht.dv) : b; };
   if (y < ny) {
     if (t < a.nct && !(t >= a.a0 && t < a.a1)) {
-      const TileBox b = plan_box(a, t);
+      const TileBox b = gr(plan_box(a, t));
       for (int i = y; i < na; i += ny)
-        if (boxes_may_interact(a.tbox[a.a0 + i], b)) {
+        if (boxes_may_interact(gr(a.tbox[a.a0 + i]), b)) {
           a.recv[t] = 1;
           if (a.send) a.send[(size_t)(t / a.tpr) * a.tpr + i] = 1;
         }
@@ -192,8 +223,20 @@ __global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a, int ny) {
   }
 }
 
-// block q: the lists of source / destination q (halo_lists_q)
-__global__ __launch_bounds__(256) void k_halo_lists(ListArgs a, HaloCaps cp) { halo_lists_q(a, cp, blockIdx.x); }
+// block q: the lists of source / destination q (halo_lists_q); with plan
+// reuse only at a rebuild (ctl[0], decided by k_halo_plan), when it also
+// keeps source q's part of the present mask for the detects until the next
+__global__ __launch_bounds__(256) void k_halo_lists(ListArgs a, HaloCaps cp, const unsigned long long *ctl,
+                                                    uint8_t *present, unsigned *myflag) {
+  if (ctl && ctl[0] == 0ull) return;
+  const int q = blockIdx.x;
+  if (myflag && q == 0 && threadIdx.x == 0) *myflag = 0u;  // (read by the plan launch before this one)
+  if (present) {
+    const int t0 = q * a.tpr, t1 = min(a.nct, t0 + a.tpr);
+    for (int t = t0 + (int)threadIdx.x; t < t1; t += blockDim.x) present[t] = a.recv[t];
+  }
+  halo_lists_q(a, cp, q);
+}
 
 // rows of the listed own tiles into the send regions: block (slot k, rank q)
 __global__ __launch_bounds__(kTile) void k_halo_pack(int n, int me, HaloFields fl, unsigned char *sbuf, HaloCaps cp) {
@@ -225,7 +268,11 @@ static size_t send_offsets(const Ctx *c, int s, int nf, unsigned long long *off)
   return at;
 }
 
-const uint8_t *halo_present(const Ctx *c) { return (const uint8_t *)c->h_plan.p; }
+// the tiles this rank holds besides its own: the last plan's (with plan
+// reuse the kept plan's, written by k_halo_lists at a rebuild)
+const uint8_t *halo_present(const Ctx *c) {
+  return c->h_present.p ? (const uint8_t *)c->h_present.p : (const uint8_t *)c->h_plan.p;
+}
 // the probe's dense halo list: its length on the device (the exchange's list
 // has per-source capacity regions, bounded by halo_hl on the host)
 const unsigned *halo_list_count(const Ctx *c) {
@@ -235,15 +282,20 @@ const unsigned *halo_list_count(const Ctx *c) {
 // the plan's buffers: recv [nct] + send [R][tpr] flags, demands ([R] send,
 // [R] receive, the total received).  hp: the own-tile
 // K0b zeroes them (the regions are recorded there); NULL: memsets here.
-static int plan_buffers(Ctx *c, int nct, int R, int tpr, int Rd, HaloPre *hp) {
+static int plan_buffers(Ctx *c, int nct, int R, int tpr, int Rd, HaloPre *hp, bool keep) {
   const size_t pbytes = (size_t)nct + (size_t)R * tpr, dwords = (size_t)(2 * Rd + 1);
   if (!ensure(c, c->h_plan, pbytes + 64, "halo plan") || !ensure(c, c->h_dem, dwords * 4, "halo demands"))
     return -1;
+  if (keep) {  // plan reuse: the kept present mask (k_halo_lists writes it at a rebuild)
+    if (!ensure(c, c->h_present, (size_t)nct + 64, "halo present mask")) return -1;
+  } else {
+    release(c->h_present);
+  }
   if (hp) {
     hp->z[0] = (unsigned *)c->h_plan.p;
     hp->zn[0] = (int)((pbytes + 3) / 4);
-    hp->z[1] = (unsigned *)c->h_dem.p;
-    hp->zn[1] = (int)dwords;
+    hp->z[1] = keep ? nullptr : (unsigned *)c->h_dem.p;  // (kept: zeroed by the plan at a rebuild)
+    hp->zn[1] = keep ? 0 : (int)dwords;
   } else {
     BSA_HIP(c, hipMemsetAsync(c->h_plan.p, 0, pbytes, c->stream));
     BSA_HIP(c, hipMemsetAsync(c->h_dem.p, 0, dwords * 4, c->stream));
@@ -256,22 +308,29 @@ static inline int tile_lo(int64_t rb) { return (int)(rb / kTile); }
 // (a rank without rows owns no tile: its clamped rb = n need not be tile-aligned)
 static inline int tile_hi(int64_t rb, int64_t re) { return re > rb ? (int)((re + kTile - 1) / kTile) : tile_lo(rb); }
 
-// box block of the exchange: [tpr own tile boxes | W request words]
-static size_t block_bytes(int tpr, int W) { return ((size_t)tpr * sizeof(TileBox) + (size_t)W * 4 + 15) / 16 * 16; }
+// box block of the exchange: [tpr own tile boxes | W request words | rebuild flag word]
+static size_t block_bytes(int tpr, int W) { return ((size_t)tpr * sizeof(TileBox) + (size_t)(W + 1) * 4 + 15) / 16 * 16; }
 
-int halo_pre(Ctx *c, int64_t rb, int64_t re, HaloPre *hp) {
+unsigned *halo_flag_word(Ctx *c) {
+  if (c->halo_mode == 2) return c->tpr_ctl.p ? (unsigned *)((unsigned long long *)c->tpr_ctl.p + 5) : nullptr;
+  const int nct = nct_of(c), tpr = tpr_of(c), W = (nct + 31) / 32;
+  return c->h_blk.p ? (unsigned *)((char *)c->h_blk.p + (size_t)tpr * sizeof(TileBox)) + W : nullptr;
+}
+
+int halo_pre(Ctx *c, int64_t rb, int64_t re, HaloPre *hp, const HaloTpr *ht) {
   *hp = HaloPre{};
+  const bool keep = ht && ht->tpr;
   const int nct = nct_of(c), a0 = tile_lo(rb), a1 = tile_hi(rb, re), na = a1 - a0;
   if (!ensure(c, c->counters, sizeof(Counters), "counters")) return -1;
   if (c->halo_mode == 2) {  // probe: source blocks of tpr = na tiles, full capacity each
     const int tpr = std::max(na, 1), Rp = (nct + tpr - 1) / tpr;
-    if (plan_buffers(c, nct, 1, tpr, Rp, hp)) return -1;
+    if (plan_buffers(c, nct, 1, tpr, Rp, hp, keep)) return -1;
     return ensure(c, c->h_hl, (size_t)Rp * tpr * 4, "halo list") ? 0 : -1;
   }
   const int R = c->nranks, tpr = tpr_of(c), W = (nct + 31) / 32;
   const size_t bb = block_bytes(tpr, W);
   if (!ensure(c, c->h_blk, bb, "halo box block") || !ensure(c, c->h_gblk, bb * R, "halo box blocks")) return -1;
-  if (plan_buffers(c, nct, R, tpr, R, hp)) return -1;
+  if (plan_buffers(c, nct, R, tpr, R, hp, keep)) return -1;
   hp->z[2] = (unsigned *)((char *)c->h_blk.p + (size_t)tpr * sizeof(TileBox));  // request words
   hp->zn[2] = W;
   hp->blk = (TileBox *)c->h_blk.p;
@@ -283,30 +342,34 @@ int halo_pre(Ctx *c, int64_t rb, int64_t re, HaloPre *hp) {
 // every tile's box is in tbox_c; the present mask and the flat list (source
 // blocks of tpr tiles, full capacity each) come out.  The buffers were zeroed
 // by the caller (plan_buffers).
-static int plan_local(Ctx *c, int a0, int a1, int tpr) {
+static int plan_local(Ctx *c, int a0, int a1, int tpr, const HaloTpr *ht) {
   const int nct = nct_of(c), na = a1 - a0;
   const int Rp = (nct + tpr - 1) / tpr;
   c->halo_hl = (int64_t)Rp * tpr;
   c->halo_tot_word = 2 * Rp;
   uint8_t *recv = (uint8_t *)c->h_plan.p;
-  PlanArgs pa{nct, tpr, 1, -1, a0, a1, (const TileBox *)c->tbox_c.p, nullptr, 0, nullptr, recv, nullptr};
+  const HaloTpr h = ht ? *ht : HaloTpr{};
+  PlanArgs pa{nct, tpr, 1, -1, a0, a1, (const TileBox *)c->tbox_c.p, nullptr, 0, nullptr, recv, nullptr,
+              0, h, (unsigned *)c->h_dem.p, 2 * Rp + 1};
   ListArgs la{nct, tpr, Rp, -1, a0, a1, 1, recv, nullptr, (int *)c->h_hl.p, nullptr, (unsigned *)c->h_dem.p,
               (Counters *)c->counters.p};
   const int ny = std::max(1, std::min(na, kPlanRows));
   hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((nct + 255) / 256), (unsigned)ny), dim3(256), 0, c->stream, pa, ny);
   BSA_HIP(c, hipGetLastError());
-  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)Rp), dim3(256), 0, c->stream, la, HaloCaps{});
+  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)Rp), dim3(256), 0, c->stream, la, HaloCaps{},
+                     (const unsigned long long *)(h.tpr ? h.ctl : nullptr),
+                     h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, h.tpr ? h.myflag : (unsigned *)nullptr);
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
 
-int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu) {
+int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht) {
   hu->rbuf = nullptr;
   const int nct = nct_of(c);
   const int a0 = tile_lo(rb), a1 = tile_hi(rb, re), na = a1 - a0;
   if (c->halo_mode == 2) {
     c->halo_fields = 0;
-    return plan_local(c, a0, a1, std::max(na, 1));
+    return plan_local(c, a0, a1, std::max(na, 1), ht);
   }
   // ---- exchange mode (several ranks); halo_pre's buffers, zeroed by the own-tile K0b
   const int R = c->nranks, me = c->rank, tpr = tpr_of(c);
@@ -317,15 +380,20 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu) {
   const size_t bb = block_bytes(tpr, W);
   // 2. own tile boxes (written by K0b) + request bits -> every rank
   unsigned *req = (unsigned *)((char *)c->h_blk.p + (size_t)tpr * sizeof(TileBox));
+  const bool keep = ht && ht->tpr;
+  // the fields per halo row fix the regions' layout (the kept send headers sit
+  // at its offsets): a change of it is a rebuild on every rank alike
+  const int nf = (c->simp.winddim == 0 && c->sim_gs_derivable) ? 6 : 8;
+  if (keep && nf != c->halo_fields) ht->force = 1;
   if (c->simp.resume_nav && c->bk_ready && na > 0) {
     hipLaunchKernelGGL(k_halo_req, dim3(64), dim3(256), 0, s, (int)(c->sim_re - c->sim_rb),
                        (const unsigned *)c->bk_rptr.p, (const unsigned *)c->bk_rcol.p, (const unsigned *)c->id2h.p,
-                       a0, a1, req);
+                       a0, a1, req, keep ? (const uint8_t *)c->h_present.p : (const uint8_t *)nullptr,
+                       keep ? ht->myflag : (unsigned *)nullptr);
     BSA_HIP(c, hipGetLastError());
   }
   if (comm_allgather(c, c->h_blk.p, c->h_gblk.p, bb)) return -1;
   // capacities and offsets of this rank's regions
-  const int nf = (c->simp.winddim == 0 && c->sim_gs_derivable) ? 6 : 8;
   HaloCaps cp{};
   size_t roff = 0;
   int hoff = 0, smax = 0;
@@ -350,15 +418,18 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu) {
     return -1;
   // 3. plan + lists, one launch
   uint8_t *recv = (uint8_t *)c->h_plan.p, *sendf = recv + nct;
+  const HaloTpr h = ht ? *ht : HaloTpr{};
   PlanArgs pa{nct, tpr, R, me, a0, a1, (const TileBox *)c->tbox_c.p, (const unsigned char *)c->h_gblk.p, bb,
-              (TileBox *)c->tbox_c.p, recv, sendf};
+              (TileBox *)c->tbox_c.p, recv, sendf, W, h, (unsigned *)c->h_dem.p, 2 * R + 1};
   ListArgs la{nct, tpr, R, me, a0, a1, 0, recv, sendf, (int *)c->h_hl.p, (unsigned char *)c->h_send.p,
               (unsigned *)c->h_dem.p, (Counters *)c->counters.p};
   const int ny = std::max(1, std::min(na, kPlanRows));
   hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((std::max(nct, R * na) + 255) / 256), (unsigned)(ny + 2)),
                      dim3(256), 0, s, pa, ny);
   BSA_HIP(c, hipGetLastError());
-  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)R), dim3(256), 0, s, la, cp);
+  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)R), dim3(256), 0, s, la, cp,
+                     (const unsigned long long *)(h.tpr ? h.ctl : nullptr),
+                     h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, h.tpr ? h.myflag : (unsigned *)nullptr);
   BSA_HIP(c, hipGetLastError());
   HaloFields fl{};
   DevBuf *src[8] = {&c->own[0], &c->own[1], &c->own[2], &c->own[3], &c->own[4], &c->own[5], &c->s_gse, &c->s_gsn};
@@ -403,8 +474,15 @@ int halo_init_caps(Ctx *c) {
   for (int q = 0; q < R; ++q) {
     const int a0 = q * tpr, a1 = a0 + tiles_of(c, q);
     const int Rp = (nct + tpr - 1) / tpr;
-    if (plan_buffers(c, nct, 1, tpr, Rp, nullptr) || !ensure(c, c->h_hl, (size_t)Rp * tpr * 4, "halo list") ||
-        plan_local(c, a0, a1, tpr))
+    // (with plan reuse every plan is made on grown boxes: the capacities too)
+    HaloTpr ht{c->tpr_on ? 1 : 0, 1, c->tpr_dx, c->tpr_ds, c->tpr_dv, nullptr, nullptr};
+    if (ht.tpr) {
+      if (!ensure(c, c->tpr_ctl, 64, "tile-pair list control")) return -1;
+      ht.ctl = (unsigned long long *)c->tpr_ctl.p;
+      ht.myflag = (unsigned *)(ht.ctl + 5);
+    }
+    if (plan_buffers(c, nct, 1, tpr, Rp, nullptr, false) || !ensure(c, c->h_hl, (size_t)Rp * tpr * 4, "halo list") ||
+        plan_local(c, a0, a1, tpr, ht.tpr ? &ht : nullptr))
       return -1;
     BSA_HIP(c, hipMemcpyAsync(recv.data(), c->h_plan.p, (size_t)nct, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
@@ -451,7 +529,8 @@ int halo_grow(Ctx *c) {
 }
 
 void halo_release(Ctx *c) {
-  DevBuf *all[] = {&c->h_blk, &c->h_gblk, &c->h_plan, &c->h_lists, &c->h_send, &c->h_recv, &c->h_hl, &c->h_dem};
+  DevBuf *all[] = {&c->h_blk, &c->h_gblk, &c->h_plan, &c->h_lists, &c->h_send, &c->h_recv, &c->h_hl, &c->h_dem,
+                   &c->h_present};
   for (auto *b : all) release(*b);
   c->halo_cap.clear();
   c->halo_hl = 0;

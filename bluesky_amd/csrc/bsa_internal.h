@@ -208,7 +208,7 @@ struct Ctx {
   // outside raises tpr_ctl[0] and the next detect rebuilds on the device
   bool tpr_on = true;                  // resident home-order detects of all rows (BSA_TPR=0: off)
   bool tpr_valid = false;              // a list + snapshot exist for tpr_key / tpr_n
-  double tpr_key[4] = {0, 0, 0, 0};    // rpz hpz tla mid of the list
+  double tpr_key[6] = {0, 0, 0, 0, 0, 0};  // rpz hpz tla mid row_begin row_end of the list
   int64_t tpr_n = -1;
   float tpr_dx = 3.2e-4f, tpr_ds = 1.6e-5f, tpr_dv = 300.f;  // ~2 km, ~100 m of reach, 300 m
   DevBuf tpr_snap;                     // PFRec per aircraft at the last build
@@ -291,6 +291,7 @@ struct Ctx {
                                    // 2 one-GPU probe of one rank's share (bsa_sim_detect_rows)
   std::vector<int64_t> halo_cap;   // R x R tile capacities [sender * R + receiver], equal on all ranks
   DevBuf h_blk, h_gblk, h_plan, h_lists, h_send, h_recv, h_hl, h_dem;
+  DevBuf h_present;                // plan reuse: the kept plan's present mask (k_halo_lists at a rebuild)
   int64_t halo_hl = 0;             // slots of the flat halo tile list (this rank's receive capacities)
   int64_t halo_grows = 0;          // capacity regrowths (aborted steps)
   int64_t halo_rx = 0, halo_tx = 0;  // bytes received / sent per CD step (the capacities' transfers)

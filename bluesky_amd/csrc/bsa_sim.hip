@@ -587,6 +587,7 @@ static int sim_cd(Ctx *c, bool allow_defer) {
 // overflow re-runs the step here with unchanged buffers)
 static int grow_after_abort(Ctx *c, const unsigned long long *ctl) {
   c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
+  c->tpr_valid = false;    // ... and any kept tile-pair list / halo plan (every rank aborted alike)
   c->zeroed_rows = -1;     // ... and zeroes every per-detect buffer (an aborted K2 wrote no inconf / tcpamax)
   {
     Counters h;
@@ -701,6 +702,7 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   c->sim_steps = c->sim_cd_calls = c->sim_last_conf = c->sim_last_los = 0;
   c->sim_gathered = true;
   c->sim_prepped = false;
+  c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
   c->sim_gs_derivable = false;  // gseast / gsnorth are the host's until K4' runs
   if (c->feed_pending) {  // a snapshot of the previous sim is dropped
     BSA_HIP(c, hipEventSynchronize(c->feed_ev));
@@ -807,6 +809,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     // re-runs the step with unchanged buffers here) and all ranks re-run it
     c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
     c->sim_prepped = false;  // (an aborted K4' prepared nothing)
+    c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
     const int64_t done = (int64_t)ctl[1];
     c->sim_steps = base + done;
     c->sim_gs_derivable = done > 0 ? c->simp.winddim == 0 : derivable0;  // K4' ran for the completed steps only
@@ -918,6 +921,7 @@ int bsa_sim_update(bsa_ctx *cc, const bsa_sim_state *s) {
   }
   if (hb.run()) return -1;
   c->sim_prepped = false;  // prepared records are of the old state
+  c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
   if (any_cd) {
     // every rank passed the same full arrays: the replicas are consistent only
     // if ALL replicated arrays were passed; otherwise the next all-gather
@@ -1114,6 +1118,7 @@ int bsa_sim_set_params(bsa_ctx *cc, const bsa_sim_params *p) {
   if (p->resume_nav && !c->simp.resume_nav) c->bk_ready = false;  // the bookkeeping starts empty
   c->simp = *p;
   c->sim_prepped = false;
+  c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
   return 0;
 }
 

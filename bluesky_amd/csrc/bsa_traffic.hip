@@ -345,6 +345,7 @@ static void set_n(Ctx *c, int64_t n) {
   c->reuse_valid = false;  // so is any reusable candidate list
   c->sim_gathered = true;  // every replica is complete after the change
   c->sim_prepped = false;  // prepared records are of the old traffic
+  c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
 }
 
 // length of each full-n per-aircraft buffer for n aircraft (several ranks: the

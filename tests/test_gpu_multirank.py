@@ -244,26 +244,40 @@ def test_home_ranges_and_row_ids(ctx):
 
 
 # ---------------------------------------------------------------- halo exchange
-def sharded_vs_world1(ctx, t, p, world, steps, between=None, resume_nav=False):
+def sharded_vs_world1(ctx, t, p, world, steps, between=None, resume_nav=False, tile=None):
     """World-1 run vs ``world`` in-process ranks: every state array bitwise, the
     C2-gathered pair lists bitwise (and the ASAS bookkeeping with resume_nav)
     after each of ``steps`` steps; ``between(k, sim)`` may change parameters
-    before step k on every rank.  Returns the ranks' halo statistics."""
+    before step k on every rank; ``tile`` = tile-pair list reuse budgets of
+    every run (None: the one-rank run rebuilds at every detect, the ranks use
+    the defaults).  Returns the ranks' halo statistics (with each rank's
+    tile_reuse_stats in the last step's) and the one-rank results."""
     init = resident.initial_state(t)
-    ref = resident.ResidentSim(init, p, ctx=ctx)
-    exp = []
-    for k in range(steps):
-        if between:
-            between(k, ref)
-        ref.step(1)
-        st = ref.stats()
-        e = dict(state=ref.read(), pairs=ctx.fetch_pairs(st['n_conf'], st['n_los']))
-        if resume_nav:
-            i, j = ref.resopairs()
-            e.update(bk=ref.asas_stats(), reso=sorted(zip(i.tolist(), j.tolist())))
-        exp.append(e)
+    if tile is None:
+        ctx.set_tile_reuse(False)
+    else:
+        ctx.set_tile_reuse(True, *tile)
+    try:
+        ref = resident.ResidentSim(init, p, ctx=ctx)
+        t0 = ctx.tile_reuse_stats()
+        exp = []
+        for k in range(steps):
+            if between:
+                between(k, ref)
+            ref.step(1)
+            st = ref.stats()
+            e = dict(state=ref.read(), pairs=ctx.fetch_pairs(st['n_conf'], st['n_los']))
+            if resume_nav:
+                i, j = ref.resopairs()
+                e.update(bk=ref.asas_stats(), reso=sorted(zip(i.tolist(), j.tolist())))
+            exp.append(e)
+        exp[-1]['tile'] = {k: v - t0[k] for k, v in ctx.tile_reuse_stats().items()}
+    finally:
+        ctx.set_tile_reuse(True)
 
     def rank(r, c, g):
+        if tile is not None:
+            c.set_tile_reuse(True, *tile)
         sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=world, group=g)
         got = []
         for k in range(steps):
@@ -275,6 +289,7 @@ def sharded_vs_world1(ctx, t, p, world, steps, between=None, resume_nav=False):
                 i, j = sim.resopairs()
                 e.update(bk=sim.asas_stats(), reso=list(zip(i.tolist(), j.tolist())))
             got.append(e)
+        got[-1]['halo'] = dict(got[-1]['halo'], tile=c.tile_reuse_stats())
         return got
 
     res = run_ranks(world, rank, timeout=600)
@@ -356,6 +371,40 @@ def test_halo_wind_then_calm_equal_world1(ctx):
     for h in halo:
         if h[4]['rx_bytes'] and h[3]['regrowths'] == h[4]['regrowths']:
             assert h[3]['rx_bytes'] > h[4]['rx_bytes'] == h[5]['rx_bytes'], h
+
+
+@pytest.mark.parametrize('world, simdt, tile, steps, swh', [
+    (3, 0.05, (2016.0, 300.0), 30, True),    # the bench cadence: plan + list kept over many detects
+    (3, 0.05, (2016.0, 300.0), 16, False),   # + vertical MVP: vs changes move the records' intervals
+    (2, 1.0, (2016.0, 300.0), 16, True),     # 250 m per step: some record leaves its box often
+    (3, 1.0, (1.0, 1.0), 8, True),           # budgets below one step's drift: rebuild at every detect
+])
+def test_halo_plan_reuse_equal_world1(ctx, world, simdt, tile, steps, swh):
+    """DESIGN.md 3.18 across ranks: the halo plan, the send / receive lists and
+    K0d's tile-pair list are built on grown boxes and kept while every rank's
+    records stay inside them (each rank's own-tile K0b raises a flag that
+    travels with the box all-gather; one raised flag rebuilds all three on
+    every rank).  Bitwise equal to the one-rank run after every step, with MVP
+    manoeuvres.  Every rank decides alike, and about as often as the one-rank
+    run with the same budgets (whose K4' checks the same records: the ranks
+    also rebuild when the halo's fields change, 8 -> 6 after the first K4')."""
+    t = synth.box(20000, 300.0, seed=103)
+    p = resident.params(simdt=simdt, swresohoriz=swh)
+    halo, exp = sharded_vs_world1(ctx, t, p, world, steps, tile=tile)
+    assert sum(len(e['pairs']['ci']) for e in exp) > 0
+    st = [h[-1]['tile'] for h in halo]
+    assert len({(s['builds'], s['detects']) for s in st}) == 1, st   # every rank decides alike
+    b, d = st[0]['builds'], st[0]['detects']
+    b1 = exp[-1]['tile']['builds']
+    print('world %d simdt %g swh %s: builds %d of %d detects (one rank: %d of %d)' %
+          (world, simdt, swh, b, d, b1, exp[-1]['tile']['detects']))
+    assert steps <= d <= steps + 2, st      # (+ a re-run step after a capacity regrowth)
+    if tile == (1.0, 1.0):
+        assert b == d, st
+    else:
+        assert 1 <= b <= b1 + 3, (st, exp[-1]['tile'])
+        if swh and simdt == 0.05:
+            assert b <= 8, st
 
 
 def test_halo_capacity_disagreement_fails_loudly():
