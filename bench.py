@@ -340,18 +340,28 @@ def main():
     if 'lds_bank_conflict_rate' in pf:
         roof['lds_bank_conflict_rate'] = pf['lds_bank_conflict_rate']
     kin = pmc.get('k_sim_pilot_kin', {})
+    kin_kernel, kin_note = 'k_sim_pilot_kin', None
+    fused = world == 1 and os.environ.get('BSA_K24', '1') != '0'
+    if not kin.get('dur_ns') and fused and pmc.get('k_rank_rows', {}).get('dur_ns'):
+        # one rank: K4' runs inside K2's launch (k_rank_rows<true>)
+        kin = pmc['k_rank_rows']
+        kin_kernel = "k_rank_rows<true> (K2 fused with K4')"
+        kin_note = ("the launch also places the detect's pairs (K2): the kinematics' bytes over the whole "
+                    "launch's duration, a lower bound of K4''s own fraction")
     propagation = None
     if kin.get('dur_ns'):
         nrows_r0 = (n + world - 1) // world
         prep = world == 1 and not args.reuse and os.environ.get('BSA_SIM_PREP', '1') != '0'
         pb = prep_bytes_per_ac(n) if prep else 0
         alg = int((KIN_BYTES_PER_AC + pb) * nrows_r0)
-        propagation = dict(kernel='k_sim_pilot_kin', bound='hbm', algorithmic_bytes=alg, from_profile=prov,
+        propagation = dict(kernel=kin_kernel, bound='hbm', algorithmic_bytes=alg, from_profile=prov,
                            bytes_per_aircraft=dict(kinematics=KIN_BYTES_PER_AC, next_detect_records=pb),
                            duration_us_profiled=kin['dur_ns'] * 1e-3,
                            achieved_GBps=alg / kin['dur_ns'], peak_GBps=HBM_PEAK_GBPS,
                            frac=alg / kin['dur_ns'] / HBM_PEAK_GBPS,
                            measured_bytes=(kin.get('hbm_read_bytes', 0) + kin.get('hbm_write_bytes', 0)) or None)
+        if kin_note:
+            propagation['note'] = kin_note
     ex = pmc.get('k_exact', {})
     exact_fp64 = None
     if ex.get('fp64_flops'):

@@ -32,6 +32,7 @@
 #include "bsa_mvp_math.h"
 #include "bsa_mvp_row.h"
 #include "bsa_prep.h"
+#include "bsa_sim_row.h"
 
 #pragma clang fp contract(off)
 
@@ -1821,6 +1822,7 @@ __global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__
   }
 }
 
+template <bool K24>
 __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters *__restrict__ cnt, unsigned long long cap,
                                                          unsigned *__restrict__ rowoff,
                                                          unsigned *__restrict__ rowcnt,
@@ -1834,7 +1836,7 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
                                                          unsigned char *__restrict__ inconf,
                                                          unsigned long long *__restrict__ tcpamax_bits,
                                                          Counters *__restrict__ cnext,
-                                                         unsigned long long *__restrict__ wnext) {
+                                                         unsigned long long *__restrict__ wnext, K24Args ka) {
   constexpr int W = kRankThreads / 64;
   __shared__ unsigned red[4][W];
   __shared__ unsigned soff[2][kRankRows + 1];  // the block's rows' exclusive offsets (conf, LoS), + total
@@ -1922,6 +1924,21 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
       gate[0] = ovf ? 1 : 0;
       gate[1] = ovf ? 0 : P;
     }
+  }
+  // fused K4' (K24): an aborted step (this detect overflowed, or an earlier
+  // step of the batch did) keeps every row's state -- including the double
+  // buffer's other half, which the host swaps in after the step
+  const bool k24_stop = K24 && (ovf || *ka.d.sticky != 0u);
+  if (K24 && k24_stop) {
+    if (ovf && b == 0 && t == 0) ka.mv.sticky[0] = 1u;
+    if (rowlane && r < nrows) {
+      const int k = rb + r;
+      ka.d.alt_w[k] = ka.d.alt[k];
+      ka.d.vs_w[k] = ka.d.vs[k];
+      ka.d.gse_w[k] = ka.d.gse[k];
+      ka.d.gsn_w[k] = ka.d.gsn[k];
+    }
+    return;
   }
   if (ovf) return;
   const unsigned ec = wc + xc - c, el = wl + xl - l;  // exclusive, within the block
@@ -2018,17 +2035,45 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
   // atomics on the bit patterns made it -- and K3's fold of the row's pairs,
   // in order (MVP.py:44-61), from LDS or from pdv / pfl
   __syncthreads();
-  if (!rowlane || r >= nrows) return;
-  inconf[r] = c ? 1 : 0;
-  unsigned long long tm = 0ull;
-  for (unsigned k = 0; k < c; ++k) {
-    const double tq = lds ? stc[ec + k] : out[(size_t)2 * P + cb + ec + k];
-    const unsigned long long bits = (unsigned long long)__double_as_longlong(tq);
-    if (tq > 0.0 && bits > tm) tm = bits;
+  const bool live = rowlane && r < nrows;
+  if (!K24 && !live) return;
+  if (live) {
+    inconf[r] = c ? 1 : 0;
+    unsigned long long tm = 0ull;
+    for (unsigned k = 0; k < c; ++k) {
+      const double tq = lds ? stc[ec + k] : out[(size_t)2 * P + cb + ec + k];
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(tq);
+      if (tq > 0.0 && bits > tm) tm = bits;
+    }
+    tcpamax_bits[r] = tm;
+    if (mf.rowdv)
+      mf.rowdv[r] = lds_fold ? mvp_fold(sdv, sfl, ec, ec + c) : mvp_fold(mf.pdv, mf.pfl, cb + ec, cb + ec + c);
   }
-  tcpamax_bits[r] = tm;
-  if (mf.rowdv)
-    mf.rowdv[r] = lds_fold ? mvp_fold(sdv, sfl, ec, ec + c) : mvp_fold(mf.pdv, mf.pfl, cb + ec, cb + ec + c);
+  if (K24) {  // K4' of this workgroup's rows (k_sim_pilot_kin<true, PREP>'s body), every lane
+    __shared__ unsigned long long sgate[2];
+    if (t == 0) {
+      sgate[0] = 0ull;
+      sgate[1] = P;
+    }
+    __syncthreads();
+    if (b == 0 && t == 0) *ka.d.steps_done += 1;
+    MvpIn mv = ka.mv;
+    mv.gate = sgate;
+    const int k = rb + r;  // (rows = all aircraft: rb = 0)
+    if (ka.prep) {  // the wave's group boxes from its lanes' records (lanes past the rows too)
+      PFRec pr{}, pb{};
+      if (ka.pa.snap && live) pb = ka.pa.snap[k];
+      if (live)
+        pr = pilot_kin_row<true, true>(rb, k, ka.simdt, ka.winddim, ka.vwn, ka.vwe, ka.wf, ka.d, mv, ka.mp, ka.pa);
+      group_boxes_v(ka.pa.n, k / kGroup, pr, ka.pa.sbox, ka.pa.gbox);
+      if (ka.pa.snap) {
+        const bool outb = live && !pf_within(pr, pb, ka.pa.dx, ka.pa.ds, ka.pa.dv);
+        if (__ballot(outb) && lane == 0) ka.pa.tpr_ctl[0] = 1ull;
+      }
+    } else if (live) {
+      pilot_kin_row<true, false>(rb, k, ka.simdt, ka.winddim, ka.vwn, ka.vwe, ka.wf, ka.d, mv, ka.mp, ka.pa);
+    }
+  }
 }
 
 // Zero the per-detect state: counters (but `tiles` unless full; with keep,
@@ -2170,6 +2215,37 @@ int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla) {
 
 // Enqueue one complete detect on the stream (K0-K2), no host synchronisation.
 // gate (device, nullable): receives {overflow, P} for the resident sim step.
+// k_rank_rows' arguments (kept for a fused launch, k24_launch)
+struct RankLaunch {
+  unsigned grid;
+  int nrows;
+  Counters *cnt;
+  unsigned long long cap;
+  unsigned *rowoff, *rowcnt;
+  const uint2 *kb;
+  int B;
+  const double *cpay;
+  int rb;
+  int *ci, *cj;
+  double *out;
+  int *li, *lj;
+  unsigned long long *stats, *gate;
+  const unsigned *build;
+  MvpFuse mf;
+  unsigned char *inconf;
+  unsigned long long *tcpamax;
+  Counters *cnext;
+  unsigned long long *wnext;
+};
+static int rank_launch(Ctx *c, const RankLaunch &a, bool k24, const K24Args &ka) {
+  const auto K = k24 ? k_rank_rows<true> : k_rank_rows<false>;
+  hipLaunchKernelGGL(K, dim3(a.grid), dim3(kRankThreads), 0, c->stream, a.nrows, a.cnt, a.cap, a.rowoff, a.rowcnt,
+                     a.kb, a.B, a.cpay, a.rb, a.ci, a.cj, a.out, a.li, a.lj, a.stats, a.gate, a.build, a.mf,
+                     a.inconf, a.tcpamax, a.cnext, a.wnext, ka);
+  BSA_HIP(c, hipGetLastError());
+  return 0;
+}
+
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
                    unsigned long long *gate) {
   c->fuse_done = false;  // set again only if K2 below evaluates MVP's per-pair vectors
@@ -2624,13 +2700,20 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   if (B) {
     hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows)), dim3(64), 0, c->stream, (int)nrows,
                        (unsigned *)c->rowcnt.p);
-    hipLaunchKernelGGL(k_rank_rows, dim3((unsigned)rank_blocks((int)nrows)), dim3(kRankThreads), 0, c->stream,
-                       (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p, (unsigned *)c->rowcnt.p,
-                       (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb, (int *)c->out_ci.p,
-                       (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
-                       (unsigned long long *)c->stats.p, gate, build, mf, (unsigned char *)c->inconf.p,
-                       (unsigned long long *)c->tcpamax.p, (Counters *)c->counters2.p,
-                       (unsigned long long *)c->workq2.p);
+    const RankLaunch rl{(unsigned)rank_blocks((int)nrows), (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p,
+                        (unsigned *)c->rowcnt.p, (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb,
+                        (int *)c->out_ci.p, (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p,
+                        (int *)c->out_lj.p, (unsigned long long *)c->stats.p, gate, build, mf,
+                        (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
+                        (Counters *)c->counters2.p, (unsigned long long *)c->workq2.p};
+    if (c->k24_want) {  // bsa_sim_step launches it fused with K4' (k24_launch)
+      c->k24_blob.resize(sizeof rl);
+      memcpy(c->k24_blob.data(), &rl, sizeof rl);
+      c->k24_pending = true;
+      c->k24_ev = timed ? ev[4] : nullptr;
+    } else {
+      rank_launch(c, rl, false, K24Args{});
+    }
     c->zeroed_rows = nrows;
   } else {
     hipLaunchKernelGGL(k_rank, dim3(256 * 4), dim3(256), 0, c->stream, (int)nrows, dcnt, cap,
@@ -2641,8 +2724,20 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (unsigned long long *)c->stats.p, gate, build, mf);
   }
   BSA_HIP(c, hipGetLastError());
-  if (mark(4)) return -1;
+  if (!c->k24_pending && mark(4)) return -1;
   c->ev_valid = c->ev_valid || timed;
+  return 0;
+}
+
+// the K2 launch kept by detect_enqueue, fused with the step's K4'
+int k24_launch(Ctx *c, const K24Args &ka) {
+  if (!c->k24_pending || c->k24_blob.size() != sizeof(RankLaunch)) return fail(c, "internal: no K2 launch to fuse");
+  RankLaunch rl;
+  memcpy(&rl, c->k24_blob.data(), sizeof rl);
+  c->k24_pending = false;
+  if (rank_launch(c, rl, true, ka)) return -1;
+  if (c->k24_ev) BSA_HIP(c, hipEventRecord(c->k24_ev, c->stream));
+  c->k24_ev = nullptr;
   return 0;
 }
 

@@ -257,6 +257,13 @@ struct Ctx {
   bool sim_ready = false;
   bool mvp_deferred = false;            // this step's K3 rows run inside K4' (sim_cd -> bsa_sim_step)
   std::vector<unsigned char> mvp_defer;  // the deferred K3 arguments (MvpIn, bsa_mvp_row.h)
+  // K2 fused with K4' (one rank): sim_cd asks (k24_want), detect_enqueue then
+  // keeps its K2 launch (k24_blob) for k24_launch, with the timed detect's
+  // last stage event; alt / vs / gseast / gsnorth double buffers
+  bool k24_want = false, k24_pending = false;
+  std::vector<unsigned char> k24_blob;
+  hipEvent_t k24_ev = nullptr;
+  DevBuf nx_alt, nx_vs, nx_gse, nx_gsn;
   bsa_sim_params simp{};
   int64_t sim_steps = 0, sim_cd_calls = 0, sim_rb = 0, sim_re = 0, sim_rpr = 0;
   int64_t sim_last_conf = 0, sim_last_los = 0;

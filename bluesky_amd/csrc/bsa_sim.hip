@@ -24,130 +24,11 @@
 #include "bsa_kin_math.h"
 #include "bsa_mvp_row.h"
 #include "bsa_prep.h"
+#include "bsa_sim_row.h"
 
 #pragma clang fp contract(off)
 
 namespace bsa {
-
-struct SimDev {
-  double *lat, *lon, *trk, *gs, *alt, *vs, *tas, *hdg, *gse, *gsn;
-  double *altprev;                 // pre-step altitude: the ACDATA feed derives traf.cas =
-                                   // vtas2cas(tas, altprev) (traffic.py:434) off the step
-  double *ax;                      // traf.ax (traffic.py:431), read by the OpenAP limits next step
-  const double *env;               // OpenAP envelope, 6 x n (hmax vmin vmax vsmin vsmax axmax) or NULL
-  const double *ptab;              // OpenAP type table (bsa_sim_set_perf) or NULL: envelope and
-  const int *ptype;                //   acceleration follow each aircraft's flight phase
-  uint8_t *phase;
-  double *atm;                     // traf.p / rho / Temp (traffic.py:389), 3 x n, or NULL
-  int n;
-  const double *aptrk, *aptas, *apalt, *apvs, *bank, *eps, *accel;
-  const double *atrk, *atas, *avs, *aalt;
-  const uint8_t *active;
-  const unsigned *sticky;          // abort flag of the step batch
-  unsigned long long *steps_done;  // steps completed in the batch
-};
-
-struct PrepArgs {
-  PrepOut out;
-  TileBox *sbox, *gbox;  // (the tile boxes follow from the group boxes in the detect's K0z)
-  double rpz, hpz, tla;
-  int mid, rec, n;
-  // tile-pair list reuse: the last build's records; a record
-  // outside its budgets raises tpr_ctl[0] (the next detect rebuilds), or NULL
-  const PFRec *snap;
-  unsigned long long *tpr_ctl;
-  float dx, ds, dv;
-};
-
-// one row of K4' (below).  The row's state is loaded before K3's part runs
-// (the loads overlap; K3 writes only the ASAS targets / asas.active, which
-// this lane then takes from its registers, MvpRowOut), so the row's memory
-// latency is paid about once instead of along a chain of dependent accesses.
-template <bool FUSE, bool PREP>
-__device__ __forceinline__ PFRec pilot_kin_row(int rb, int k, double simdt, int winddim, double vwn, double vwe,
-                                               const WindField &wf, const SimDev &d, const MvpIn &mv,
-                                               const bsa_mvp_params &mp, const PrepArgs &pa) {
-  kin::In s;
-  s.tas = d.tas[k];
-  s.hdg = d.hdg[k];
-  s.alt = d.alt[k];
-  s.vs = d.vs[k];
-  s.lat = d.lat[k];
-  s.lon = d.lon[k];
-  s.bank = d.bank[k];
-  s.eps = d.eps[k];
-  s.accel = d.accel[k];
-  const double aptrk = d.aptrk[k], aptas = d.aptas[k], apalt = d.apalt[k], apvs = d.apvs[k];
-  double atrk = d.atrk[k], atas = d.atas[k], avs = d.avs[k], aalt = d.aalt[k];
-  bool act = d.active[k] != 0;
-  const double ax0 = (d.ptab || d.env) ? d.ax[k] : 0.0;
-  if (FUSE) {
-    const MvpRowOut o = mvp_row(rb, k - rb, mp, mv);
-    if (o.act_valid) act = o.active != 0;
-    if (o.valid) {
-      atrk = o.trk;
-      atas = o.tas;
-      avs = o.vs;
-      aalt = o.alt;
-    }
-  }
-  if (winddim == 2) {  // pilot.py:32 and traffic.py:463 read the field at the same pre-step position
-    kin::windfield_2d(wf, s.lat, s.lon, vwn, vwe);
-    winddim = 1;
-  }
-  const double ptrk = act ? atrk : aptrk;             // pilot.py:41
-  double asastas = atas;                              // pilot.py:37-38: no wind, GS = TAS
-  if (winddim > 0) {                                  // pilot.py:31-35: ASAS GS -> TAS
-    const double asastasnorth = atas * cos(atrk * kD2R) - vwn;
-    const double asastaseast = atas * sin(atrk * kD2R) - vwe;
-    asastas = sqrt(asastasnorth * asastasnorth + asastaseast * asastaseast);
-  }
-  s.ptas = act ? asastas : aptas;                     // pilot.py:42
-  s.palt = act ? aalt : apalt;                        // pilot.py:43
-  s.pvs = fabs(act ? avs : apvs);                     // pilot.py:44,48
-  if (winddim > 0) {                                  // pilot.py:51-61: wind correction
-    const double Vw = sqrt(vwn * vwn + vwe * vwe);
-    const double winddir = atan2(vwe, vwn);
-    const double drift = ptrk * kD2R - winddir;
-    const double steer = asin(kin::npmin(1.0, kin::npmax(-1.0, Vw * sin(drift) / kin::npmax(0.001, s.tas))));
-    s.phdg = kin::nprem(ptrk + steer * kR2D, 360.);
-  } else {
-    s.phdg = kin::nprem(ptrk, 360.);                  // pilot.py:63
-  }
-  if (d.atm) {  // Traffic.update's first statement: p, rho, Temp = vatmos(alt) (traffic.py:389)
-    double p, rho, T;
-    kin::vatmos(s.alt, p, rho, T);
-    d.atm[k] = p;
-    d.atm[d.n + k] = rho;
-    d.atm[2 * d.n + k] = T;
-  }
-  if (d.ptab) {  // OpenAP.update (perfoap.py:115-131) on the pre-step state, then applylimits
-    const double *row = d.ptab + (size_t)d.ptype[k] * kin::kPerfCols;
-    const int ph = kin::openap_phase(row[22], s.vs, s.alt);
-    d.phase[k] = (uint8_t)ph;
-    kin::openap_limits(kin::openap_envelope(row, ph), ax0, s.ptas, s.pvs, s.palt);
-    s.accel = ph == kin::kPhaseGD ? 2.0 : 0.5;  // OpenAP.acceleration (perfoap.py:271-280)
-  } else if (d.env) {  // Pilot.applylimits (pilot.py:65-68, OpenAP), traffic.py:404
-    const kin::Envelope e{d.env[k], d.env[d.n + k], d.env[2 * d.n + k], d.env[3 * d.n + k],
-                          d.env[4 * d.n + k], d.env[5 * d.n + k]};
-    kin::openap_limits(e, ax0, s.ptas, s.pvs, s.palt);
-  }
-  const kin::Out o = kin::step(s, simdt, winddim, vwn, vwe);
-  d.tas[k] = o.tas;
-  d.hdg[k] = o.hdg;
-  d.alt[k] = o.alt;
-  d.vs[k] = o.vs;
-  d.lat[k] = o.lat;
-  d.lon[k] = o.lon;
-  d.gs[k] = o.gs;
-  d.trk[k] = o.trk;
-  d.gse[k] = o.gseast;
-  d.gsn[k] = o.gsnorth;
-  d.altprev[k] = s.alt;
-  d.ax[k] = o.ax;
-  if (PREP) return prep_home_record(k, o.lat, o.lon, o.trk, o.gs, o.alt, o.vs, pa.rpz, pa.hpz, pa.tla, pa.mid, pa.rec, pa.out);
-  return PFRec{};
-}
 
 // Pilot.APorASAS (pilot.py:28-63; no wind, constant wind or a 2-D field) +
 // UpdateAirSpeed/GroundSpeed/Position, rows [rb, re).  FUSE (a CD step without
@@ -229,6 +110,10 @@ static SimDev sim_dev(Ctx *c) {
   d.hdg = (double *)c->s_hdg.p;
   d.gse = (double *)c->s_gse.p;
   d.gsn = (double *)c->s_gsn.p;
+  d.alt_w = d.alt;
+  d.vs_w = d.vs;
+  d.gse_w = d.gse;
+  d.gsn_w = d.gsn;
   d.altprev = (double *)c->s_altprev.p;
   d.ax = (double *)c->s_ax.p;
   d.env = c->sim_limits ? (const double *)c->s_env.p : nullptr;
@@ -339,7 +224,7 @@ void sim_release(Ctx *c) {
                    &c->s_atrk, &c->s_atas, &c->s_avs, &c->s_aalt, &c->s_ase, &c->s_asn,
                    &c->s_active, &c->g_send, &c->g_recv, &c->pg_send, &c->pg_recv, &c->sim_ctl, &c->s_altprev, &c->s_ax, &c->s_env,
                    &c->s_ptab, &c->s_ptype, &c->s_phase, &c->s_noreso, &c->s_resooff, &c->s_dropped, &c->s_atm,
-                   &c->xfer_stage, &c->lbyidx, &c->fetch_stage, &c->tpr_snap, &c->tpr_ctl};
+                   &c->xfer_stage, &c->lbyidx, &c->fetch_stage, &c->tpr_snap, &c->tpr_ctl, &c->nx_alt, &c->nx_vs, &c->nx_gse, &c->nx_gsn};
   for (auto *b : all) release(*b);
   bk_release(c);
   halo_release(c);
@@ -729,8 +614,20 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     const bool derivable0 = c->sim_gs_derivable;
     BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 32, c->stream));  // sticky, steps_done, demands
     while (c->sim_steps < target) {
-      if (c->sim_steps % c->simp.cd_every == 0)
-        if (bsa::sim_cd(c, true)) return -1;
+      if (c->sim_steps % c->simp.cd_every == 0) {
+        // one rank: K2 and this step's K4' as one launch (k24_launch below;
+        // BSA_K24=0 off) -- K4' then starts on each workgroup's rows as soon as
+        // their fold is done, instead of behind the whole of K2
+        static const bool k24_env = !(getenv("BSA_K24") && atoi(getenv("BSA_K24")) == 0);
+        c->k24_want = k24_env && c->nranks == 1 && c->halo_mode == 0 && !c->simp.resume_nav && re > rb &&
+                      c->k2_bucket > 0;
+        const int r = bsa::sim_cd(c, true);
+        c->k24_want = false;
+        if (r) {
+          c->k24_pending = false;
+          return -1;
+        }
+      }
       // K4' workgroup size: one wave (at 100k rows 256-lane groups left half the
       // CUs one group short, 391 groups on 256 CUs: 0.1753 -> 0.1718 ms per
       // step with 64; BSA_K4_BLOCK=128/256 for A/B)
@@ -776,11 +673,31 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
       const int64_t nb = std::max<int64_t>(1, (re - rb + blk - 1) / blk);
       bsa::MvpIn mv{};
       if (c->mvp_deferred) memcpy(&mv, c->mvp_defer.data(), sizeof(mv));
-      const auto K4 = c->mvp_deferred ? (prep ? bsa::k_sim_pilot_kin<true, true> : bsa::k_sim_pilot_kin<true, false>)
-                                      : (prep ? bsa::k_sim_pilot_kin<false, true> : bsa::k_sim_pilot_kin<false, false>);
-      hipLaunchKernelGGL(K4, dim3((unsigned)nb), dim3(blk), 0, c->stream, (int)rb, (int)re, c->simp.simdt,
-                         c->simp.winddim, c->simp.windnorth, c->simp.windeast, bsa::wind_field(c), bsa::sim_dev(c), mv,
-                         c->simp.mvp, pa);
+      if (c->k24_pending) {  // K2 of this step's detect, fused with K4' (double-buffered alt / vs / gse / gsn)
+        const int64_t n = c->n;
+        if (!c->mvp_deferred) return bsa::fail(c, "internal: fused K2 + K4' without the deferred MVP rows");
+        if (!bsa::ensure(c, c->nx_alt, n * 8, "next altitudes") || !bsa::ensure(c, c->nx_vs, n * 8, "next vs") ||
+            !bsa::ensure(c, c->nx_gse, n * 8, "next gseast") || !bsa::ensure(c, c->nx_gsn, n * 8, "next gsnorth"))
+          return -1;
+        bsa::SimDev d = bsa::sim_dev(c);
+        d.alt_w = (double *)c->nx_alt.p;
+        d.vs_w = (double *)c->nx_vs.p;
+        d.gse_w = (double *)c->nx_gse.p;
+        d.gsn_w = (double *)c->nx_gsn.p;
+        const bsa::K24Args ka{d, mv, c->simp.mvp, pa, bsa::wind_field(c), c->simp.simdt, c->simp.windnorth,
+                              c->simp.windeast, c->simp.winddim, prep ? 1 : 0};
+        if (bsa::k24_launch(c, ka)) return -1;
+        std::swap(c->own[4], c->nx_alt);
+        std::swap(c->own[5], c->nx_vs);
+        std::swap(c->s_gse, c->nx_gse);
+        std::swap(c->s_gsn, c->nx_gsn);
+      } else {
+        const auto K4 = c->mvp_deferred ? (prep ? bsa::k_sim_pilot_kin<true, true> : bsa::k_sim_pilot_kin<true, false>)
+                                        : (prep ? bsa::k_sim_pilot_kin<false, true> : bsa::k_sim_pilot_kin<false, false>);
+        hipLaunchKernelGGL(K4, dim3((unsigned)nb), dim3(blk), 0, c->stream, (int)rb, (int)re, c->simp.simdt,
+                           c->simp.winddim, c->simp.windnorth, c->simp.windeast, bsa::wind_field(c), bsa::sim_dev(c),
+                           mv, c->simp.mvp, pa);
+      }
       c->mvp_deferred = false;
       c->sim_prepped = prep;
       if (prep) {
