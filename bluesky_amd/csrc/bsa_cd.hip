@@ -794,6 +794,32 @@ struct PfKnobs {
   int pieces;  // units per item (tile pair, 64-row slice): 1, 2, 4 (or 8, BSA_PF_PIECES)
   int pnear;   // ... per near item (the pair's boxes overlap: the densest items)
 };
+// Longest items first (a kept tile-pair list): the sweep's
+// span is set by its longest items (a dense item's refine runs up to ~60 us;
+// one that starts late ends long after the median wave).  Every unit adds its
+// duration to its list slot's cost; K1b lists the slots above a threshold for
+// the next detect (consecutive detects sweep nearly the same pairs), whose
+// prefilter dequeues those items first -- split as near items are -- and skips
+// them among the regular units (flag == epoch).  Every slot is swept exactly
+// once either way: results never depend on which items are listed.
+// Two tiers: list 0 (the longest, cost >= thresh[0]) in twice a near item's
+// pieces, list 1 (cost >= thresh[1]) split as near items are.
+struct HeavyArgs {
+  const unsigned *list[2];  // this detect's listed slots, or list[0] NULL (off)
+  const unsigned *count;    // ... their numbers [2]
+  unsigned *count_next;     // the next detect's [2], zeroed here (K1b appends)
+  const unsigned *flag;     // per slot: == epoch -> listed this detect
+  unsigned *cost;           // per slot: s_memrealtime ticks of its units (summed)
+  unsigned epoch;
+};
+struct HeavyNext {
+  unsigned *cost;           // read and zeroed
+  unsigned *list[2], *count, *flag;
+  unsigned epoch;           // the next detect's
+  unsigned thresh[2];       // ticks (100 MHz)
+  const unsigned long long *work;  // [1] near, [2] far items of this detect's list
+  unsigned long long icap;
+};
 #ifndef BSA_PF_WAVES_PER_EU
 #define BSA_PF_WAVES_PER_EU 4
 #endif
@@ -870,7 +896,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
     uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn, int diag,
-    TprArgs tp) {
+    TprArgs tp, HeavyArgs hv) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
   __shared__ float4 cen[PF_WAVES][32];      //                      e e' n n'     (stage 1)
@@ -934,7 +960,17 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // divisor expanded into ~50 scalar instructions per unit)
   const unsigned lnear = (unsigned)__builtin_ctz((unsigned)kn.pnear), lpc = (unsigned)__builtin_ctz((unsigned)kn.pieces);
   const unsigned inear = (unsigned)work[1], unear = inear << lnear;
-  const unsigned nunits = unear + ((unsigned)work[2] << lpc);
+  const unsigned nfar = (unsigned)work[2];
+  const unsigned nreg = unear + (nfar << lpc);
+  unsigned nh0 = 0, nh1 = 0;
+  if (hv.list[0]) {
+    nh0 = __builtin_amdgcn_readfirstlane(hv.count[0]);
+    nh1 = __builtin_amdgcn_readfirstlane(hv.count[1]);
+    if (blockIdx.x == 0 && threadIdx.x < 2) hv.count_next[threadIdx.x] = 0u;
+  }
+  const unsigned lh0 = lnear + 1u;
+  const unsigned hu0 = nh0 << lh0, hunits = hu0 + (nh1 << lnear);
+  const unsigned nunits = hunits + nreg;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
   unsigned long long *wq = work + shard * kWorkStride;
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
@@ -998,15 +1034,35 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const unsigned long long tr0 = __builtin_amdgcn_s_memrealtime();
     unsigned tr_subs = 0;
 #endif
-    do {  // one item; `break` ends it
-    // the item: (row tile | slice << 22, column tile)
-    const bool inr = item < unear;
-    const unsigned ls = inr ? lnear : lpc;
+    // the unit's list slot and piece: a listed item's piece (the first hunits
+    // units), or a regular unit -- skipped when its item is listed
+    unsigned long long slot;
+    unsigned ls, piece;
+    bool skip = false;
+    const unsigned long long hq0 = hv.cost ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    if (item < hunits) {
+      const bool t0 = item < hu0;
+      ls = t0 ? lh0 : lnear;
+      const unsigned ui = t0 ? item : item - hu0;
+      piece = ui & ((1u << ls) - 1u);
+      slot = hv.list[t0 ? 0 : 1][ui >> ls];
+      skip = !(slot < inear || (slot >= icap - nfar && slot < icap));  // (a slot of a list since rebuilt)
+      if (skip) slot = 0;
+    } else {
+      const unsigned uj = item - hunits;
+      const bool inr = uj < unear;
+      ls = inr ? lnear : lpc;
+      const unsigned ui = inr ? uj : uj - unear;
+      piece = ui & ((1u << ls) - 1u);
+      const unsigned e = inr ? (ui >> ls) : inear + (ui >> ls);
+      slot = e < inear ? (unsigned long long)e : icap - 1 - (unsigned long long)(e - inear);
+      if (hv.list[0]) skip = hv.flag[slot] == hv.epoch;
+    }
     const unsigned npc = 1u << ls;
-    const unsigned ui = inr ? item : item - unear;
-    const unsigned piece = ui & (npc - 1u);
-    const unsigned e = inr ? (ui >> ls) : inear + (ui >> ls);
-    const uint2 it = items[e < inear ? (unsigned long long)e : icap - 1 - (unsigned long long)(e - inear)];
+    const uint2 it = items[slot];  // (issued with the flag's load: the skip needs both)
+    do {  // one item; `break` ends it
+    if (skip) break;
+    // the item: (row tile | slice << 22, column tile)
     const uint2 rc = make_uint2(it.x & 0x3fffffu, it.y);
     const unsigned slice = it.x >> 22;
     // column sub-groups of this tile that may interact with the wave's row box:
@@ -1273,6 +1329,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       if (!more) break;
     }
     } while (0);
+    if (hv.cost && lane == 0 && !skip)  // (non-returning)
+      atomicAdd(&hv.cost[slot], (unsigned)(__builtin_amdgcn_s_memrealtime() - hq0));
 #ifdef BSA_PF_TRACE
     if (lane == 0 && pf_trace) {  // per-wave record region (no atomics)
       const unsigned long long slot = ((unsigned long long)blockIdx.x * PF_WAVES + w) * kTraceWave + tr_n++;
@@ -1549,7 +1607,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
     unsigned char *__restrict__ cflag, double *__restrict__ cpay, unsigned char *__restrict__ inconf,
     unsigned long long *__restrict__ tcpamax_bits, unsigned *__restrict__ rowcnt, uint2 *__restrict__ kb,
     int B,
-    unsigned *__restrict__ rctl, const Snap *__restrict__ snap_cur, Snap *__restrict__ snap_build, int nsnap) {
+    unsigned *__restrict__ rctl, const Snap *__restrict__ snap_cur, Snap *__restrict__ snap_build, int nsnap,
+    HeavyNext hn) {
+  if (hn.cost) {  // the next detect's listed items (HeavyArgs), on the grid's last lanes (idle: past the candidates)
+    const unsigned long long inear = hn.work[1], m = inear + hn.work[2];
+    const unsigned long long nt = (unsigned long long)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    for (unsigned long long k = nt - 1 - ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x); k < m; k += nt) {
+      const unsigned long long slot = k < inear ? k : hn.icap - 1 - (k - inear);
+      const unsigned cst = hn.cost[slot];
+      hn.cost[slot] = 0u;
+      const int tier = cst >= hn.thresh[0] ? 0 : (cst >= hn.thresh[1] ? 1 : 2);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const unsigned long long mk = __ballot(tier == q);
+        if (mk) {
+          const int lead = __ffsll((long long)mk) - 1;
+          unsigned base = 0;
+          if (lane == lead) base = atomicAdd(&hn.count[q], (unsigned)__popcll(mk));
+          base = (unsigned)__shfl((int)base, lead);
+          if (tier == q) {
+            hn.list[q][base + lane_prefix(mk)] = (unsigned)slot;
+            hn.flag[slot] = hn.epoch;
+          }
+        }
+      }
+    }
+  }
   if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
   if (rctl) {  // reuse: after a build this detect's state becomes the snapshot
     const bool built = rctl[0] != 0;
@@ -2626,6 +2710,34 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     c->trace_bytes = need;
   }
 #endif
+  // longest items first (HeavyArgs): detects of a kept tile-pair list only
+  // (Ctx::hv_us: the listing threshold, < 0 off)
+  HeavyArgs hv{};
+  HeavyNext hn{};
+  if (tpr && c->hv_us >= 0.0) {
+    const bool fresh = c->hv_icap != icap || !c->hv_cnt.p;
+    if (!ensure(c, c->hv_cost, icap * 4, "item costs") || !ensure(c, c->hv_flag, icap * 4, "listed item flags") ||
+        !ensure(c, c->hv_list[0], icap * 4, "listed items") || !ensure(c, c->hv_list[1], icap * 4, "listed items") ||
+        !ensure(c, c->hv_list[2], icap * 4, "listed items") || !ensure(c, c->hv_list[3], icap * 4, "listed items") ||
+        !ensure(c, c->hv_cnt, 64, "listed item counts"))
+      return -1;
+    if (fresh) {
+      BSA_HIP(c, hipMemsetAsync(c->hv_cost.p, 0, icap * 4, c->stream));
+      BSA_HIP(c, hipMemsetAsync(c->hv_flag.p, 0, icap * 4, c->stream));
+      BSA_HIP(c, hipMemsetAsync(c->hv_cnt.p, 0, 64, c->stream));
+      c->hv_icap = icap;
+    }
+    const unsigned E = ++c->hv_epoch;  // (flags hold epochs >= 1; 0 = never)
+    unsigned *cn = (unsigned *)c->hv_cnt.p;
+    const unsigned a = E & 1, b = (E + 1) & 1;  // this detect's / the next one's lists and counts
+    const double x = c->hv_x > 0.0 ? c->hv_x : 1e30;  // (tier 0 off: no slot reaches it)
+    hv = HeavyArgs{{(const unsigned *)c->hv_list[2 * a].p, (const unsigned *)c->hv_list[2 * a + 1].p}, cn + 2 * a,
+                   cn + 2 * b, (const unsigned *)c->hv_flag.p, (unsigned *)c->hv_cost.p, E};
+    hn = HeavyNext{(unsigned *)c->hv_cost.p, {(unsigned *)c->hv_list[2 * b].p, (unsigned *)c->hv_list[2 * b + 1].p},
+                   cn + 2 * b, (unsigned *)c->hv_flag.p, E + 1,
+                   {(unsigned)std::min(c->hv_us * x * 100.0, 4e9), (unsigned)std::min(c->hv_us * 100.0, 4e9)},
+                   (const unsigned long long *)c->workq.p, icap};
+  }
   // rows sharing the column records: row i is column roff + i (its diagonal)
   const int diag = shared ? (int)roff : -1;
   const unsigned pf_grid = (unsigned)std::max<long long>(
@@ -2635,13 +2747,14 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, TprArgs{});
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, TprArgs{},
+                       HeavyArgs{});
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, tp);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, tp, hv);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count of the
@@ -2661,7 +2774,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
                        (unsigned *)c->rowcnt.p, (uint2 *)c->kbuck.p, B,
                        reuse ? (unsigned *)c->reuse_ctl.p : nullptr,
-                       (const Snap *)c->snap_cur.p, (Snap *)c->snap_build.p, (int)n);
+                       (const Snap *)c->snap_cur.p, (Snap *)c->snap_build.p, (int)n, hn);
   }
   BSA_HIP(c, hipGetLastError());
   if (mark(3)) return -1;

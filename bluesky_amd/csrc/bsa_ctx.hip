@@ -293,6 +293,11 @@ bsa_ctx *bsa_create(int device) {
     return nullptr;
   }
   c->device = device;
+  // longest prefilter items first (bsa_cd.hip HeavyArgs): the listing
+  // threshold, or off (BSA_PF_HEAVY=0); results never depend on it
+  if (const char *v = getenv("BSA_PF_HEAVY_US")) c->hv_us = atof(v);
+  if (getenv("BSA_PF_HEAVY") && atoi(getenv("BSA_PF_HEAVY")) == 0) c->hv_us = -1.0;
+  if (const char *v = getenv("BSA_PF_HEAVY_X")) c->hv_x = atof(v);
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     bsa::fail(nullptr, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -315,7 +320,9 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->gbox_r, &c->gbox_c, &c->sbox_c, &c->workq, &c->workq2, &c->counters2, &c->rowcnt, &c->rowoff,
                         &c->cflag, &c->stats,
                         &c->tilepairs, &c->scan_ws, &c->snap_build, &c->snap_cur, &c->reuse_ctl, &c->reuse_use,
-                        &c->geo_in, &c->geo_pts, &c->geo_out, &c->wfield};
+                        &c->geo_in, &c->geo_pts, &c->geo_out, &c->wfield,
+                        &c->hv_cost, &c->hv_flag, &c->hv_list[0], &c->hv_list[1], &c->hv_list[2], &c->hv_list[3],
+                        &c->hv_cnt};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);
   bsa::feed_release(c);

@@ -213,6 +213,12 @@ struct Ctx {
   float tpr_dx = 3.2e-4f, tpr_ds = 1.6e-5f, tpr_dv = 300.f;  // ~2 km, ~100 m of reach, 300 m
   DevBuf tpr_snap;                     // PFRec per aircraft at the last build
   DevBuf tpr_ctl;                      // u64: [0] build flag, [1] near items, [2] far items, [3] builds, [4] detects
+  // longest items first (bsa_cd.hip HeavyArgs): per list slot cost / flag, two item lists and counts
+  DevBuf hv_cost, hv_flag, hv_list[4], hv_cnt;  // lists: [parity][tier]
+  unsigned long long hv_icap = 0;
+  unsigned hv_epoch = 0;
+  double hv_us = 16.0;                 // listing threshold [us] per item (BSA_PF_HEAVY_US at bsa_create; < 0: off)
+  double hv_x = 3.0;                   // ... x this: the top tier, twice the pieces (BSA_PF_HEAVY_X; <= 0: one tier)
 
   // detect timing: one set of 5 events per detect since the last reset
   std::vector<hipEvent_t> evpool;

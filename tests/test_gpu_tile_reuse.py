@@ -70,3 +70,25 @@ def test_tile_reuse_builds_rarely_at_the_bench_cadence(ctx):
     _, b0 = run(ctx, init, resident.params(simdt=1.0), 0, (1.0, 1.0))
     _, b = run(ctx, init, resident.params(simdt=1.0), 10, (1.0, 1.0))
     assert b['builds'] - b0['builds'] == b['detects'] - b0['detects'] == 9, b
+
+
+@pytest.mark.parametrize('us', ['0', '20', '1e9'])
+def test_longest_items_first_is_bitwise(monkeypatch, us):
+    """The prefilter's listed items ("longest items first"):
+    the slots whose units took longer than the threshold at the last detect
+    are swept first and skipped among the regular units.  Threshold 0 lists
+    every slot (each is swept once, as a listed item), 1e9 none: the state and
+    the pair lists are bitwise those of a run without tile-pair list reuse."""
+    monkeypatch.setenv('BSA_PF_HEAVY_US', us)
+    c = _lib.Context(0)
+    try:
+        t = synth.box(20000, 300.0, seed=109)
+        init = resident.initial_state(t)
+        p = resident.params(simdt=0.5, swresohoriz=False)
+        exp, _ = run(c, init, p, 12, None)
+        got, st = run(c, init, p, 12, (2016.0, 300.0))
+        same(got, exp)
+        assert sum(len(x[1]['ci']) for x in exp) > 0
+        assert st['detects'] >= 11
+    finally:
+        c.close()
