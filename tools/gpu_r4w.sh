@@ -1,0 +1,10 @@
+# K2 placing two pairs per lane per trip: parity (detect / sim / multirank / drop-in), then A/B vs base
+set -u
+OUT=gpurun_out/r4w
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+    tests/test_gpu_detect.py tests/test_gpu_sim.py tests/test_gpu_multirank.py tests/test_gpu_asas_dropin.py \
+    tests/test_gpu_trace.py tests/test_gpu_fullsize.py > $OUT/tests.log 2>&1
+rc=$?; tail -3 $OUT/tests.log; [ $rc -eq 0 ] || { grep -E "Error|FAILED|assert" $OUT/tests.log | head -20; exit $rc; }
+bash tools/gpu_ab2.sh libbsaccel_base.so libbsaccel.so 3
