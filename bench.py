@@ -273,8 +273,8 @@ def geo_matrix_line(ctx, t, m=8192):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=60)
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--n', type=int, default=100000)
     ap.add_argument('--workload', default='box100k', choices=['box10k', 'box100k', 'global1m'])
     ap.add_argument('--cd-every', type=int, default=1)

@@ -12,6 +12,8 @@ if [ "${PYTEST:-1}" = 1 ]; then
   rc=$?; echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log
   [ $rc -eq 0 ] || exit $rc
 fi
+# (PMC passes: 8 steps after 4 warm-up ones, so the prefilter's listed items
+# -- built from the previous detect -- are in steady state.)
 # The profiled runs skip the bench's secondary lines (--no-variants): their
 # gated / cadence-skipped launches would otherwise dilute the per-launch
 # averages of the headline workload's kernels.
@@ -24,10 +26,18 @@ for set in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_ACTIVE_INST_VALU"; do
   i=$((i+1))
   timeout -k 10 120 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/pmc_p$i -o run -- \
-      python bench.py --steps 3 --warmup 1 --no-cpu --no-variants > $OUT/pmc_p$i.log 2>&1
+      python bench.py --steps 8 --warmup 4 --no-cpu --no-variants > $OUT/pmc_p$i.log 2>&1
   rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python tools/pmc_roofline.py $OUT/pmc_latest.json $OUT/pmc_p1 $OUT/pmc_p2 $OUT/pmc_p3 $OUT/pmc_p4
 cp $OUT/pmc_latest.json profiles/pmc_latest.json
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err
-rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json
+rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; [ $rc -eq 0 ] || exit $rc
+if [ "${PROBE:-0}" = 1 ]; then  # the per-rank share of a sharded step
+  timeout -k 10 400 python -u tools/rowslice_probe.py box100k global1m > $OUT/rowslice_probe.log 2>&1
+  rc=$?; echo "rowslice rc=$rc"; cut -c1-300 $OUT/rowslice_probe.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/probe -o run --output-format csv -- \
+      python tools/probe_rank.py global1m 8 2 20 > $OUT/probe_rank.log 2>&1
+  rc=$?; echo "probe rc=$rc"; grep "per detect" $OUT/probe_rank.log; [ $rc -eq 0 ] || exit $rc
+  find $OUT/probe -name "*kernel_trace.csv" -size +4M -delete
+fi
