@@ -50,9 +50,9 @@ def prep_bytes_per_ac(n):
     return PREP_BYTES_PER_AC + (PREP_REC_BYTES if rec else 0)
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E (spec)
 PMC_JSON = os.path.join(REPO, 'profiles', 'pmc_latest.json')
-TIMING_SAMPLE = 10           # detects per HIP-event-timed detect (bsa_set_timing_sample; each timed one
-                             # costs ~24 us of event bubbles, profiles/r02 kernel trace: 2 of the default
-                             # 20 timed steps carry them)
+TIMING_SAMPLE = 20           # detects per HIP-event-timed detect (bsa_set_timing_sample; each timed one
+                             # costs ~24 us of event bubbles, profiles/r02 kernel trace: 3 of the default
+                             # 60 timed steps carry them, ~1.2 us per step)
 
 
 def pmc_figures(lib_sha):
