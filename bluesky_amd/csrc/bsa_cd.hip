@@ -1592,8 +1592,12 @@ constexpr int kPayStride = 6;  // doubles per candidate record (cpay): key, qdr,
 // mode: with all three paths in one body the register allocation covered the
 // union (205 VGPRs, 2 waves per SIMD)
 constexpr int kExactRec = 0, kExactKwik = 1, kExactHome = 2;
+// Stored-record modes at 3 waves per SIMD (139 VGPRs): at 4 the 128-VGPR cap
+// spilled 12 B per lane to scratch inside the fp64 chain, and the dense list's
+// ~2 400 working waves fit 3 per SIMD in one round anyway (box100k: 0.1394 ->
+// 0.1377 ms per step, A/B 4 x 60 steps)
 #ifndef BSA_EXACT_WAVES
-#define BSA_EXACT_WAVES 4
+#define BSA_EXACT_WAVES 3
 #endif
 #ifndef BSA_EXACT_HOME_WAVES
 #define BSA_EXACT_HOME_WAVES 2
