@@ -263,7 +263,9 @@ struct TprCheck {
 // names the aircraft (the resident sim): record k reads index k, coalesced.
 // Tiles: workgroup b prepares tile tile_base + b, or tile_list[b] (a halo
 // tile list of the row-sharded step, -1 = unused slot).
-__global__ __launch_bounds__(kTile) void k_prep_cols(int cnt, const unsigned *__restrict__ perm, int presorted, int rec,
+// (the waves-per-EU floors below keep the occupancy these kernels had before
+// the library's max-ilp scheduling, Makefile: it would trade it for ILP)
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(6))) void k_prep_cols(int cnt, const unsigned *__restrict__ perm, int presorted, int rec,
                                                      SoA6 own, SoA6 intr, int distinct, int shared,
                                                      double rpz, double hpz, double tla,
                                                      ColRec *__restrict__ C, PFRec *__restrict__ PC,
@@ -391,7 +393,7 @@ __device__ __forceinline__ bool list_word(int k) {
   return k == kCand || k == kTiles || k == kNear || k == kGroups || k >= kStamp;
 }
 
-__global__ __launch_bounds__(kTile) void k_boxes(int cnt, const PFRec *__restrict__ P,
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8))) void k_boxes(int cnt, const PFRec *__restrict__ P,
                                                  TileBox *__restrict__ sbox, TileBox *__restrict__ gbox,
                                                  TileBox *__restrict__ tbox, const unsigned *__restrict__ build,
                                                  Counters *__restrict__ reset) {
@@ -593,7 +595,7 @@ struct TprArgs {
 // 1954 tiles.  Every other tile is still tested against the row tile, without
 // an append: a kept pair with a tile the halo plan did not deliver sets
 // Counters::halo_miss (the step fails loudly), as the full sweep did.
-__global__ __launch_bounds__(kTPDirectThreads) void k_tilepairs_direct(
+__global__ __launch_bounds__(kTPDirectThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_tilepairs_direct(
     int nrt, int nct, int nrows, const TileBox *__restrict__ rb, const TileBox *__restrict__ rg,
     const TileBox *__restrict__ cb, int noprune, uint2 *__restrict__ out, unsigned long long cap,
     Counters *__restrict__ cnt, unsigned long long *__restrict__ icnt, const unsigned *__restrict__ build,

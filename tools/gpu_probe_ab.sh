@@ -1,7 +1,9 @@
-# Per-rank probe (global1m) of the current build against a reference build.
+# A/B of library builds on the per-rank probe (box100k rows of R ranks)
+# usage: bash tools/gpu_probe_ab.sh LIB_A LIB_B ...
 set -u
-mkdir -p gpurun_out/pab
-for L in ${LIBS:-libbsaccel.so libbsaccel_ref.so}; do
-  BSACCEL_LIB=$PWD/bluesky_amd/$L timeout -k 10 400 python tools/rowslice_probe.py ${WL:-global1m} > gpurun_out/pab/rs_$L.log 2>&1 || { tail -3 gpurun_out/pab/rs_$L.log; exit 1; }
-  echo "== $L"; cut -c1-200 gpurun_out/pab/rs_$L.log
+OUT=gpurun_out/pab
+mkdir -p $OUT
+for L in "$@"; do
+  BSACCEL_LIB=$PWD/bluesky_amd/$L timeout -k 10 200 python -u tools/rowslice_probe.py box100k > $OUT/rs_$L.log 2>&1 || { tail -3 $OUT/rs_$L.log; exit 1; }
+  echo "== $L"; cut -c1-140 $OUT/rs_$L.log
 done
