@@ -206,6 +206,44 @@ def halo_line(ctx, sim, cd_steps=None):
     return out
 
 
+PARITY_PAIR_KEYS = ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'li', 'lj', 'inconf', 'tcpamax')
+
+
+def parity_vs_world1(ctx, init, p, rank, world, device, steps=2, group=None):
+    """the first multi-GPU run checks itself.  Every rank
+    runs ``steps`` steps of the sharded sim (halo exchange over RCCL, or the
+    in-process group in tests); the state is all-gathered and the last CD
+    call's pairs are gathered to rank 0 (C2), which runs the same steps at
+    world 1 in a second context on its own GPU and compares both BITWISE
+    (every state array's bytes, every pair array).  Collective: every rank
+    learns the verdict (all-reduce), so a divergence stops every rank."""
+    import hashlib
+    sim = resident.ResidentSim(init, p, ctx=ctx, rank=rank, world=world, group=group)
+    sim.step(steps)
+    got = sim.read()                       # collective: the all-gathered state
+    gp = sim.gather_pairs(root=0)          # collective: rank-order pair blocks on rank 0
+    bad = []
+    out = dict(steps=steps, world=world)
+    if rank == 0:
+        c1 = _lib.Context(device)
+        try:
+            ref = resident.ResidentSim(init, p, ctx=c1)
+            ref.step(steps)
+            exp, st = ref.read(), ref.stats()
+            ep = c1.fetch_pairs(st['n_conf'], st['n_los'])
+        finally:
+            c1.close()
+        bad = [k for k in sorted(exp) if np.asarray(got[k]).tobytes() != np.asarray(exp[k]).tobytes()]
+        bad += ['pairs.' + k for k in PARITY_PAIR_KEYS if np.asarray(gp[k]).tobytes() != np.asarray(ep[k]).tobytes()]
+        h = hashlib.sha256()
+        for k in sorted(got):
+            h.update(np.ascontiguousarray(got[k]).tobytes())
+        out.update(state_sha256=h.hexdigest(), n_conf=len(ep['ci']), n_los=len(ep['li']), mismatched=bad)
+    flag = ctx.allreduce_max([1.0 if bad else 0.0])
+    out['ok'] = bool(flag[0] == 0.0)
+    return out
+
+
 def timed_steps(ctx, sim, warmup, steps):
     """Run warmup + steps resident sim steps; the timed batch's wall time, max over ranks."""
     sim.step(warmup)
@@ -284,6 +322,9 @@ def main():
                     help='candidate-list reuse budgets [m] (bsa_set_candidate_reuse); default off')
     ap.add_argument('--no-variants', action='store_true',
                     help='skip the secondary lines (reference CD cadence, candidate-list reuse)')
+    ap.add_argument('--parity-steps', type=int, default=2,
+                    help='with several GPUs: steps of the sharded run checked bitwise against one GPU first '
+                         '(0: skip)')
     args = ap.parse_args()
 
     rank, world, local = dist.env_rank_world()
@@ -297,6 +338,16 @@ def main():
         ctx.set_candidate_reuse(True, args.reuse[0], args.reuse[1])
     t = synth.workload(args.workload, n=args.n, seed=7)
     n = t.ntraf
+    parity = None
+    if world > 1 and args.parity_steps > 0:   # the sharded step equals one GPU's, bitwise, or nothing is timed
+        parity = parity_vs_world1(ctx, resident.initial_state(t), resident.params(cd_every=args.cd_every),
+                                  rank, world, local, steps=args.parity_steps)
+        if not parity['ok']:
+            if rank == 0:
+                print(json.dumps(dict(metric='CD pair-evals/s at 100k aircraft (GPU-resident sim step, ASAS every '
+                                             'step)', value=None, n_gpus=world, parity_vs_world1=False,
+                                      parity=parity, error='sharded run differs from one GPU')), flush=True)
+            sys.exit(3)
     sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=args.cd_every),
                                ctx=ctx, rank=rank, world=world)
 
@@ -389,7 +440,9 @@ def main():
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
                cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),
                propagation=propagation, exact_fp64=exact_fp64,
-               build=dict(lib_path=os.path.relpath(lib_path, REPO), lib_sha256=lib_sha))
+               build=dict(lib_path=os.path.relpath(lib_path, REPO), lib_sha256=lib_sha),
+               parity_vs_world1=None if parity is None else parity['ok'],
+               parity=parity)
     if world > 1:   # the halo exchange that replaced the full-state all-gather
         out['halo'] = halo_line(ctx, sim, cd_steps)
     if world > 1:   # C2: the last CD call's pair lists of all ranks to rank 0's host

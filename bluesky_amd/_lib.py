@@ -189,6 +189,7 @@ SIGNATURES.update({
     'bsa_sim_read_asas': (ctypes.c_int, [_vp, ctypes.POINTER(AsasOut)]),
     'bsa_sim_halo_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_set_halo_cap': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64]),
+    'bsa_sim_halo_recheck': (ctypes.c_int, [_vp]),
     'bsa_sim_comm_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_set_atmos': (ctypes.c_int, [_vp, ctypes.c_int]),
     'bsa_sim_read_atmos': (ctypes.c_int, [_vp, _c_dp, _c_dp, _c_dp]),
@@ -214,12 +215,22 @@ def load(path=None):
             lib = ctypes.CDLL(p)
         except OSError as e:
             raise AccelUnavailable('cannot load %s: %s' % (p, e))
+        skipped = []
         for name, (res, args) in SIGNATURES.items():
-            if p != os.path.join(_HERE, 'libbsaccel.so') and not hasattr(lib, name):
-                continue   # an older build selected with BSACCEL_LIB for an A/B measurement
+            if not hasattr(lib, name) and p != os.path.join(_HERE, 'libbsaccel.so') \
+                    and os.environ.get('BSACCEL_AB') == '1':
+                skipped.append(name)   # an older build selected for an A/B measurement
+                continue
+            if not hasattr(lib, name):
+                raise AccelUnavailable('%s lacks %s (stale build? set BSACCEL_AB=1 to load an older '
+                                       'build for an A/B measurement)' % (p, name))
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args
+        if skipped:
+            import sys
+            print('[bsaccel] %s: %d symbols missing (BSACCEL_AB=1): %s' % (p, len(skipped), ' '.join(skipped)),
+                  file=sys.stderr)
         v = lib.bsa_abi_version()
         if v != ABI_VERSION:
             raise AccelUnavailable('ABI mismatch: library %d, bindings %d' % (v, ABI_VERSION))
@@ -739,6 +750,10 @@ class Context:
         """bsa_sim_set_halo_cap (testing aid): this rank's copy of one tile capacity."""
         self.check(self.lib.bsa_sim_set_halo_cap(self.h, int(sender), int(receiver), int(tiles)),
                    'bsa_sim_set_halo_cap')
+
+    def sim_halo_recheck(self):
+        """bsa_sim_halo_recheck (collective): the next exchange re-checks the region layout."""
+        self.check(self.lib.bsa_sim_halo_recheck(self.h), 'bsa_sim_halo_recheck')
 
     def sim_asas_stats(self):
         """ASAS bookkeeping counts after the last CD call (resume_nav on); the

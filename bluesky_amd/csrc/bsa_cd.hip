@@ -1811,7 +1811,7 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
   if (t0 == 0) {
     unsigned long long pre[kCandShards + 1];
     (void)cand_prefix(cnt, cap, pre);
-    unsigned long long ncand = 0;  // candidates written (the shard counts include reserved, unused slots)
+    unsigned long long ncand = 0;  // candidates written (the prefilter's per-workgroup counts; the list is dense)
     for (int q = 0; q < 32; ++q) ncand += cnt->gpart[q][1];
     cnt->conf = ovf ? 0 : P;
     cnt->los = ovf ? 0 : L;
@@ -1990,7 +1990,7 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
     tl += wsum[1][q];
   }
   if (b == 0 && t == 0) {
-    unsigned long long ncand = 0;  // candidates written (the shard counts include reserved, unused slots)
+    unsigned long long ncand = 0;  // candidates written (the prefilter's per-workgroup counts; the list is dense)
     for (int q = 0; q < 32; ++q) ncand += cnt->gpart[q][1];
     cnt->conf = ovf ? 0 : P;
     cnt->los = ovf ? 0 : L;
@@ -2150,7 +2150,10 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
     MvpIn mv = ka.mv;
     mv.gate = sgate;
     const int k = rb + r;  // (rows = all aircraft: rb = 0)
-    if (ka.prep) {  // the wave's group boxes from its lanes' records (lanes past the rows too)
+    // the wave's group boxes from its lanes' records (lanes past nrows too, whose zeroed
+    // records reduce to nothing); waves past the block's rows (BSA_RANK_LANES_PER_ROW > 1)
+    // hold no rows and must not write a box (wave-uniform: kRankRows % 64 == 0)
+    if (ka.prep && rowlane) {
       PFRec pr{}, pb{};
       if (ka.pa.snap && live) pb = ka.pa.snap[k];
       if (live)
@@ -2891,7 +2894,7 @@ int detect_finish(Ctx *c, bool *retry) {
     worst = std::max(worst, h.cshard[q][0]);
     total += h.cshard[q][0];
   }
-  total = h.cand;  // (the shard counts include reserved, unused slots; K2 summed the written ones)
+  total = h.cand;  // (the list is dense: the shard counts equal the candidates written, K2 summed them)
   if (worst > c->cand_cap / kCandShards) {
     c->cand_cap = (unsigned long long)kCandShards * (worst + worst / 4 + 1024);
     c->reuse_valid = false;

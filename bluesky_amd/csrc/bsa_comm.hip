@@ -266,10 +266,48 @@ int comm_gatherv(Ctx *c, int root, const void *send, size_t bytes, void *recv, c
 // recv[roff[q], + rlen[q]); peer[q] = where that region starts in rank q's
 // send buffer (in-process group).  The lengths are agreed by all ranks (the
 // capacity matrix), so every send has its matching receive.
+// Region layout agreement of the halo exchange, collective (every rank calls
+// it at the same exchange: the trigger is a capacity generation / field count
+// that changes on every rank alike).  Each rank contributes what it will send
+// to every peer (length, offset in its buffer) and what it expects to receive
+// from every peer (length, offset in the peer's buffer); after one host
+// all-reduce(max) -- each entry is written by exactly one rank -- every rank
+// holds all four R x R matrices and fails, with the same message on every
+// rank, if any send disagrees with its receive.  RCCL's grouped send / recv
+// with unequal lengths hangs or truncates, so this runs BEFORE ncclGroupStart.
+static int halo_check_layout(Ctx *c, const size_t *soff, const size_t *slen, const size_t *rlen,
+                             const size_t *peer) {
+  const int R = c->nranks, me = c->rank;
+  const size_t RR = (size_t)R * R;
+  std::vector<double> v(4 * RR, 0.0);  // [send len][send off][expected len][expected off], [sender * R + receiver]
+  for (int q = 0; q < R; ++q) {
+    if (q == me) continue;
+    v[(size_t)me * R + q] = (double)slen[q];
+    v[RR + (size_t)me * R + q] = (double)soff[q];
+    v[2 * RR + (size_t)q * R + me] = (double)rlen[q];
+    v[3 * RR + (size_t)q * R + me] = (double)peer[q];
+  }
+  if (comm_allreduce_host(c, v.data(), (int)v.size(), true)) return -1;
+  for (int s = 0; s < R; ++s)
+    for (int q = 0; q < R; ++q) {
+      const size_t k = (size_t)s * R + q;
+      if (s == q) continue;
+      if (v[k] != v[2 * RR + k] || (v[k] != 0.0 && v[RR + k] != v[3 * RR + k]))
+        return fail(c, "halo lengths disagree: rank %d sends %.0f B at %.0f, rank %d expects %.0f B at %.0f", s,
+                    v[k], v[RR + k], q, v[2 * RR + k], v[3 * RR + k]);
+    }
+  return 0;
+}
+
 int comm_halo(Ctx *c, const void *send, const size_t *soff, const size_t *slen, size_t stot, void *recv,
               const size_t *roff, const size_t *rlen, const size_t *peer) {
   if (!comm_multi(c)) return 0;
   const int R = c->nranks, me = c->rank;
+  if (c->halo_chk_gen != c->halo_cap_gen || c->halo_chk_nf != c->halo_fields) {
+    if (halo_check_layout(c, soff, slen, rlen, peer)) return -1;
+    c->halo_chk_gen = c->halo_cap_gen;
+    c->halo_chk_nf = c->halo_fields;
+  }
   {
     size_t tx = 0, rx = 0;
     for (int q = 0; q < R; ++q)

@@ -477,7 +477,9 @@ int halo_init_caps(Ctx *c) {
     // (with plan reuse every plan is made on grown boxes: the capacities too)
     HaloTpr ht{c->tpr_on ? 1 : 0, 1, c->tpr_dx, c->tpr_ds, c->tpr_dv, nullptr, nullptr};
     if (ht.tpr) {
+      const bool fresh = !c->tpr_ctl.p;  // (ensure does not zero: the build / detect counters start at 0)
       if (!ensure(c, c->tpr_ctl, 64, "tile-pair list control")) return -1;
+      if (fresh) BSA_HIP(c, hipMemsetAsync(c->tpr_ctl.p, 0, 64, c->stream));
       ht.ctl = (unsigned long long *)c->tpr_ctl.p;
       ht.myflag = (unsigned *)(ht.ctl + 5);
     }
@@ -494,6 +496,7 @@ int halo_init_caps(Ctx *c) {
       int64_t &m = c->halo_cap[(size_t)sd * R + q];
       if (m) m = std::min<int64_t>(m + m / 4 + 2, tiles_of(c, sd));
     }
+  c->halo_cap_gen++;  // (every rank, bsa_sim_init): the next exchange re-checks the region layout
   return 0;
 }
 
@@ -524,7 +527,10 @@ int halo_grow(Ctx *c) {
         grew = true;
       }
     }
-  if (grew) c->halo_grows++;
+  if (grew) {
+    c->halo_grows++;
+    c->halo_cap_gen++;  // (collective: the same decision on every rank)
+  }
   return 0;
 }
 

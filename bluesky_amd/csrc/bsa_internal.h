@@ -309,6 +309,12 @@ struct Ctx {
   int64_t halo_grows = 0;          // capacity regrowths (aborted steps)
   int64_t halo_rx = 0, halo_tx = 0;  // bytes received / sent per CD step (the capacities' transfers)
   int halo_fields = 8;             // fp64 arrays per halo row of the last exchange (6 when derivable)
+  // region layout agreement (comm_halo): every rank's send lengths / offsets
+  // are compared with every receiver's expectation whenever the layout may have
+  // changed -- a new capacity generation (init, regrowth: collective events) or
+  // field count -- before any grouped send / recv is enqueued
+  int64_t halo_cap_gen = 0, halo_chk_gen = -1;
+  int halo_chk_nf = -1;
   int halo_tot_word = 0;           // h_dem word holding the last plan's received-tile total
 
   // 2-D wind field (bsa_set_windfield): lat lon vnorth veast of wf_nvec points

@@ -941,6 +941,13 @@ int bsa_sim_set_halo_cap(bsa_ctx *cc, int sender, int receiver, int64_t tiles) {
   return 0;
 }
 
+int bsa_sim_halo_recheck(bsa_ctx *cc) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  c->halo_chk_gen = -1;  // (collective by contract: every rank calls it before the same step)
+  return 0;
+}
+
 int bsa_sim_row_ids(bsa_ctx *cc, int32_t *ids) {
   Ctx *c = (Ctx *)cc;
   if (!c || !ids) return -1;

@@ -1,14 +1,21 @@
 """Row-sharded multi-GPU plumbing: one process per GPU.
 
-* ``row_range(n, rank, world)`` -- the contiguous ownship rows a rank owns
-  (same formula as bsa_sim_init: ceil(n / world) rows per rank).
+* ``home_range(n, rank, world)`` -- the contiguous range of HOME positions a
+  rank owns, exactly as bsa_sim_init partitions them (bsa_sim.hip): ``rpr`` =
+  ceil(n / world) rounded up to a whole 512-row tile, rank r owns
+  ``[r * rpr, min(n, (r + 1) * rpr))``.  Home positions are the spatial (home)
+  order of the initial traffic, so the aircraft a rank owns
+  are ``h2id[rb:re]`` -- not an index range; ``bsa_sim_row_ids`` lists them.
 * ``rendezvous_unique_id(rank, world)`` -- ships the 128-byte RCCL id from
   rank 0 to the other local ranks through a file in /tmp (single node, the
   driver's ``torch.distributed.run`` launch); no PyTorch is imported, so the
   process only ever loads /opt/rocm's HIP runtime and RCCL.
-* ``merge_rank_pairs(parts)`` -- the C2 pair gather: concatenating the row
-  shards' canonically ordered pair lists in rank order IS the reference's
-  global row-major order.
+* ``merge_rank_pairs(parts, rows)`` -- the C2 pair gather on the host: each
+  rank's pairs are row-major over ITS rows (aircraft-index order), and the rows
+  of different ranks interleave in index order, so the reference's global
+  row-major order (np.where, StateBasedCD.py:93-101) is the rank-order
+  concatenation stably sorted by row (what bsa_gather_pairs does on the root,
+  home_pairs_to_ids in bsa_ctx.hip).
 """
 import os
 import time
@@ -23,8 +30,13 @@ def env_rank_world():
     return rank, world, local
 
 
-def row_range(n, rank, world):
-    rpr = -(-n // world) if world > 0 else n
+HOME_TILE = 512   # kTile: a rank's home range is whole 512-row tiles (bsa_sim.hip, sim_rpr)
+
+
+def home_range(n, rank, world):
+    """Home positions [rb, re) of ``rank``: bsa_sim_init's partition."""
+    world = max(int(world), 1)
+    rpr = ((n + world - 1) // world + HOME_TILE - 1) // HOME_TILE * HOME_TILE
     rb = min(n, rank * rpr)
     return rb, min(n, rb + rpr)
 
@@ -81,10 +93,34 @@ def init_comm(ctx, rank, world):
     ctx.comm_rank_world = (rank, world)
 
 
-def merge_rank_pairs(parts):
-    """Concatenate per-rank detect outputs (dicts of arrays) in rank order."""
+PAIR_KEYS = {'ci': ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'dcpa'), 'li': ('li', 'lj')}
+
+
+def merge_rank_pairs(parts, rows=None):
+    """Merge per-rank detect outputs (dicts of arrays as fetch_pairs /
+    oracle detect_arrays return them, pairs row-major over the rank's rows)
+    into the global row-major result.  ``rows``: each rank's row ids (the
+    per-row arrays inconf / tcpamax are in that order); their union must be
+    every row once.  Pair arrays are concatenated in rank order and stably
+    sorted by row index (a row belongs to one rank, so its pairs stay in order)."""
     out = {}
-    for k in parts[0]:
-        vals = [p[k] for p in parts if p[k] is not None]
-        out[k] = np.concatenate(vals) if vals else None
+    for lead, keys in PAIR_KEYS.items():
+        if lead not in parts[0]:
+            continue
+        order = np.argsort(np.concatenate([p[lead] for p in parts]), kind='stable')
+        for k in keys:
+            if k in parts[0] and all(p.get(k) is not None for p in parts):
+                out[k] = np.concatenate([p[k] for p in parts])[order]
+    if rows is not None:
+        ids = np.concatenate([np.asarray(r, dtype=np.int64) for r in rows])
+        n = len(ids)
+        if not np.array_equal(np.sort(ids), np.arange(n)):
+            raise ValueError('rank rows do not partition 0..%d' % (n - 1))
+        for k in parts[0]:
+            if k in out or parts[0][k] is None or len(parts[0][k]) != len(rows[0]):
+                continue
+            v = np.concatenate([p[k] for p in parts])
+            full = np.empty(n, dtype=v.dtype)
+            full[ids] = v
+            out[k] = full
     return out

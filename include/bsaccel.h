@@ -486,6 +486,13 @@ int bsa_sim_comm_stats(bsa_ctx *ctx, int64_t *out3);
  * is caught on one GPU).  tiles >= 0; the next bsa_sim_init or regrowth
  * recomputes the capacities. */
 int bsa_sim_set_halo_cap(bsa_ctx *ctx, int sender, int receiver, int64_t tiles);
+/* Collective (every rank, before the same step): the next halo exchange
+ * re-checks the region layout on all ranks -- every send length / offset
+ * against its receiver's expectation, one host all-reduce -- as it does after
+ * bsa_sim_init and every capacity regrowth, before any RCCL send / recv is
+ * enqueued; a disagreement fails the step on every rank ("halo lengths
+ * disagree").  Testing aid with bsa_sim_set_halo_cap. */
+int bsa_sim_halo_recheck(bsa_ctx *ctx);
 /* ASAS bookkeeping after the last CD call (resume_nav = 1; replaces
  * ASAS.update's Python sets, asas.py:490-502):
  * [0] |resopairs| of this rank's rows, [1] |confpairs_unique|,

@@ -31,6 +31,22 @@ for set in "FETCH_SIZE" "WRITE_SIZE" \
 done
 python tools/pmc_roofline.py $OUT/pmc_latest.json $OUT/pmc_p1 $OUT/pmc_p2 $OUT/pmc_p3 $OUT/pmc_p4
 cp $OUT/pmc_latest.json profiles/pmc_latest.json
+# K4' on its own (BSA_K24=0: K2 and K4' as two launches): the propagation
+# kernel's standalone duration and HBM bytes, which the fused default launch
+# only bounds (VERDICT r04 missing #3); same passes, kernel-trace only
+if [ "${K24PASS:-1}" = 1 ]; then
+  timeout -k 10 300 env BSA_K24=0 rocprofv3 --kernel-trace --stats -d $OUT/k24off_stats -o run --output-format csv -- \
+      python bench.py --steps 20 --warmup 3 --no-cpu --no-variants > $OUT/k24off_stats.log 2>&1
+  rc=$?; echo "k24=0 stats rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  j=0
+  for set in "FETCH_SIZE" "WRITE_SIZE"; do
+    j=$((j+1))
+    BSA_K24=0 timeout -k 10 120 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $OUT/k24off_p$j -o run -- \
+        python bench.py --steps 8 --warmup 4 --no-cpu --no-variants > $OUT/k24off_p$j.log 2>&1
+    rc=$?; echo "k24=0 pmc pass $j rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+  python tools/pmc_roofline.py $OUT/pmc_k24off.json $OUT/k24off_p1 $OUT/k24off_p2
+fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; [ $rc -eq 0 ] || exit $rc
 if [ "${PROBE:-0}" = 1 ]; then  # the per-rank share of a sharded step
