@@ -190,6 +190,8 @@ SIGNATURES.update({
     'bsa_sim_halo_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_set_halo_cap': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64]),
     'bsa_sim_halo_recheck': (ctypes.c_int, [_vp]),
+    'bsa_set_exact_fusion': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    'bsa_exact_fusion_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_comm_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_set_atmos': (ctypes.c_int, [_vp, ctypes.c_int]),
     'bsa_sim_read_atmos': (ctypes.c_int, [_vp, _c_dp, _c_dp, _c_dp]),
@@ -750,6 +752,17 @@ class Context:
         """bsa_sim_set_halo_cap (testing aid): this rank's copy of one tile capacity."""
         self.check(self.lib.bsa_sim_set_halo_cap(self.h, int(sender), int(receiver), int(tiles)),
                    'bsa_sim_set_halo_cap')
+
+    def set_exact_fusion(self, on=True, max_records=64):
+        """bsa_set_exact_fusion: K1b fused into the prefilter (default on); max_records < 64
+        only to exercise the unfused retry in tests."""
+        self.check(self.lib.bsa_set_exact_fusion(self.h, int(bool(on)), int(max_records)), 'bsa_set_exact_fusion')
+
+    def exact_fusion_stats(self):
+        """bsa_exact_fusion_stats: fused detects, their unfused retries, whether the last one fused."""
+        v = np.zeros(3, np.int64)
+        self.check(self.lib.bsa_exact_fusion_stats(self.h, ptr(v, _c_i64p)), 'bsa_exact_fusion_stats')
+        return dict(fused=int(v[0]), retries=int(v[1]), last=bool(v[2]))
 
     def sim_halo_recheck(self):
         """bsa_sim_halo_recheck (collective): the next exchange re-checks the region layout."""

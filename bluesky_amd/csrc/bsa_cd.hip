@@ -695,6 +695,133 @@ __device__ __forceinline__ unsigned lane_prefix(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
+// ------------------------------------------------------------------ K1b pair math (also fused into K1a)
+struct PairResult {
+  bool conf, los;
+  double qdr, dist, tcpa, tin, dcpa;
+};
+
+// One (i, j) entry of StateBasedCD.detect + geo.qdrdist_matrix, i != j.
+// KWIK (opt-in variant, BSA_FLAG_KWIK): geo.kwikqdrdist_matrix (geo.py:347-363)
+// replaces qdrdist_matrix, its metre distance handed over in nm (/ nm) so that
+// StateBasedCD.py:22's `* nm` restores metres -- the reference's own detect
+// with the geo function swapped (tools/make_golden.py captures exactly that).
+template <bool KWIK>
+__device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c, double rpz,
+                                                double hpz, double tla) {
+  PairResult o;
+  double qdr, dist_nm;
+  if (KWIK) {
+    // geo.kwikqdrdist_matrix [i, j]: cavelat at lata[j] + latb[i] (geo.py:355)
+    double dist_m;
+    kwik_entry(r.lat, r.lon, c.lat, c.lon, c.olat + r.ilat, qdr, dist_m);
+    dist_nm = dist_m / kNM;
+  } else {
+    // geo.qdrdist_matrix (geo.py:118-160)
+    qdrdist_entry(r.lat, r.lon, r.sinlat, r.coslat, r.hemA, c.lat, c.lon, c.sinlat, c.coslat, c.hemA,
+                  c.eps, qdr, dist_nm);
+  }
+
+  // ---- StateBasedCD.detect (StateBasedCD.py:22-83), off-diagonal entry
+  const double dist = dist_nm * kNM + 0.0;
+  const double qdrrad = qdr * kD2R;
+  const double dx = dist * sin(qdrrad);
+  const double dy = dist * cos(qdrrad);
+  const double du = c.u - r.u;  // own.u[j] - int.u[i]
+  const double dv = c.v - r.v;
+  double dv2 = du * du + dv * dv;
+  dv2 = (fabs(dv2) < 1e-6) ? 1e-6 : dv2;
+  const double vrel = sqrt(dv2);
+  const double tcpa = -(du * dx + dv * dy) / dv2 + 0.0;
+  const double dcpa2 = dist * dist - tcpa * tcpa * dv2;
+  const double R2 = rpz * rpz;
+  const bool swhorconf = dcpa2 < R2;
+  const double dxinhor = sqrt(np_max(0., R2 - dcpa2));
+  const double dtinhor = dxinhor / vrel;
+  const double tinhor = swhorconf ? tcpa - dtinhor : 1e8;
+  const double touthor = swhorconf ? tcpa + dtinhor : -1e8;
+  const double dalt = c.alt - r.alt + 0.0;  // own.alt[j] - int.alt[i]
+  double dvs = c.vs - r.vs;
+  dvs = (fabs(dvs) < 1e-6) ? 1e-6 : dvs;
+  const double tcrosshi = (dalt + hpz) / -dvs;
+  const double tcrosslo = (dalt - hpz) / -dvs;
+  const double tinver = np_min(tcrosshi, tcrosslo);
+  const double toutver = np_max(tcrosshi, tcrosslo);
+  const double tinconf = np_max(tinver, tinhor);
+  const double toutconf = np_min(toutver, touthor);
+  o.conf = swhorconf && (tinconf <= toutconf) && (toutconf > 0.0) && (tinconf < tla);
+  o.los = (dist < rpz) && (fabs(dalt) < hpz);  // StateBasedCD.py:94
+  o.qdr = qdr;
+  o.dist = dist;
+  o.tcpa = tcpa;
+  o.tin = tinconf;
+  o.dcpa = sqrt(np_max(dcpa2, 0.0));
+  return o;
+}
+
+constexpr int kPayStride = 6;  // doubles per candidate record (cpay): key, qdr, dist, tcpa, tin, dcpa
+
+// The outputs of one evaluated candidate with row buckets (B > 0; K1b and the
+// fused pass below): a conflict's 48-B record (word 0 = the column's sorted
+// position, so K2's fused MVP reads the intruder's state without an id2h
+// lookup) and the pair's (column, candidate) entry in its row's conflict /
+// LoS bucket, at the slot the row count's atomic returns (a full bucket raises
+// k2_demand: the detect is retried with wider buckets)
+__device__ __forceinline__ void exact_bucket(const PairResult &o, int row, unsigned oj, unsigned py,
+                                             unsigned long long id, int nrows, int B, double *__restrict__ cpay,
+                                             unsigned *__restrict__ rowcnt, uint2 *__restrict__ kb,
+                                             Counters *__restrict__ cnt) {
+  if (o.conf) {
+    double *rec = cpay + id * kPayStride;
+    rec[0] = __longlong_as_double((long long)py);
+    rec[1] = o.qdr;
+    rec[2] = o.dist;
+    rec[3] = o.tcpa;
+    rec[4] = o.tin;
+    rec[5] = o.dcpa;
+    const unsigned s = atomicAdd(&rowcnt[row], 1u);
+    if (s < (unsigned)B) kb[(size_t)row * B + s] = make_uint2(oj, (unsigned)id);
+    else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
+  }
+  if (o.los) {
+    const unsigned s = atomicAdd(&rowcnt[nrows + 1 + row], 1u);
+    if (s < (unsigned)B) kb[((size_t)nrows + row) * B + s] = make_uint2(oj, (unsigned)id);
+    else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
+  }
+}
+
+// K1b fused into the prefilter (stored fp64 records, row
+// buckets, not KWIK / candidate reuse): each prefilter workgroup evaluates the
+// candidates it appended at the end of its sweep (they sit in its LDS stages),
+// and the blocks its waves flushed mid-sweep (a full stage; recorded in LDS).
+// A candidate's id (its cpay record, its
+// bucket entries) is its slot in the candidate array, shard * ccap + position,
+// not K1b's flat index -- K2 reads only what the buckets name.  The candidate
+// list, every record and every bucket come out exactly as with K1b's launch
+// (the list's order differs, which nothing downstream depends on: K2 ranks
+// each row's bucket by column).  R == NULL: K1b runs as its own launch.
+struct ExactFuse {
+  const RowRec *R;                 // row records (the column records + roff when shared)
+  const ColRec *C;                 // column records (sorted / home order)
+  const unsigned *perm_r, *perm_c;  // sorted position -> index (perm_r NULL: home rows rb + x)
+  double rpz, hpz, tla;
+  int rb, nrows, B;
+  double *cpay;
+  unsigned *rowcnt;
+  uint2 *kb;
+  unsigned nrec;                   // flush records per wave (<= kFuseRecs; bsa_set_exact_fusion)
+};
+
+// One candidate p = (row, sorted column) at slot id: K1b's work for it.
+__device__ __forceinline__ void fuse_exact_one(const ExactFuse &xf, uint2 p, unsigned long long id,
+                                               Counters *__restrict__ cnt) {
+  const unsigned oi = xf.perm_r ? xf.perm_r[p.x] : (unsigned)xf.rb + p.x, oj = xf.perm_c[p.y];
+  if (xf.perm_r ? oi == oj : oi == p.y) return;  // an aircraft against itself (never a pair)
+  const PairResult o = eval_pair<false>(xf.R[p.x], xf.C[p.y], xf.rpz, xf.hpz, xf.tla);
+  exact_bucket(o, (int)oi - xf.rb, oj, p.y, id, xf.nrows, xf.B, xf.cpay, xf.rowcnt, xf.kb, cnt);
+}
+
+
 // ------------------------------------------------------------------ K1a prefilter
 constexpr int PF_BLOCK = 256;
 constexpr int PF_WAVES = PF_BLOCK / 64;
@@ -789,6 +916,10 @@ __device__ __forceinline__ bool pf_refine(const float4 &rp, const float4 &rv, co
 #define PF_RES 128
 #endif
 constexpr int PF_WROWS = 64;   // rows per wave (one per lane)
+// fused K1b: mid-sweep flushes a wave can record for the end of its
+// workgroup's sweep (each holds >= 65 candidates: >= 4 160 per wave; more sets
+// Counters::fuse_ovf and the detect is retried with K1b's own launch)
+constexpr int kFuseRecs = kFuseRecsMax;
 constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 // Work distribution knob of the sweep (BSA_PF_SHARDS overrides it for
 // measurements; results never depend on it)
@@ -898,7 +1029,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     Counters *__restrict__ cnt,
     unsigned long long *__restrict__ work, RefineParams prm,
     uint2 *__restrict__ cand, unsigned long long cap, const unsigned *__restrict__ build, PfKnobs kn, int diag,
-    TprArgs tp, HeavyArgs hv) {
+    TprArgs tp, HeavyArgs hv, ExactFuse xf) {
   __shared__ unsigned short q1s[PF_WAVES][PF_Q1];
   __shared__ float4 cka[PF_WAVES][32];      // staged column pairs: k k' s s'     (stage 1)
   __shared__ float4 cen[PF_WAVES][32];      //                      e e' n n'     (stage 1)
@@ -994,6 +1125,9 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   uint2 *stg = cst[w];
   unsigned nst = 0;
   unsigned nemit = 0;  // candidates this wave wrote (statistics)
+  // fused K1b: the blocks this wave flushed mid-sweep, {position, count} (wave-uniform count)
+  __shared__ uint2 xrc[PF_WAVES][kFuseRecs];
+  unsigned nxr = 0;
   auto flush_stage = [&]() {
     __builtin_amdgcn_wave_barrier();
     unsigned long long r = 0;
@@ -1001,6 +1135,13 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     const unsigned nb = __builtin_amdgcn_readfirstlane((unsigned)r);
     for (unsigned k = lane; k < nst; k += 64)
       if (nb + k < ccap32) ccand[nb + k] = stg[k];
+    if (xf.R) {  // fused K1b: the block is evaluated at the end of the workgroup's sweep
+      if (lane == 0) {
+        if (nxr < xf.nrec) xrc[w][nxr] = make_uint2(nb, nst);
+        else cnt->fuse_ovf = 1ull;  // (the detect is retried with K1b as its own launch)
+      }
+      ++nxr;
+    }
     nst = 0;
     __builtin_amdgcn_wave_barrier();
   };
@@ -1351,12 +1492,13 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // and the roofline's sub-group count: one atomic per workgroup, spread over
   // 32 lines (4096 waves adding to one word serialised at ~12 ns each, ~50 us
   // of the sweep's tail when the waves finish together)
-  __shared__ unsigned wsubs[PF_WAVES], wcand[PF_WAVES], wst[PF_WAVES];
+  __shared__ unsigned wsubs[PF_WAVES], wcand[PF_WAVES], wst[PF_WAVES], wxr[PF_WAVES];
   __shared__ unsigned wbase;
   if (lane == 0) {
     wsubs[w] = subs;
     wcand[w] = nemit;
     wst[w] = nst;
+    wxr[w] = min(nxr, xf.nrec);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1369,11 +1511,29 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     wbase = ts ? (unsigned)atomicAdd(cshard, (unsigned long long)ts) : 0u;
   }
   __syncthreads();
-  {
+  if (!xf.R) {  // (fused K1b: nothing reads the final candidates back from the list)
     unsigned o = wbase;
     for (int q = 0; q < w; ++q) o += wst[q];
     for (unsigned k = lane; k < nst; k += 64)
       if (o + k < ccap32) ccand[o + k] = stg[k];
+  } else {  // fused K1b (ExactFuse)
+    // the workgroup's own final candidates [wbase, wbase + ts) of its shard,
+    // from its waves' LDS stages (all 256 lanes: ~150 candidates at the 100k box)
+    const unsigned o1 = wst[0], o2 = o1 + wst[1], o3 = o2 + wst[2], ts = o3 + wst[3];
+    const unsigned long long sbase = (unsigned long long)(shard % kCandShards) * ccap;
+    for (unsigned k = threadIdx.x; k < ts; k += PF_BLOCK) {
+      const int q = (k >= o1) + (k >= o2) + (k >= o3);
+      const unsigned kq = k - (q == 0 ? 0u : (q == 1 ? o1 : (q == 2 ? o2 : o3)));
+      if (wbase + k < ccap32) fuse_exact_one(xf, cst[q][kq], sbase + wbase + k, cnt);
+    }
+    // ... and the blocks its waves flushed mid-sweep (written to the list by
+    // this workgroup, visible to it after the barrier above)
+    for (int q = 0; q < PF_WAVES; ++q)
+      for (unsigned r = 0; r < wxr[q]; ++r) {
+        const uint2 bk = xrc[q][r];
+        for (unsigned k = threadIdx.x; k < bk.y; k += PF_BLOCK)
+          if (bk.x + k < ccap32) fuse_exact_one(xf, ccand[bk.x + k], sbase + bk.x + k, cnt);
+      }
   }
 #ifdef BSA_PF_STAMPS
   PF_STAMP(3);
@@ -1514,76 +1674,42 @@ __device__ __forceinline__ bool cand_overflow(const Counters *cnt, unsigned long
   const unsigned long long ccap = cap / kCandShards;
   bool o = cnt->k2_demand != 0;  // a K2 row bucket was full: retried with wider buckets
   o |= cnt->halo_ovf != 0 || cnt->halo_miss != 0;  // halo tiles missing: the step is re-run
+  o |= cnt->fuse_ovf != 0;  // fused K1b out of flush records: re-run with K1b's own launch
 #pragma unroll
   for (int q = 0; q < kCandShards; ++q) o |= cnt->cshard[q][0] > ccap;
   return o;
 }
 
 
-struct PairResult {
-  bool conf, los;
-  double qdr, dist, tcpa, tin, dcpa;
-};
-
-// One (i, j) entry of StateBasedCD.detect + geo.qdrdist_matrix, i != j.
-// KWIK (opt-in variant, BSA_FLAG_KWIK): geo.kwikqdrdist_matrix (geo.py:347-363)
-// replaces qdrdist_matrix, its metre distance handed over in nm (/ nm) so that
-// StateBasedCD.py:22's `* nm` restores metres -- the reference's own detect
-// with the geo function swapped (tools/make_golden.py captures exactly that).
-template <bool KWIK>
-__device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c, double rpz,
-                                                double hpz, double tla) {
-  PairResult o;
-  double qdr, dist_nm;
-  if (KWIK) {
-    // geo.kwikqdrdist_matrix [i, j]: cavelat at lata[j] + latb[i] (geo.py:355)
-    double dist_m;
-    kwik_entry(r.lat, r.lon, c.lat, c.lon, c.olat + r.ilat, qdr, dist_m);
-    dist_nm = dist_m / kNM;
-  } else {
-    // geo.qdrdist_matrix (geo.py:118-160)
-    qdrdist_entry(r.lat, r.lon, r.sinlat, r.coslat, r.hemA, c.lat, c.lon, c.sinlat, c.coslat, c.hemA,
-                  c.eps, qdr, dist_nm);
+// The next detect's listed items (HeavyArgs): every item whose units took at
+// least a threshold is listed (two tiers), its cost word zeroed.  Runs on the
+// grid's last lanes (K1b: the lanes past the candidate count; k_rowblk when K1b
+// is fused into the prefilter).  Wave-uniform per loop trip.
+__device__ __forceinline__ void heavy_next(const HeavyNext &hn) {
+  const unsigned long long inear = hn.work[1], m = inear + hn.work[2];
+  const unsigned long long nt = (unsigned long long)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  for (unsigned long long k = nt - 1 - ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x); k < m; k += nt) {
+    const unsigned long long slot = k < inear ? k : hn.icap - 1 - (k - inear);
+    const unsigned cst = hn.cost[slot];
+    hn.cost[slot] = 0u;
+    const int tier = cst >= hn.thresh[0] ? 0 : (cst >= hn.thresh[1] ? 1 : 2);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const unsigned long long mk = __ballot(tier == q);
+      if (mk) {
+        const int lead = __ffsll((long long)mk) - 1;
+        unsigned base = 0;
+        if (lane == lead) base = atomicAdd(&hn.count[q], (unsigned)__popcll(mk));
+        base = (unsigned)__shfl((int)base, lead);
+        if (tier == q) {
+          hn.list[q][base + lane_prefix(mk)] = (unsigned)slot;
+          hn.flag[slot] = hn.epoch;
+        }
+      }
+    }
   }
-
-  // ---- StateBasedCD.detect (StateBasedCD.py:22-83), off-diagonal entry
-  const double dist = dist_nm * kNM + 0.0;
-  const double qdrrad = qdr * kD2R;
-  const double dx = dist * sin(qdrrad);
-  const double dy = dist * cos(qdrrad);
-  const double du = c.u - r.u;  // own.u[j] - int.u[i]
-  const double dv = c.v - r.v;
-  double dv2 = du * du + dv * dv;
-  dv2 = (fabs(dv2) < 1e-6) ? 1e-6 : dv2;
-  const double vrel = sqrt(dv2);
-  const double tcpa = -(du * dx + dv * dy) / dv2 + 0.0;
-  const double dcpa2 = dist * dist - tcpa * tcpa * dv2;
-  const double R2 = rpz * rpz;
-  const bool swhorconf = dcpa2 < R2;
-  const double dxinhor = sqrt(np_max(0., R2 - dcpa2));
-  const double dtinhor = dxinhor / vrel;
-  const double tinhor = swhorconf ? tcpa - dtinhor : 1e8;
-  const double touthor = swhorconf ? tcpa + dtinhor : -1e8;
-  const double dalt = c.alt - r.alt + 0.0;  // own.alt[j] - int.alt[i]
-  double dvs = c.vs - r.vs;
-  dvs = (fabs(dvs) < 1e-6) ? 1e-6 : dvs;
-  const double tcrosshi = (dalt + hpz) / -dvs;
-  const double tcrosslo = (dalt - hpz) / -dvs;
-  const double tinver = np_min(tcrosshi, tcrosslo);
-  const double toutver = np_max(tcrosshi, tcrosslo);
-  const double tinconf = np_max(tinver, tinhor);
-  const double toutconf = np_min(toutver, touthor);
-  o.conf = swhorconf && (tinconf <= toutconf) && (toutconf > 0.0) && (tinconf < tla);
-  o.los = (dist < rpz) && (fabs(dalt) < hpz);  // StateBasedCD.py:94
-  o.qdr = qdr;
-  o.dist = dist;
-  o.tcpa = tcpa;
-  o.tin = tinconf;
-  o.dcpa = sqrt(np_max(dcpa2, 0.0));
-  return o;
 }
-
-constexpr int kPayStride = 6;  // doubles per candidate record (cpay): key, qdr, dist, tcpa, tin, dcpa
 
 // Results are stored per candidate (flag, key, payload) rather than appended
 // to a shared list: appending needs an atomic with return on ONE counter per
@@ -1615,31 +1741,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
     int B,
     unsigned *__restrict__ rctl, const Snap *__restrict__ snap_cur, Snap *__restrict__ snap_build, int nsnap,
     HeavyNext hn) {
-  if (hn.cost) {  // the next detect's listed items (HeavyArgs), on the grid's last lanes (idle: past the candidates)
-    const unsigned long long inear = hn.work[1], m = inear + hn.work[2];
-    const unsigned long long nt = (unsigned long long)gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    for (unsigned long long k = nt - 1 - ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x); k < m; k += nt) {
-      const unsigned long long slot = k < inear ? k : hn.icap - 1 - (k - inear);
-      const unsigned cst = hn.cost[slot];
-      hn.cost[slot] = 0u;
-      const int tier = cst >= hn.thresh[0] ? 0 : (cst >= hn.thresh[1] ? 1 : 2);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const unsigned long long mk = __ballot(tier == q);
-        if (mk) {
-          const int lead = __ffsll((long long)mk) - 1;
-          unsigned base = 0;
-          if (lane == lead) base = atomicAdd(&hn.count[q], (unsigned)__popcll(mk));
-          base = (unsigned)__shfl((int)base, lead);
-          if (tier == q) {
-            hn.list[q][base + lane_prefix(mk)] = (unsigned)slot;
-            hn.flag[slot] = hn.epoch;
-          }
-        }
-      }
-    }
-  }
+  if (hn.cost) heavy_next(hn);  // the next detect's listed items, on the grid's last lanes (idle: past the candidates)
   if (cand_overflow(cnt, cap)) return;  // the caller retries with more room
   if (rctl) {  // reuse: after a build this detect's state becomes the snapshot
     const bool built = rctl[0] != 0;
@@ -1694,41 +1796,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kEx
 #endif
         flag = (o.conf ? 1 : 0) | (o.los ? 2 : 0);
         row = (int)oi - rb;
-        // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
-        double *rec = cpay + idx * kPayStride;
-        if (flag && !B) rec[0] = __longlong_as_double((long long)(((unsigned long long)oi << 32) | oj));
-        // row buckets: word 0 carries the column's sorted (home) position, so
-        // K2's fused MVP reads the intruder's state without an id2h lookup
-        if (o.conf && B) rec[0] = __longlong_as_double((long long)p.y);
-        if (o.conf) {
-          rec[1] = o.qdr;
-          rec[2] = o.dist;
-          rec[3] = o.tcpa;
-          rec[4] = o.tin;
-          rec[5] = o.dcpa;
-          if (!B) {  // (row buckets: k_rank_rows writes both per row)
+        if (B) {  // row buckets (k_rank_rows writes inconf / tcpamax per row)
+          exact_bucket(o, row, oj, p.y, idx, nrows, B, cpay, rowcnt, kb, cnt);
+        } else {
+          // one 48-B record per candidate: key | qdr dist tcpa tin dcpa (conflicts)
+          double *rec = cpay + idx * kPayStride;
+          if (flag) rec[0] = __longlong_as_double((long long)(((unsigned long long)oi << 32) | oj));
+          if (o.conf) {
+            rec[1] = o.qdr;
+            rec[2] = o.dist;
+            rec[3] = o.tcpa;
+            rec[4] = o.tin;
+            rec[5] = o.dcpa;
             inconf[row] = 1;
             // tcpamax = max_j(tcpa * swconfl) >= +-0 (StateBasedCD.py:90): only
             // positive tcpa can raise it, and positive doubles order as integers.
             if (o.tcpa > 0.0)
               atomicMax(&tcpamax_bits[row], (unsigned long long)__double_as_longlong(o.tcpa));
-          }
-          if (B) {  // row bucket: (column, candidate) at the slot its count returned
-            const unsigned s = atomicAdd(&rowcnt[row], 1u);
-            if (s < (unsigned)B) kb[(size_t)row * B + s] = make_uint2(oj, (unsigned)idx);
-            else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
-          } else {
             atomicAdd(&rowcnt[row], 1u);
           }
-        }
-        if (o.los) {
-          if (B) {
-            const unsigned s = atomicAdd(&rowcnt[nrows + 1 + row], 1u);
-            if (s < (unsigned)B) kb[((size_t)nrows + row) * B + s] = make_uint2(oj, (unsigned)idx);
-            else atomicMax(&cnt->k2_demand, (unsigned long long)s + 1);
-          } else {
-            atomicAdd(&rowcnt[nrows + 1 + row], 1u);
-          }
+          if (o.los) atomicAdd(&rowcnt[nrows + 1 + row], 1u);
         }
       }
     }
@@ -1893,8 +1980,14 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
 // per-row counts: bcnt[b], bcnt[nb + b]); one wave per block, kRankRows / 64
 // rows per lane (one load round trip; an overflowed detect's sums are never
 // read: k_rank_rows checks the overflow itself)
-__global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__ rowcnt) {
+constexpr unsigned kHeavyBlocks = 1024;  // k_rowblk's extra one-wave blocks for the heavy-item listing
+__global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__ rowcnt, HeavyNext hn) {
+  // (K1b fused into the prefilter: the next detect's listed items here, on
+  // every lane of the grid -- the host adds kHeavyBlocks blocks past the nb
+  // row blocks for them, ~1 slot per lane at the 100k box)
+  if (hn.cost) heavy_next(hn);
   const int nb = rank_blocks(nrows), b = blockIdx.x, lane = threadIdx.x;
+  if (b >= nb) return;
   unsigned c = 0, l = 0;
 #pragma unroll
   for (int q = 0; q < kRankRows / 64; ++q) {
@@ -2747,6 +2840,20 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                    {(unsigned)std::min(c->hv_us * x * 100.0, 4e9), (unsigned)std::min(c->hv_us * 100.0, 4e9)},
                    (const unsigned long long *)c->workq.p, icap};
   }
+  // K2 row buckets (B pairs per row per list; a fuller row retries wider, then without)
+  const int B = c->k2_bucket;
+  if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * sizeof(uint2), "K2 row buckets")) return -1;
+  // K1b fused into the prefilter (ExactFuse): stored records, row buckets, no
+  // KWIK / candidate reuse (BSA_FUSE_EXACT=0: K1b as its own launch, for A/B)
+  static const bool fuse_env = !(getenv("BSA_FUSE_EXACT") && atoi(getenv("BSA_FUSE_EXACT")) == 0);
+  const bool fuse = fuse_env && c->fuse_on && !c->fuse_skip && B > 0 && recs && !kwik && !reuse;
+  c->fuse_skip = false;  // (one retry unfused; the next detect fuses again)
+  ExactFuse xf{};
+  if (fuse)
+    xf = ExactFuse{rowrec, (const ColRec *)c->colrec.p, perm_r, perm_c, rpz, hpz, tla, (int)rb, (int)nrows, B,
+                   (double *)c->cpay.p, (unsigned *)c->rowcnt.p, (uint2 *)c->kbuck.p, (unsigned)c->fuse_recs};
+  c->last_fused = fuse;
+  if (fuse) c->fuse_count++;
   // rows sharing the column records: row i is column roff + i (its diagonal)
   const int diag = shared ? (int)roff : -1;
   const unsigned pf_grid = (unsigned)std::max<long long>(
@@ -2757,23 +2864,20 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, TprArgs{},
-                       HeavyArgs{});
+                       HeavyArgs{}, xf);
   else
     hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
                        (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
                        (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
                        (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, tp, hv);
+                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, tp, hv, xf);
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count of the
   // dense candidate list; 2048 workgroups (524 k lanes: the 100k box's ~153 k
   // candidates in one stride, the workgroups past the count exit at once;
   // BSA_K1B_GRID overrides for A/B)
-  // K2 row buckets (B pairs per row per list; a fuller row retries wider, then without)
-  const int B = c->k2_bucket;
-  if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * sizeof(uint2), "K2 row buckets")) return -1;
-  {
+  if (!fuse) {
     const auto KEX = !recs ? k_exact<kExactHome> : (kwik ? k_exact<kExactKwik> : k_exact<kExactRec>);
     static const int k1b_grid = getenv("BSA_K1B_GRID") ? atoi(getenv("BSA_K1B_GRID")) : 0;
     hipLaunchKernelGGL(KEX, dim3(k1b_grid > 0 ? (unsigned)k1b_grid : 256u * 8u), dim3(256), 0, c->stream, rowrec, (const ColRec *)c->colrec.p,
@@ -2820,8 +2924,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     }
   }
   if (B) {
-    hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows)), dim3(64), 0, c->stream, (int)nrows,
-                       (unsigned *)c->rowcnt.p);
+    const bool hl = fuse && hn.cost;  // the heavy-item listing moves here from K1b
+    hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows) + (hl ? kHeavyBlocks : 0u)), dim3(64), 0,
+                       c->stream, (int)nrows, (unsigned *)c->rowcnt.p, hl ? hn : HeavyNext{});
     const RankLaunch rl{(unsigned)rank_blocks((int)nrows), (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p,
                         (unsigned *)c->rowcnt.p, (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb,
                         (int *)c->out_ci.p, (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p,
@@ -2884,6 +2989,12 @@ int detect_finish(Ctx *c, bool *retry) {
     return 0;
   }
   c->zeroed_rows = -1;  // (a retry zeroes everything again; so does any host-side recovery)
+  if (h.fuse_ovf) {  // a wave flushed more blocks than the fused K1b records: K1b as its own launch
+    c->fuse_skip = true;
+    c->fuse_retries++;
+    *retry = true;
+    return 0;
+  }
   if (h.k2_demand) {  // a K2 row bucket was full: nothing was written (the
     grow_k2_bucket(c, h.k2_demand);  // candidate list itself is complete: a reusable one stays valid)
     *retry = true;

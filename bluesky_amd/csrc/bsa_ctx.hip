@@ -2,8 +2,14 @@
 // include/bsaccel.h.  No exception crosses the ABI: every entry point
 // returns a status and keeps its message in the context.
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdarg>
+#include <cstring>
+#include <mutex>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "bsa_internal.h"
 
@@ -44,6 +50,130 @@ bool ensure(Ctx *c, DevBuf &b, size_t bytes, const char *what) {
   }
   b.bytes = rounded;
   return true;
+}
+
+// ---------------------------------------------------------------- pinned host staging
+// The drop-ins move 5-15 MB per call at 100k aircraft (bsa_sim_update's
+// arrays, the pair lists, the ASAS outputs).  hipMemcpyAsync from pageable
+// memory bounces through the runtime's own buffers one array at a time;
+// here the host side is one parallel copy into a pinned buffer of the
+// context and the device side ONE DMA of the whole batch.
+namespace {
+struct CopyPool {
+  std::mutex use;  // one batch at a time (other callers copy on their own thread)
+  std::mutex m;
+  std::condition_variable cv, done_cv;
+  std::vector<std::thread> th;
+  std::vector<HostCopy> pieces;
+  std::atomic<size_t> next{0}, done{0};
+  unsigned gen = 0;
+  int busy = 0;
+  bool stop = false;
+  CopyPool() {
+    int nt = 8;
+    if (const char *e = getenv("BSA_COPY_THREADS")) nt = atoi(e);
+    const unsigned hw = std::thread::hardware_concurrency();
+    nt = std::max(0, std::min(nt, (int)(hw > 1 ? hw - 1 : 0)));
+    for (int k = 0; k < nt; ++k) th.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : th) t.join();
+  }
+  void work() {
+    for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+      memcpy(pieces[k].dst, pieces[k].src, pieces[k].bytes);
+      done.fetch_add(1);
+    }
+  }
+  void loop() {
+    unsigned seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return stop || gen != seen; });
+        if (stop) return;
+        seen = gen;
+        ++busy;
+      }
+      work();
+      {
+        std::lock_guard<std::mutex> lk(m);
+        --busy;
+      }
+      done_cv.notify_all();
+    }
+  }
+};
+CopyPool &copy_pool() {
+  static CopyPool *p = new CopyPool();  // (never destroyed: no join at static teardown)
+  return *p;
+}
+}  // namespace
+
+void host_copy(const HostCopy *jobs, int n) {
+  constexpr size_t kPiece = size_t(256) << 10, kSmall = size_t(1) << 20;
+  size_t total = 0;
+  for (int k = 0; k < n; ++k) total += jobs[k].bytes;
+  CopyPool &P = copy_pool();
+  std::unique_lock<std::mutex> use(P.use, std::try_to_lock);
+  if (total < kSmall || P.th.empty() || !use.owns_lock()) {
+    for (int k = 0; k < n; ++k)
+      if (jobs[k].bytes) memcpy(jobs[k].dst, jobs[k].src, jobs[k].bytes);
+    return;
+  }
+  {
+    // (under the lock, once no worker is inside work(): a late waker of the
+    // last batch must never see the piece list change under it)
+    std::unique_lock<std::mutex> lk(P.m);
+    P.done_cv.wait(lk, [&] { return P.busy == 0; });
+    P.pieces.clear();
+    for (int k = 0; k < n; ++k)
+      for (size_t o = 0; o < jobs[k].bytes; o += kPiece)
+        P.pieces.push_back(HostCopy{(char *)jobs[k].dst + o, (const char *)jobs[k].src + o,
+                                    std::min(kPiece, jobs[k].bytes - o)});
+    P.next = 0;
+    P.done = 0;
+    ++P.gen;
+  }
+  P.cv.notify_all();
+  P.work();
+  std::unique_lock<std::mutex> lk(P.m);
+  P.done_cv.wait(lk, [&] { return P.done.load() == P.pieces.size() && P.busy == 0; });
+}
+
+unsigned char *pin_stage(Ctx *c, size_t bytes) {
+  if (c->pin_busy) {  // a DMA from the buffer may still run
+    if (hipEventSynchronize(c->pin_ev) != hipSuccess) {
+      fail(c, "pinned staging: event wait failed");
+      return nullptr;
+    }
+    c->pin_busy = false;
+  }
+  if (c->pin_bytes < bytes) {
+    if (c->pin) (void)hipHostFree(c->pin);
+    c->pin = nullptr;
+    c->pin_bytes = 0;
+    const size_t rounded = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    if (hipHostMalloc(&c->pin, rounded, hipHostMallocDefault) != hipSuccess) {
+      c->pin = nullptr;
+      fail(c, "hipHostMalloc(%zu) for the pinned staging failed", rounded);
+      return nullptr;
+    }
+    c->pin_bytes = rounded;
+  }
+  return (unsigned char *)c->pin;
+}
+
+int pin_issued(Ctx *c) {
+  if (!c->pin_ev) BSA_HIP(c, hipEventCreateWithFlags(&c->pin_ev, hipEventDisableTiming));
+  BSA_HIP(c, hipEventRecord(c->pin_ev, c->stream));
+  c->pin_busy = true;
+  return 0;
 }
 
 // like ensure, but a grown buffer keeps its contents (persistent device state)
@@ -230,16 +360,25 @@ static int fetch_home_device(Ctx *c, int32_t *ci, int32_t *cj, double *const dst
                      (const int *)c->out_lj.p, (int *)(st + o_ci), (int *)(st + o_cj), (double *)(st + o_pay),
                      (int *)(st + o_li), (int *)(st + o_lj));
   BSA_HIP(c, hipGetLastError());
-  auto cp = [&](void *dst, size_t off, size_t bytes) -> int {
-    if (dst && bytes) BSA_HIP(c, hipMemcpyAsync(dst, st + off, bytes, hipMemcpyDeviceToHost, c->stream));
-    return 0;
-  };
-  if (cp(ci, o_ci, P * 4) || cp(cj, o_cj, P * 4) || cp(li, o_li, L * 4) || cp(lj, o_lj, L * 4) ||
-      cp(inconf, o_inc, R) || cp(tcpamax, o_tm, R * 8))
-    return -1;
-  for (int f = 0; f < 5; ++f)
-    if (cp(dst5[f], o_pay + (size_t)f * P * 8, P * 8)) return -1;
+  // the re-ordered lists [0, o_len) in ONE DMA into the pinned staging, then
+  // one parallel host copy into the caller's arrays
+  unsigned char *pin = pin_stage(c, o_len);
+  if (!pin) return -1;
+  BSA_HIP(c, hipMemcpyAsync(pin, st, o_len, hipMemcpyDeviceToHost, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
+  HostCopy jobs[11];
+  int nj = 0;
+  auto cp = [&](void *dst, size_t off, size_t bytes) {
+    if (dst && bytes) jobs[nj++] = HostCopy{dst, pin + off, bytes};
+  };
+  cp(ci, o_ci, P * 4);
+  cp(cj, o_cj, P * 4);
+  cp(li, o_li, L * 4);
+  cp(lj, o_lj, L * 4);
+  cp(inconf, o_inc, R);
+  cp(tcpamax, o_tm, R * 8);
+  for (int f = 0; f < 5; ++f) cp(dst5[f], o_pay + (size_t)f * P * 8, P * 8);
+  host_copy(jobs, nj);
   return 0;
 }
 
@@ -248,9 +387,18 @@ static int upload6(Ctx *c, DevBuf *dst, int64_t n, const double *const src[6]) {
   for (int k = 0; k < 6; ++k) {
     if (!src[k]) return fail(c, "NULL %s array", names[k]);
     if (!ensure(c, dst[k], (size_t)n * 8, names[k])) return -1;
-    if (n) BSA_HIP(c, hipMemcpyAsync(dst[k].p, src[k], (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
   }
-  return 0;
+  if (!n) return 0;
+  // one parallel host copy into the pinned staging, then the six DMAs
+  const size_t nb = (size_t)n * 8;
+  unsigned char *pin = pin_stage(c, 6 * nb);
+  if (!pin) return -1;
+  HostCopy jobs[6];
+  for (int k = 0; k < 6; ++k) jobs[k] = HostCopy{pin + k * nb, src[k], nb};
+  host_copy(jobs, 6);
+  for (int k = 0; k < 6; ++k)
+    BSA_HIP(c, hipMemcpyAsync(dst[k].p, pin + k * nb, nb, hipMemcpyHostToDevice, c->stream));
+  return pin_issued(c);
 }
 
 }  // namespace bsa
@@ -311,6 +459,10 @@ void bsa_destroy(bsa_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->pin) (void)hipHostFree(c->pin);
+  if (c->pin_ev) (void)hipEventDestroy(c->pin_ev);
+  c->pin = nullptr;
+  c->pin_ev = nullptr;
   bsa::DevBuf *all[] = {&c->rowrec, &c->colrec, &c->pfrow, &c->pfcol, &c->counters, &c->cand,
                         &c->ckey, &c->cval, &c->ckey2, &c->cval2, &c->cpay, &c->kbuck, &c->lkey, &c->lkey2,
                         &c->out_ci, &c->out_cj, &c->out_li, &c->out_lj, &c->out_pay, &c->inconf,
@@ -407,10 +559,6 @@ int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *d
   if (bsa::sim_adopt_pairs(c)) return -1;
   if (!c->have_pairs) return bsa::fail(c, "no detect results to fetch");
   const int64_t P = c->last_conf, L = c->last_los, R = c->last_re - c->last_rb;
-  auto cp = [&](void *dst, const void *src, size_t bytes) -> int {
-    if (dst && bytes) BSA_HIP(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
-    return 0;
-  };
   const double *pay = (const double *)c->out_pay.p;
   if (dcpa && !(c->last_flags & BSA_FLAG_WITH_DCPA)) return bsa::fail(c, "dcpa requested without BSA_FLAG_WITH_DCPA");
   if (c->last_home && c->last_rb == c->sim_rb && c->last_re == c->sim_re && c->lbyidx.p &&
@@ -435,13 +583,32 @@ int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *d
     put(tcpamax, h.tcpamax.data(), R * 8);
     return 0;
   }
-  if (cp(ci, c->out_ci.p, P * 4) || cp(cj, c->out_cj.p, P * 4) || cp(qdr, pay + 0 * P, P * 8) ||
-      cp(dist, pay + 1 * P, P * 8) || cp(tcpa, pay + 2 * P, P * 8) || cp(tinconf, pay + 3 * P, P * 8) ||
-      cp(li, c->out_li.p, L * 4) || cp(lj, c->out_lj.p, L * 4) || cp(inconf, c->inconf.p, R) ||
-      cp(tcpamax, c->tcpamax.p, R * 8))
-    return -1;
-  if (dcpa && cp(dcpa, pay + 4 * P, P * 8)) return -1;
+  // every requested array by DMA into the pinned staging, then one parallel
+  // host copy into the caller's arrays
+  struct {
+    void *dst;
+    const void *src;
+    size_t bytes;
+  } part[11] = {{ci, c->out_ci.p, (size_t)P * 4},  {cj, c->out_cj.p, (size_t)P * 4},   {qdr, pay, (size_t)P * 8},
+                {dist, pay + P, (size_t)P * 8},     {tcpa, pay + 2 * P, (size_t)P * 8}, {tinconf, pay + 3 * P, (size_t)P * 8},
+                {dcpa, pay + 4 * P, (size_t)P * 8}, {li, c->out_li.p, (size_t)L * 4},  {lj, c->out_lj.p, (size_t)L * 4},
+                {inconf, c->inconf.p, (size_t)R},   {tcpamax, c->tcpamax.p, (size_t)R * 8}};
+  size_t total = 0;
+  for (auto &q : part)
+    if (q.dst && q.bytes) total += (q.bytes + 255) / 256 * 256;
+  unsigned char *pin = bsa::pin_stage(c, total);
+  if (!pin) return -1;
+  bsa::HostCopy jobs[11];
+  int nj = 0;
+  size_t off = 0;
+  for (auto &q : part) {
+    if (!q.dst || !q.bytes) continue;
+    BSA_HIP(c, hipMemcpyAsync(pin + off, q.src, q.bytes, hipMemcpyDeviceToHost, c->stream));
+    jobs[nj++] = bsa::HostCopy{q.dst, pin + off, q.bytes};
+    off += (q.bytes + 255) / 256 * 256;
+  }
   BSA_HIP(c, hipStreamSynchronize(c->stream));
+  bsa::host_copy(jobs, nj);
   return 0;
 }
 
@@ -464,6 +631,23 @@ int bsa_set_row_bucket(bsa_ctx *c, int width) {
   if (!c) return -1;
   if (width < 0 || width > 64) return bsa::fail(c, "row bucket width must be in [0, 64]");
   c->k2_bucket = width;
+  return 0;
+}
+
+int bsa_set_exact_fusion(bsa_ctx *c, int on, int max_records) {
+  if (!c) return -1;
+  if (max_records < 0 || max_records > bsa::kFuseRecsMax)
+    return bsa::fail(c, "max_records must be in [0, %d]", bsa::kFuseRecsMax);
+  c->fuse_on = on != 0;
+  c->fuse_recs = max_records;
+  return 0;
+}
+
+int bsa_exact_fusion_stats(bsa_ctx *c, int64_t *out3) {
+  if (!c || !out3) return -1;
+  out3[0] = c->fuse_count;
+  out3[1] = c->fuse_retries;
+  out3[2] = c->last_fused ? 1 : 0;
   return 0;
 }
 

@@ -113,6 +113,8 @@ constexpr int kCandShards = BSA_CAND_SHARDS;  // candidate list shards (one coun
 constexpr unsigned kDangling = 0xffffffffu;  // resopairs column of a deleted intruder (sorts last in a row)
 
 // counters block on the device
+constexpr int kFuseRecsMax = 64;  // fused K1b: mid-sweep flush records per prefilter wave (LDS)
+
 struct Counters {
   unsigned long long cand;    // host-side total (sum of the shard counts)
   unsigned long long conf;
@@ -124,6 +126,7 @@ struct Counters {
   unsigned long long k2_demand;   // K2 row buckets: the largest row count beyond Ctx::k2_bucket (0: fit)
   unsigned long long halo_ovf;    // halo exchange: more tiles to send / receive than the capacities
   unsigned long long halo_miss;   // halo exchange inconsistent (a kept tile pair without its data): bug
+  unsigned long long fuse_ovf;    // fused K1b: a wave flushed more blocks than it can record (retry unfused)
   // diagnostic builds only (-DBSA_PF_STAMPS): prefilter s_memtime cycles per phase
   unsigned long long stamp[8];
   unsigned long long cshard[kCandShards][16];  // candidates per shard (word 0 of each line)
@@ -138,6 +141,18 @@ struct DevBuf {
 
 struct Ctx;
 bool ensure(Ctx *c, DevBuf &b, size_t bytes, const char *what);
+// Pinned host staging (bsa_ctx.hip): host_copy copies its jobs with a small
+// thread pool (chunks of 256 KiB; small totals on the calling thread);
+// pin_stage returns the context's pinned buffer of >= bytes once no DMA from
+// it is pending; pin_issued marks a DMA from it just enqueued on c->stream.
+struct HostCopy {
+  void *dst;
+  const void *src;
+  size_t bytes;
+};
+void host_copy(const HostCopy *jobs, int n);
+unsigned char *pin_stage(Ctx *c, size_t bytes);
+int pin_issued(Ctx *c);
 bool ensure_keep(Ctx *c, DevBuf &b, size_t bytes, const char *what);  // grows, keeps contents
 void release(DevBuf &b);
 
@@ -234,6 +249,12 @@ struct Ctx {
   // MVP / kinematics staging (host-buffer entry points)
   DevBuf seg, mvp_stage, kin_stage, mvp_pdv, mvp_pfl, mvp_rowdv;
   DevBuf xfer_stage;  // batched home-order transfers (bsa_sim.hip: HomeBatch), index-order staging
+  // pinned host staging of the drop-ins' transfers (pin_stage, bsa_ctx.hip):
+  // one DMA per batch; pin_ev guards the buffer while a DMA from it may run
+  void *pin = nullptr;
+  size_t pin_bytes = 0;
+  hipEvent_t pin_ev = nullptr;
+  bool pin_busy = false;
 
   // multi-GPU: comm is an ncclComm_t (one process per GPU) or group an
   // in-process group of contexts (bsa_comm.hip); at most one is set
@@ -309,6 +330,11 @@ struct Ctx {
   int64_t halo_grows = 0;          // capacity regrowths (aborted steps)
   int64_t halo_rx = 0, halo_tx = 0;  // bytes received / sent per CD step (the capacities' transfers)
   int halo_fields = 8;             // fp64 arrays per halo row of the last exchange (6 when derivable)
+  bool last_fused = false;  // the last detect ran K1b fused into the prefilter (ExactFuse, bsa_cd.hip)
+  bool fuse_skip = false;   // a fused detect ran out of flush records: its retry runs K1b as its own launch
+  bool fuse_on = true;      // bsa_set_exact_fusion
+  int fuse_recs = kFuseRecsMax;  // ... per-wave mid-sweep flush records (testing knob)
+  int64_t fuse_count = 0, fuse_retries = 0;  // bsa_exact_fusion_stats
   // region layout agreement (comm_halo): every rank's send lengths / offsets
   // are compared with every receiver's expectation whenever the layout may have
   // changed -- a new capacity generation (init, regrowth: collective events) or

@@ -300,16 +300,25 @@ struct HomeBatch {
     if (f.nf == 0 || n <= 0) return 0;
     if (!ensure(c, c->xfer_stage, bytes, "transfer staging")) return -1;
     unsigned char *st = (unsigned char *)c->xfer_stage.p;
-    if (up)
-      for (int q = 0; q < f.nf; ++q)
-        BSA_HIP(c, hipMemcpyAsync(st + f.off[q], hsrc[q], (size_t)n * f.esz[q], hipMemcpyHostToDevice, c->stream));
+    // the host side through the pinned staging: one parallel host copy and
+    // ONE DMA of the whole batch (pin_stage, bsa_ctx.hip)
+    unsigned char *pin = pin_stage(c, bytes);
+    if (!pin) return -1;
+    HostCopy jobs[kXferMax];
+    if (up) {
+      for (int q = 0; q < f.nf; ++q) jobs[q] = HostCopy{pin + f.off[q], hsrc[q], (size_t)n * f.esz[q]};
+      host_copy(jobs, f.nf);
+      BSA_HIP(c, hipMemcpyAsync(st, pin, bytes, hipMemcpyHostToDevice, c->stream));
+    }
     hipLaunchKernelGGL(k_home_xfer, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, (int)n, f,
                        (const unsigned *)c->h2id.p, st);
     BSA_HIP(c, hipGetLastError());
-    if (!up)
-      for (int q = 0; q < f.nf; ++q)
-        BSA_HIP(c, hipMemcpyAsync(hdst[q], st + f.off[q], (size_t)n * f.esz[q], hipMemcpyDeviceToHost, c->stream));
+    if (!up) BSA_HIP(c, hipMemcpyAsync(pin, st, bytes, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
+    if (!up) {
+      for (int q = 0; q < f.nf; ++q) jobs[q] = HostCopy{hdst[q], pin + f.off[q], (size_t)n * f.esz[q]};
+      host_copy(jobs, f.nf);
+    }
     f.nf = 0;
     bytes = 0;
     return 0;
@@ -497,6 +506,10 @@ static int grow_after_abort(Ctx *c, const unsigned long long *ctl) {
   Counters h;
   BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
   if (h.k2_demand) grow_k2_bucket(c, h.k2_demand);  // a K2 row bucket was full on this rank
+  if (h.fuse_ovf) {  // fused K1b out of flush records: the re-run's detect unfused
+    c->fuse_skip = true;
+    c->fuse_retries++;
+  }
   unsigned long long worst = 0;
   for (int q = 0; q < kCandShards; ++q) worst = std::max(worst, h.cshard[q][0]);
   if (worst > c->cand_cap / kCandShards)

@@ -132,6 +132,17 @@ int bsa_set_candidate_capacity(bsa_ctx *ctx, int64_t capacity);
  * scatter into row segments, width 0).  Default 8.  Results never depend on
  * it (tests set it to exercise every path). */
 int bsa_set_row_bucket(bsa_ctx *ctx, int width);
+/* K1b (the exact fp64 evaluation of the prefilter's candidates) fused into
+ * the prefilter's launch (on by default; stored records, row buckets, not
+ * KWIK / candidate reuse): each prefilter workgroup evaluates the candidates
+ * it produced at the end of its sweep.  max_records (0..64, default 64): the
+ * mid-sweep flushes a wave records for that; a wave that flushes more makes
+ * the detect retry with K1b as its own launch (0 forces that retry whenever
+ * a wave flushes mid-sweep: a testing knob).  Results never depend on it. */
+int bsa_set_exact_fusion(bsa_ctx *ctx, int on, int max_records);
+/* [0] detects enqueued with K1b fused, [1] of them retried unfused (a wave ran
+ * out of flush records), [2] whether the last detect fused (0 / 1). */
+int bsa_exact_fusion_stats(bsa_ctx *ctx, int64_t *out3);
 /* Candidate-list reuse across detects (own == intruder, whole row range, not
  * KWIK / NOPRUNE).  A detect that builds the list inflates
  * every aircraft's reach by a horizontal budget sigma_h [m] and a vertical

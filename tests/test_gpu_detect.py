@@ -186,3 +186,55 @@ def test_row_bucket_widths_are_identical(ctx):
         assert len(exp['ci']) > 0
     finally:
         ctx.set_row_bucket(8)
+
+
+def _fusion_ctx():
+    from bluesky_amd import _lib
+    return _lib.Context(0)
+
+
+@pytest.mark.parametrize('case', ['box4000', 'global4000', 'dense2000'])
+def test_fused_exact_equals_own_launch(case):
+    """K1b fused into the prefilter's launch (bsa_set_exact_fusion, default on)
+    and K1b as its own launch give bitwise identical results; the fused run
+    really fused (bsa_exact_fusion_stats), and against the oracle too."""
+    t = {'box4000': lambda: synth.box(4000, 150.0, seed=11),
+         'global4000': lambda: synth.global_traffic(4000, seed=13),
+         'dense2000': lambda: synth.box(2000, 60.0, seed=17)}[case]()
+    c = _fusion_ctx()
+    try:
+        a = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c)
+        st = c.exact_fusion_stats()
+        assert st['last'] and st['fused'] >= 1
+        c.set_exact_fusion(False)
+        b = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c)
+        assert not c.exact_fusion_stats()['last']
+    finally:
+        c.close()
+    for k in a:
+        if a[k] is not None:
+            assert np.array_equal(a[k], b[k]), k
+    util.assert_detect_equal(a, ocd.detect_arrays(t, t, RPZ, HPZ, TLA), RPZ, TLA)
+
+
+def test_fused_exact_out_of_records_retries_unfused():
+    """A wave that flushes more blocks mid-sweep than it can record makes the
+    detect retry with K1b's own launch (max_records 0: any mid-sweep flush):
+    the results are those of the fused run, and the next detect fuses again."""
+    t = synth.box(3000, 100.0, seed=19)   # dense (<= 29 conflicts a row): waves flush full stages mid-sweep
+    c = _fusion_ctx()
+    try:
+        a = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c)
+        c.set_exact_fusion(True, 0)
+        b = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c)
+        st = c.exact_fusion_stats()
+        assert st['retries'] >= 1 and not st['last']
+        c.set_exact_fusion(True, 64)
+        d = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c)
+        assert c.exact_fusion_stats()['last']
+    finally:
+        c.close()
+    for k in a:
+        if a[k] is not None:
+            assert np.array_equal(a[k], b[k]), k
+            assert np.array_equal(a[k], d[k]), k
