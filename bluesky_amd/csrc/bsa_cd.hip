@@ -1683,8 +1683,10 @@ __device__ __forceinline__ bool cand_overflow(const Counters *cnt, unsigned long
 
 // The next detect's listed items (HeavyArgs): every item whose units took at
 // least a threshold is listed (two tiers), its cost word zeroed.  Runs on the
-// grid's last lanes (K1b: the lanes past the candidate count; k_rowblk when K1b
-// is fused into the prefilter).  Wave-uniform per loop trip.
+// grid's last lanes (K1b: the lanes past the candidate count; k_rowblk's extra
+// blocks when K1b is fused into the prefilter -- in K2's launch, whose lanes
+// would have had the time, its code cost K2 +5 us even when skipped).
+// Wave-uniform per loop trip.
 __device__ __forceinline__ void heavy_next(const HeavyNext &hn) {
   const unsigned long long inear = hn.work[1], m = inear + hn.work[2];
   const unsigned long long nt = (unsigned long long)gridDim.x * blockDim.x;
