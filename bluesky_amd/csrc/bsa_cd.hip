@@ -2846,9 +2846,14 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const int B = c->k2_bucket;
   if (B && !ensure(c, c->kbuck, (size_t)2 * nrows * B * sizeof(uint2), "K2 row buckets")) return -1;
   // K1b fused into the prefilter (ExactFuse): stored records, row buckets, no
-  // KWIK / candidate reuse (BSA_FUSE_EXACT=0: K1b as its own launch, for A/B)
-  static const bool fuse_env = !(getenv("BSA_FUSE_EXACT") && atoi(getenv("BSA_FUSE_EXACT")) == 0);
-  const bool fuse = fuse_env && c->fuse_on && !c->fuse_skip && B > 0 && recs && !kwik && !reuse;
+  // KWIK / candidate reuse, not one rank's share of a sharded step (there the
+  // sweep is short and the workgroups' end-of-sweep evaluation lengthened it
+  // more than K1b's launch cost: global1m rank 2 of 8, prefilter 46 + K1b 11
+  // -> 63 us; box100k one rank: 0.1387-0.1396 -> 0.1336-0.1367 ms per step).
+  // BSA_FUSE_EXACT=0/1 overrides (A/B).
+  static const int fuse_env = getenv("BSA_FUSE_EXACT") ? atoi(getenv("BSA_FUSE_EXACT")) : -1;
+  const bool fuse = fuse_env != 0 && (fuse_env == 1 || !halo) && c->fuse_on && !c->fuse_skip && B > 0 && recs &&
+                    !kwik && !reuse;
   c->fuse_skip = false;  // (one retry unfused; the next detect fuses again)
   ExactFuse xf{};
   if (fuse)
