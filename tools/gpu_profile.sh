@@ -46,6 +46,7 @@ if [ "${K24PASS:-1}" = 1 ]; then
     rc=$?; echo "k24=0 pmc pass $j rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
   python tools/pmc_roofline.py $OUT/pmc_k24off.json $OUT/k24off_p1 $OUT/k24off_p2
+  cp $OUT/pmc_k24off.json profiles/pmc_k24off.json
 fi
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; [ $rc -eq 0 ] || exit $rc

@@ -24,7 +24,7 @@ def main():
         sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
         for R in (1, 2, 4, 8):
             rpr = ((n + R - 1) // R + 511) // 512 * 512
-            worst, max_halo = None, 0
+            worst, max_halo, per_rank = None, 0, []
             for r in range(R):
                 rb, re = min(n, r * rpr), min(n, (r + 1) * rpr)
                 if re <= rb:
@@ -40,11 +40,12 @@ def main():
                 row = dict(rank=r, rows=re - rb, ms={k: round(v, 4) for k, v in tm.items()},
                            tiles=ts['tiles'] / d, groups=ts['groups'] / d, candidates=ts['candidates'] / d,
                            halo_tiles=halo, halo_MB=halo * 6 * 512 * 8 / 1e6)
+                per_rank.append(round(tm['total'], 4))
                 if worst is None or tm['total'] > worst['ms']['total']:
                     worst = row
                 max_halo = max(max_halo, halo)
             print(name, 'R=%d' % R, json.dumps(worst), 'max halo tiles %d (%.2f MB)'
-                  % (max_halo, max_halo * 6 * 512 * 8 / 1e6), flush=True)
+                  % (max_halo, max_halo * 6 * 512 * 8 / 1e6), 'per-rank total ms %s' % per_rank, flush=True)
 
 
 if __name__ == '__main__':
