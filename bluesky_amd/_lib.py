@@ -190,6 +190,7 @@ SIGNATURES.update({
     'bsa_sim_halo_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_set_halo_cap': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64]),
     'bsa_sim_halo_recheck': (ctypes.c_int, [_vp]),
+    'bsa_sim_probe_rank': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     'bsa_set_exact_fusion': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     'bsa_exact_fusion_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_sim_comm_stats': (ctypes.c_int, [_vp, _c_i64p]),
@@ -763,6 +764,10 @@ class Context:
         v = np.zeros(3, np.int64)
         self.check(self.lib.bsa_exact_fusion_stats(self.h, ptr(v, _c_i64p)), 'bsa_exact_fusion_stats')
         return dict(fused=int(v[0]), retries=int(v[1]), last=bool(v[2]))
+
+    def sim_probe_rank(self, rank, nranks):
+        """bsa_sim_probe_rank (measurement aid): the one-rank sim's steps play rank `rank` of `nranks`."""
+        self.check(self.lib.bsa_sim_probe_rank(self.h, int(rank), int(nranks)), 'bsa_sim_probe_rank')
 
     def sim_halo_recheck(self):
         """bsa_sim_halo_recheck (collective): the next exchange re-checks the region layout."""

@@ -926,6 +926,36 @@ int bsa_sim_detect_rows(bsa_ctx *cc, int64_t row_begin, int64_t row_end, int64_t
   return r;
 }
 
+int bsa_sim_probe_rank(bsa_ctx *cc, int rank, int nranks) {
+  Ctx *c = (Ctx *)cc;
+  if (!c) return -1;
+  if (!c->sim_ready) return bsa::fail(c, "bsa_sim_probe_rank before bsa_sim_init");
+  if (c->nranks != 1) return bsa::fail(c, "bsa_sim_probe_rank: a one-rank sim only (it plays one rank of several)");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return bsa::fail(c, "bad probe rank %d of %d", rank, nranks);
+  BSA_HIP(c, hipSetDevice(c->device));
+  const int64_t n = c->n;
+  c->tpr_valid = false;  // (its tile-pair list / plan are rebuilt for the new rows)
+  c->sim_prepped = false;
+  if (nranks == 1) {  // back to the whole sim
+    c->sim_rb = 0;
+    c->sim_re = n;
+    c->halo_mode = 0;
+    return bsa::set_home_maps(c);  // (the rows' index order: row ids, fetched pairs)
+  }
+  // the rank's home range (bsa_sim_init's partition) and the one-GPU halo
+  // mode of bsa_sim_detect_rows: the other ranks' tiles are prepared once here
+  // (their rows do not move: only this rank's K4' runs), the rank's own tiles
+  // and its halo by every detect
+  const int64_t rpr = ((n + nranks - 1) / nranks + bsa::kTile - 1) / bsa::kTile * bsa::kTile;
+  c->sim_rb = std::min<int64_t>(n, (int64_t)rank * rpr);
+  c->sim_re = std::min<int64_t>(n, c->sim_rb + rpr);
+  if (c->sim_rb % bsa::kTile != 0) return bsa::fail(c, "probe rank %d of %d holds no rows", rank, nranks);
+  if (bsa::set_home_maps(c) || bsa::sim_gather(c) || bsa::prep_all_tiles(c, c->simp.rpz, c->simp.hpz, c->simp.tla))
+    return -1;
+  c->halo_mode = 2;
+  return 0;
+}
+
 int bsa_sim_halo_stats(bsa_ctx *cc, int64_t *out4) {
   Ctx *c = (Ctx *)cc;
   if (!c || !out4) return -1;

@@ -497,6 +497,13 @@ int bsa_sim_comm_stats(bsa_ctx *ctx, int64_t *out3);
  * is caught on one GPU).  tiles >= 0; the next bsa_sim_init or regrowth
  * recomputes the capacities. */
 int bsa_sim_set_halo_cap(bsa_ctx *ctx, int sender, int receiver, int64_t tiles);
+/* Measurement aid (tools/probe_step.py): a ONE-rank sim plays rank `rank` of
+ * `nranks` on this GPU -- bsa_sim_step then runs that rank's share of the
+ * sharded step (its home rows: own tiles, halo plan and halo tiles as
+ * bsa_sim_detect_rows does, K3 / K4' on its rows) with no collective; the
+ * other rows do not move.  The results are not the sim's (timing only);
+ * nranks = 1 returns to the whole sim (re-init it for results). */
+int bsa_sim_probe_rank(bsa_ctx *ctx, int rank, int nranks);
 /* Collective (every rank, before the same step): the next halo exchange
  * re-checks the region layout on all ranks -- every send length / offset
  * against its receiver's expectation, one host all-reduce -- as it does after

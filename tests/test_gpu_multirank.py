@@ -588,3 +588,28 @@ def test_bench_parity_vs_world1_group(world):
     res = run_ranks(world, rank)
     assert all(x['ok'] for x in res), res
     assert res[0]['mismatched'] == [] and res[0]['n_conf'] > 0 and len(res[0]['state_sha256']) == 64
+
+
+def test_probe_rank_step_runs_one_rank_share():
+    """bsa_sim_probe_rank (measurement aid of tools/probe_step.py): a one-rank
+    sim steps only rank r's home rows in the one-GPU halo mode; the rows of the
+    other ranks do not move, and nranks = 1 returns to the whole sim."""
+    t = synth.box(3001, 100.0, seed=61)
+    init = resident.initial_state(t)
+    c = _lib.Context(0)
+    try:
+        sim = resident.ResidentSim(init, resident.params(cd_every=1), ctx=c)
+        before = sim.read()
+        c.sim_probe_rank(1, 2)
+        sim.step(3)
+        st = sim.stats()
+        assert (st['row_begin'], st['row_end']) == dist.home_range(t.ntraf, 1, 2)
+        after = sim.read()
+        mine = np.zeros(t.ntraf, bool)
+        mine[sim.row_ids()] = True
+        assert not np.array_equal(after['lat'][mine], before['lat'][mine])   # its rows moved
+        assert np.array_equal(after['lat'][~mine], before['lat'][~mine])     # the others did not
+        c.sim_probe_rank(0, 1)
+        assert (sim.stats()['row_begin'], sim.stats()['row_end']) == (0, t.ntraf)
+    finally:
+        c.close()
