@@ -587,6 +587,7 @@ struct TprArgs {
   float dx, ds, dv;
   const PFRec *pc;  // this detect's column records (rows = columns)
   PFRec *snap;
+  unsigned *myflag;  // several ranks / the probe: the rank's rebuild flag, cleared here (the plan read it)
 };
 
 // Halo mode (hl != NULL): the columns are this rank's own tiles [p0, p1) and
@@ -601,6 +602,7 @@ __global__ __launch_bounds__(kTPDirectThreads) __attribute__((amdgpu_waves_per_e
     Counters *__restrict__ cnt, unsigned long long *__restrict__ icnt, const unsigned *__restrict__ build,
     const uint8_t *__restrict__ present, int p0, int p1, const TileBox *__restrict__ gbc,
     const int *__restrict__ hl, int nhl, const unsigned *__restrict__ nhl_dev, TprArgs tp) {
+  if (tp.myflag && blockIdx.x == 0 && threadIdx.x == 0) *tp.myflag = 0u;  // (k_halo_plan's blocks all read it)
   if (build && !build[0]) return;
   // tile-pair list reuse: no build this detect -> the kept
   // list's item counts into the dequeue words, nothing else
@@ -2768,7 +2770,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const unsigned long long icap = (unsigned long long)ntp * kSlicesPerTile;  // items: 8 slices per tile pair
   if (tpr)  // (after halo_mid, which may have forced the rebuild)
     tp = TprArgs{(unsigned long long *)c->tpr_ctl.p, ht.force, c->tpr_dx, c->tpr_ds, c->tpr_dv,
-                 (const PFRec *)c->pfcol.p + roff, (PFRec *)c->tpr_snap.p + roff};
+                 (const PFRec *)c->pfcol.p + roff, (PFRec *)c->tpr_snap.p + roff, halo ? ht.myflag : nullptr};
   if ((nct <= kTPDirectMax || tp_list) && !tp_super)
     hipLaunchKernelGGL(k_tilepairs_direct, dim3((unsigned)nrt), dim3(kTPDirectThreads), 0, c->stream, nrt, nct,
                        (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,

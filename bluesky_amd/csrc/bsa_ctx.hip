@@ -176,6 +176,19 @@ int pin_issued(Ctx *c) {
   return 0;
 }
 
+// Device-side gather of up to kGatherMax word arrays into one staging region
+// (part k's wlen[k] words at word woff[k], 256-B aligned), so that a download
+// is ONE DMA
+__global__ __launch_bounds__(256) void k_gather_words(GatherParts g, unsigned *__restrict__ dst) {
+  const unsigned long long nw = g.woff[g.n];
+  for (unsigned long long w = blockIdx.x * 256ull + threadIdx.x; w < nw; w += (unsigned long long)gridDim.x * 256) {
+    int p = 0;
+    while (p + 1 < g.n && w >= g.woff[p + 1]) ++p;
+    const unsigned long long i = w - g.woff[p];
+    if (i < g.wlen[p]) dst[w] = g.src[p][i];
+  }
+}
+
 // like ensure, but a grown buffer keeps its contents (persistent device state)
 bool ensure_keep(Ctx *c, DevBuf &b, size_t bytes, const char *what) {
   if (bytes == 0) bytes = 16;
@@ -593,22 +606,32 @@ int bsa_fetch_pairs(bsa_ctx *c, int32_t *ci, int32_t *cj, double *qdr, double *d
                 {dist, pay + P, (size_t)P * 8},     {tcpa, pay + 2 * P, (size_t)P * 8}, {tinconf, pay + 3 * P, (size_t)P * 8},
                 {dcpa, pay + 4 * P, (size_t)P * 8}, {li, c->out_li.p, (size_t)L * 4},  {lj, c->out_lj.p, (size_t)L * 4},
                 {inconf, c->inconf.p, (size_t)R},   {tcpamax, c->tcpamax.p, (size_t)R * 8}};
-  size_t total = 0;
-  for (auto &q : part)
-    if (q.dst && q.bytes) total += (q.bytes + 255) / 256 * 256;
-  unsigned char *pin = bsa::pin_stage(c, total);
-  if (!pin) return -1;
+  // gathered on the device into one staging region (one launch), ONE DMA
+  // into the pinned staging, one parallel host copy into the caller's arrays
+  bsa::GatherParts g{};
   bsa::HostCopy jobs[11];
-  int nj = 0;
   size_t off = 0;
   for (auto &q : part) {
     if (!q.dst || !q.bytes) continue;
-    BSA_HIP(c, hipMemcpyAsync(pin + off, q.src, q.bytes, hipMemcpyDeviceToHost, c->stream));
-    jobs[nj++] = bsa::HostCopy{q.dst, pin + off, q.bytes};
+    g.src[g.n] = (const unsigned *)q.src;
+    g.woff[g.n] = off / 4;
+    g.wlen[g.n] = (q.bytes + 3) / 4;  // (a byte array's last word: inside its 2 MiB-rounded allocation)
+    jobs[g.n] = bsa::HostCopy{q.dst, nullptr, q.bytes};
+    g.n++;
     off += (q.bytes + 255) / 256 * 256;
   }
+  g.woff[g.n] = off / 4;
+  if (!g.n) return 0;
+  if (!bsa::ensure(c, c->fetch_stage, off, "fetch staging")) return -1;
+  unsigned char *pin = bsa::pin_stage(c, off);
+  if (!pin) return -1;
+  hipLaunchKernelGGL(bsa::k_gather_words, dim3((unsigned)std::min<size_t>((off / 4 + 255) / 256, 2048)), dim3(256), 0,
+                     c->stream, g, (unsigned *)c->fetch_stage.p);
+  BSA_HIP(c, hipGetLastError());
+  BSA_HIP(c, hipMemcpyAsync(pin, c->fetch_stage.p, off, hipMemcpyDeviceToHost, c->stream));
   BSA_HIP(c, hipStreamSynchronize(c->stream));
-  bsa::host_copy(jobs, nj);
+  for (int k = 0; k < g.n; ++k) jobs[k].src = pin + g.woff[k] * 4;
+  bsa::host_copy(jobs, g.n);
   return 0;
 }
 

@@ -189,9 +189,30 @@ __device__ __forceinline__ bool plan_rebuild(const PlanArgs &a) {
   return any;
 }
 
-__global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a, int ny) {
+// One launch for the plan AND the lists (round 5: the lists were their own
+// launch, ~5 us at 1M R = 8 even when a kept plan made both return at once):
+// rows y < npy are the plan's blocks; row y == npy holds one list block per
+// source / destination q (blockIdx.x < nlist), which -- when the plan is
+// (re)built -- waits until every plan block has counted itself done (`done`,
+// a zeroed word behind the plan flags; the plan blocks never wait, so the
+// waiting list blocks cannot starve them).  The lists are k_halo_lists_q.
+__device__ void halo_lists_block(const ListArgs &a, const HaloCaps &cp, int q, uint8_t *present);
+__global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a, int ny, int npy, ListArgs la, HaloCaps cp, int nlist,
+                                                   uint8_t *present, unsigned *done) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int na = a.a1 - a.a0, y = blockIdx.y;
+  if (y == npy) {  // a list block
+    const int q = blockIdx.x;
+    if (q >= nlist || (a.ht.tpr && !plan_rebuild(a))) return;  // (the same decision as every plan block)
+    if (threadIdx.x == 0) {
+      const unsigned np = gridDim.x * (unsigned)npy;
+      while (__hip_atomic_load(done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < np) __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+    __threadfence();  // (every lane: the plan's stores after the count)
+    halo_lists_block(la, cp, q, present);
+    return;
+  }
   if (a.ht.tpr) {
     const bool rb = plan_rebuild(a);
     if (t == 0 && y == 0) {  // (every block reads the words first: the flag is cleared after this launch)
@@ -221,16 +242,18 @@ __global__ __launch_bounds__(256) void k_halo_plan(PlanArgs a, int ny) {
     const int q = t / na, i = t - q * na;
     if (q != a.me && req_bit(a, q, a.a0 + i)) a.send[(size_t)q * a.tpr + i] = 1;
   }
+  // this block's plan stores, then its count (the list blocks wait for all)
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(done, 1u);
 }
 
-// block q: the lists of source / destination q (halo_lists_q); with plan
-// reuse only at a rebuild (ctl[0], decided by k_halo_plan), when it also
-// keeps source q's part of the present mask for the detects until the next
-__global__ __launch_bounds__(256) void k_halo_lists(ListArgs a, HaloCaps cp, const unsigned long long *ctl,
-                                                    uint8_t *present, unsigned *myflag) {
-  if (ctl && ctl[0] == 0ull) return;
-  const int q = blockIdx.x;
-  if (myflag && q == 0 && threadIdx.x == 0) *myflag = 0u;  // (read by the plan launch before this one)
+// list block q: the lists of source / destination q (halo_lists_q); with
+// plan reuse only at a rebuild (decided by every block alike), when it also
+// keeps source q's part of the present mask for the detects until the next.
+// (The rank's rebuild flag is cleared by K0d, after every block of this
+// launch has read it.)
+__device__ void halo_lists_block(const ListArgs &a, const HaloCaps &cp, int q, uint8_t *present) {
   if (present) {
     const int t0 = q * a.tpr, t1 = min(a.nct, t0 + a.tpr);
     for (int t = t0 + (int)threadIdx.x; t < t1; t += blockDim.x) present[t] = a.recv[t];
@@ -282,8 +305,13 @@ const unsigned *halo_list_count(const Ctx *c) {
 // the plan's buffers: recv [nct] + send [R][tpr] flags, demands ([R] send,
 // [R] receive, the total received).  hp: the own-tile
 // K0b zeroes them (the regions are recorded there); NULL: memsets here.
+static size_t plan_bytes(int nct, int R, int tpr) { return ((size_t)nct + (size_t)R * tpr + 3) / 4 * 4; }
+// the merged plan / lists launch's done counter: the word behind the plan flags
+static unsigned *plan_done_word(Ctx *c, int nct, int R, int tpr) {
+  return (unsigned *)((char *)c->h_plan.p + plan_bytes(nct, R, tpr));
+}
 static int plan_buffers(Ctx *c, int nct, int R, int tpr, int Rd, HaloPre *hp, bool keep) {
-  const size_t pbytes = (size_t)nct + (size_t)R * tpr, dwords = (size_t)(2 * Rd + 1);
+  const size_t pbytes = plan_bytes(nct, R, tpr) + 4, dwords = (size_t)(2 * Rd + 1);  // (+ the done word)
   if (!ensure(c, c->h_plan, pbytes + 64, "halo plan") || !ensure(c, c->h_dem, dwords * 4, "halo demands"))
     return -1;
   if (keep) {  // plan reuse: the kept present mask (k_halo_lists writes it at a rebuild)
@@ -354,11 +382,9 @@ static int plan_local(Ctx *c, int a0, int a1, int tpr, const HaloTpr *ht) {
   ListArgs la{nct, tpr, Rp, -1, a0, a1, 1, recv, nullptr, (int *)c->h_hl.p, nullptr, (unsigned *)c->h_dem.p,
               (Counters *)c->counters.p};
   const int ny = std::max(1, std::min(na, kPlanRows));
-  hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((nct + 255) / 256), (unsigned)ny), dim3(256), 0, c->stream, pa, ny);
-  BSA_HIP(c, hipGetLastError());
-  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)Rp), dim3(256), 0, c->stream, la, HaloCaps{},
-                     (const unsigned long long *)(h.tpr ? h.ctl : nullptr),
-                     h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, h.tpr ? h.myflag : (unsigned *)nullptr);
+  const unsigned gx = (unsigned)std::max((nct + 255) / 256, Rp);
+  hipLaunchKernelGGL(k_halo_plan, dim3(gx, (unsigned)(ny + 1)), dim3(256), 0, c->stream, pa, ny, ny, la, HaloCaps{}, Rp,
+                     h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, plan_done_word(c, nct, 1, tpr));
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -424,12 +450,9 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht) {
   ListArgs la{nct, tpr, R, me, a0, a1, 0, recv, sendf, (int *)c->h_hl.p, (unsigned char *)c->h_send.p,
               (unsigned *)c->h_dem.p, (Counters *)c->counters.p};
   const int ny = std::max(1, std::min(na, kPlanRows));
-  hipLaunchKernelGGL(k_halo_plan, dim3((unsigned)((std::max(nct, R * na) + 255) / 256), (unsigned)(ny + 2)),
-                     dim3(256), 0, s, pa, ny);
-  BSA_HIP(c, hipGetLastError());
-  hipLaunchKernelGGL(k_halo_lists, dim3((unsigned)R), dim3(256), 0, s, la, cp,
-                     (const unsigned long long *)(h.tpr ? h.ctl : nullptr),
-                     h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, h.tpr ? h.myflag : (unsigned *)nullptr);
+  const unsigned gx = (unsigned)std::max((std::max(nct, R * na) + 255) / 256, R);
+  hipLaunchKernelGGL(k_halo_plan, dim3(gx, (unsigned)(ny + 3)), dim3(256), 0, s, pa, ny, ny + 2, la, cp, R,
+                     h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, plan_done_word(c, nct, R, tpr));
   BSA_HIP(c, hipGetLastError());
   HaloFields fl{};
   DevBuf *src[8] = {&c->own[0], &c->own[1], &c->own[2], &c->own[3], &c->own[4], &c->own[5], &c->s_gse, &c->s_gsn};

@@ -151,6 +151,14 @@ struct HostCopy {
   size_t bytes;
 };
 void host_copy(const HostCopy *jobs, int n);
+constexpr int kGatherMax = 12;
+struct GatherParts {
+  const unsigned *src[kGatherMax];
+  unsigned long long woff[kGatherMax + 1];
+  unsigned long long wlen[kGatherMax];
+  int n;
+};
+__global__ void k_gather_words(GatherParts g, unsigned *__restrict__ dst);
 unsigned char *pin_stage(Ctx *c, size_t bytes);
 int pin_issued(Ctx *c);
 bool ensure_keep(Ctx *c, DevBuf &b, size_t bytes, const char *what);  // grows, keeps contents

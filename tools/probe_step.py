@@ -5,7 +5,7 @@ rows -- with no collective (bsa_sim_probe_rank), timed as one batch of STEPS
 steps (one host synchronisation at its end, no stage events).  Collectives
 (box all-gather, halo send / recv, gate all-reduce) are excluded: they need
 the 8-GPU node.  Prints every rank's ms per step and the slowest.
-Usage: python tools/probe_step.py [WORKLOAD [R [STEPS]]]"""
+Usage: python tools/probe_step.py [WORKLOAD [R [STEPS [RANK]]]]  (RANK: that rank of R only)"""
 import json
 import os
 import sys
@@ -19,14 +19,15 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else 'global1m'
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 40
+    only = int(sys.argv[4]) if len(sys.argv) > 4 else None
     t = synth.workload(name)
     ctx = _lib.Context(0)
     ctx.set_timing_sample(0)
     sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
     out = {}
-    for ranks in sorted({1, R}):
+    for ranks in sorted({1, R}) if only is None else [R]:
         per = []
-        for r in range(ranks):
+        for r in range(ranks) if only is None else [only]:
             ctx.sim_probe_rank(r, ranks)
             sim.step(5)                      # warm-up: this rank's plan / lists / buffers
             ctx.sync()
