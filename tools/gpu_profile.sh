@@ -53,8 +53,10 @@ rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json; [ $rc -eq 0 ] || exit $rc
 if [ "${PROBE:-0}" = 1 ]; then  # the per-rank share of a sharded step
   timeout -k 10 400 python -u tools/rowslice_probe.py box100k global1m > $OUT/rowslice_probe.log 2>&1
   rc=$?; echo "rowslice rc=$rc"; cut -c1-300 $OUT/rowslice_probe.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -u tools/probe_step.py global1m 8 40 > $OUT/probe_step.log 2>&1
+  rc=$?; echo "probe_step rc=$rc"; tail -1 $OUT/probe_step.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/probe -o run --output-format csv -- \
-      python tools/probe_rank.py global1m 8 2 20 > $OUT/probe_rank.log 2>&1
-  rc=$?; echo "probe rc=$rc"; grep "per detect" $OUT/probe_rank.log; [ $rc -eq 0 ] || exit $rc
+      python tools/probe_step.py global1m 8 30 4 > $OUT/probe_rank.log 2>&1
+  rc=$?; echo "probe rc=$rc"; grep "ms per step" $OUT/probe_rank.log; [ $rc -eq 0 ] || exit $rc
   find $OUT/probe -name "*kernel_trace.csv" -size +4M -delete
 fi
