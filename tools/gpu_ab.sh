@@ -5,6 +5,7 @@
 #   CONFIGS="name:LIB[:ENV=V,ENV=V] ..."   (default "base:libbsaccel.so")
 #   REPS=3  STEPS=60  WARMUP=10  BENCH_ARGS="--workload global1m"
 #   PROBE=1 (tools/rowslice_probe.py per config; PROBE_WL="box100k global1m")
+#   STEP_PROBE="global1m 8 40 4" (tools/probe_step.py per config and rep: one rank's whole step)
 #   PYTEST="tests/test_gpu_detect.py ..." (parity subset first, on the default library)
 #
 # e.g. CONFIGS="a:libbsaccel.so b:libbsaccel_x.so c:libbsaccel.so:BSA_PF_PIECES_NEAR=4" REPS=3 bash tools/gpu_ab.sh
@@ -27,6 +28,11 @@ for r in $(seq ${REPS:-3}); do
     python -c "
 import json; d=json.load(open('$o.json')); k=d['kernels_ms_rank0']
 print('%-12s ms/step %.4f  k0 %.4f pf %.4f ex %.4f k2 %.4f  cand %d' % ('$name', d['ms_per_step'], k['k0_prep'], k['prefilter'], k['exact'], k['k2_sort'], d['n_candidates']))"
+    if [ -n "${STEP_PROBE:-}" ]; then
+      env BSACCEL_AB=1 BSACCEL_LIB=$PWD/bluesky_amd/$lib ${envs//,/ } timeout -k 10 240 \
+          python -u tools/probe_step.py $STEP_PROBE > $o.step 2>&1 || { tail -3 $o.step; exit 1; }
+      echo "$name step probe: $(grep 'ms per step' $o.step | tail -1)"
+    fi
   done
 done
 if [ "${PROBE:-0}" = 1 ]; then
