@@ -62,7 +62,7 @@ struct BkIn {
 };
 
 __device__ __forceinline__ bool bk_aborted(const unsigned long long *gate, const unsigned *sticky) {
-  return sticky[0] != 0 || gate[0] != 0;
+  return sticky[0] != 0 || gate[0] >= kGateOverflow;
 }
 
 // ResumeNav's decision for resopair (i, j), asas.py:424-452.  j == kDangling:
@@ -118,7 +118,7 @@ __global__ void k_bk_check(int nrows, const unsigned *nptr, unsigned long long n
   if (bk_aborted(gate, sticky)) return;
   const unsigned long long total = nptr[nrows];
   if (total > ncap) {
-    gate[0] = 2;
+    gate[0] = kGateBkOverflow;
     *demand = total > *demand ? total : *demand;
   }
 }
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void k_bk_pack(int nrows, const unsigned *rowo
   const unsigned t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
   if (need > W) {
     if (t == 0) {
-      gate[0] = 2;
+      gate[0] = kGateBkOverflow;
       atomicMax(demand, need);
     }
     return;

@@ -118,7 +118,8 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
                                                    SoA6 own, SoA6 intr, double rpz, double hpz,
                                                    double tla, RowRec *__restrict__ R,
                                                    PFRec *__restrict__ PR, PFVel *__restrict__ PV,
-                                                   float4 *__restrict__ PP, int mid) {
+                                                   float4 *__restrict__ PP, int mid, uint8_t *__restrict__ rowbad,
+                                                   int rb) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt) return;
   const int o = (int)perm[k];
@@ -155,6 +156,8 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   // within ~0.6 deg of a pole (or |lat| > 90: the refine's local east / north
   // basis is ill-conditioned), or a non-finite position: never refine
   v.flags = (!(cosl > 1e-2) || !(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) ? 1u : 0u;
+  // every tcpa of the row, hence its tcpamax, is NaN (K2; rows in index order)
+  rowbad[o - rb] = (isfinite(la) && isfinite(lo) && isfinite(r.u) && isfinite(r.v)) ? 0 : 1;
   PR[k] = p;
   PV[k] = v;
 }
@@ -215,6 +218,17 @@ struct ZeroArgs {
   unsigned *x[3];  // more word regions to zero (the halo plan's buffers: HaloPre), or NULL
   int xn[3];
 };
+// Non-finite tcpa inputs (Ctx::nonfin): producers (the column records'
+// makers) store `epoch` into *word when a column's position or velocity is
+// non-finite; K2 makes every row's tcpamax NaN when *word == epoch, and a
+// row's own when rowbad[row] is set (rows of their own, written by
+// k_prep_rows in index order; NULL when the rows are columns)
+struct NfArgs {
+  unsigned long long *word;
+  unsigned long long epoch;
+  const uint8_t *rowbad;
+};
+
 __device__ __forceinline__ bool list_word(int k);
 __device__ __forceinline__ void zero_state(const ZeroArgs &z, int t, int nt) {
   constexpr int kWords = (int)(sizeof(Counters) / 8);
@@ -272,7 +286,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(6))) void
                                                      PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
                                                      ReuseParams rz, FusedBoxes fb, ZeroArgs zs, int tile_base,
                                                      const int *__restrict__ tile_list, HaloUnpack hu,
-                                                     Counters *__restrict__ hcnt, TprCheck tck) {
+                                                     Counters *__restrict__ hcnt, TprCheck tck, NfArgs nf) {
   __shared__ TileBox fgb[kTile / 64];
   // K0z (fused): nothing here reads that state
   if (zs.cnt) zero_state(zs, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
@@ -292,6 +306,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(6))) void
     const double tlap = tla > 0.0 ? tla : 0.0;
     const ColRec c = col_record(own, intr, o);
     if (rec) C[k] = c;
+    if (nf.word && !col_tcpa_finite(c)) *nf.word = nf.epoch;
     const double lo = c.lon, sinl = c.sinlat, cosl = c.coslat, gs = own.gs[o], olat = c.olat;
     const double lor = lo * kD2R;
     // (own.lat[j] == 0) leaves the different-hemisphere radius unbounded below
@@ -1895,8 +1910,10 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
                                               int *__restrict__ li, int *__restrict__ lj,
                                               unsigned long long *__restrict__ stats,
                                               unsigned long long *__restrict__ gate,
-                                              const unsigned *__restrict__ build, MvpFuse mf) {
+                                              const unsigned *__restrict__ build, MvpFuse mf, NfArgs nf,
+                                              unsigned long long *__restrict__ tcpamax_bits) {
   const bool ovf = cand_overflow(cnt, cap);
+  const bool nfcol = nf.word && *nf.word == nf.epoch;
   const unsigned P = rowoff[nrows], L = rowoff[2 * nrows + 1] - P;
   const unsigned t0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (t0 == 0) {
@@ -1926,12 +1943,15 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
       stats[3] += 1;
     }
     if (gate) {
-      gate[0] = ovf ? 1 : 0;
+      gate[0] = ovf ? kGateOverflow : (nfcol ? kGateNonfinite : 0);
       gate[1] = ovf ? 0 : P;
     }
   }
   if (ovf) return;
   const unsigned stride = gridDim.x * blockDim.x;
+  if (nfcol || nf.rowbad)  // non-finite tcpa inputs: tcpamax NaN (K1b's atomics left the others)
+    for (int r = (int)t0; r < nrows; r += (int)stride)
+      if (nfcol || nf.rowbad[r]) tcpamax_bits[r] = kNanBits;
   for (unsigned x = t0; x < P + L; x += stride) {
     const bool conf = x < P;
     const unsigned long long *keys = conf ? skey : lkey;
@@ -2023,7 +2043,8 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
                                                          unsigned char *__restrict__ inconf,
                                                          unsigned long long *__restrict__ tcpamax_bits,
                                                          Counters *__restrict__ cnext,
-                                                         unsigned long long *__restrict__ wnext, K24Args ka) {
+                                                         unsigned long long *__restrict__ wnext, K24Args ka,
+                                                         NfArgs nf) {
   constexpr int W = kRankThreads / 64;
   __shared__ unsigned red[4][W];
   __shared__ unsigned soff[2][kRankRows + 1];  // the block's rows' exclusive offsets (conf, LoS), + total
@@ -2036,6 +2057,9 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
   const bool rowlane = t < kRankRows;  // lanes past the block's rows only place pairs
   const int r = rowlane ? b * kRankRows + t : nrows;
   const unsigned c = r < nrows ? rowcnt[r] : 0u, l = r < nrows ? rowcnt[nrows + 1 + r] : 0u;
+  // non-finite tcpa inputs (NfArgs; loaded with the counts)
+  const bool nfcol = nf.word && *nf.word == nf.epoch;
+  const unsigned nfrow = nf.rowbad && r < nrows ? nf.rowbad[r] : 0u;
   // the next detect's per-row counts and counters start at zero (its K0z
   // launch is skipped, detect_enqueue): this block's counts are read, the
   // next detect's counter block (cnext / wnext, double-buffered) is idle
@@ -2108,7 +2132,7 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
       stats[3] += 1;
     }
     if (gate) {
-      gate[0] = ovf ? 1 : 0;
+      gate[0] = ovf ? kGateOverflow : (nfcol ? kGateNonfinite : 0);
       gate[1] = ovf ? 0 : P;
     }
   }
@@ -2232,7 +2256,9 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
       const unsigned long long bits = (unsigned long long)__double_as_longlong(tq);
       if (tq > 0.0 && bits > tm) tm = bits;
     }
-    tcpamax_bits[r] = tm;
+    // non-finite tcpa inputs in some column (every row) or in this row: NaN,
+    // as np.max propagates it
+    tcpamax_bits[r] = nfcol || nfrow ? kNanBits : tm;
     if (mf.rowdv)
       mf.rowdv[r] = lds_fold ? mvp_fold(sdv, sfl, ec, ec + c) : mvp_fold(mf.pdv, mf.pfl, cb + ec, cb + ec + c);
   }
@@ -2398,7 +2424,8 @@ int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla) {
   hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)nct), dim3(kTile), 0, c->stream, (int)n,
                      (const unsigned *)c->h2id.p, 1, 0, own, own, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, stage1_mid(0, false, 0),
-                     ReuseParams{}, fb, zs, 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, TprCheck{});
+                     ReuseParams{}, fb, zs, 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, TprCheck{},
+                     NfArgs{});
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -2426,14 +2453,25 @@ struct RankLaunch {
   unsigned long long *tcpamax;
   Counters *cnext;
   unsigned long long *wnext;
+  NfArgs nf;
 };
 static int rank_launch(Ctx *c, const RankLaunch &a, bool k24, const K24Args &ka) {
   const auto K = k24 ? k_rank_rows<true> : k_rank_rows<false>;
   hipLaunchKernelGGL(K, dim3(a.grid), dim3(kRankThreads), 0, c->stream, a.nrows, a.cnt, a.cap, a.rowoff, a.rowcnt,
                      a.kb, a.B, a.cpay, a.rb, a.ci, a.cj, a.out, a.li, a.lj, a.stats, a.gate, a.build, a.mf,
-                     a.inconf, a.tcpamax, a.cnext, a.wnext, ka);
+                     a.inconf, a.tcpamax, a.cnext, a.wnext, ka, a.nf);
   BSA_HIP(c, hipGetLastError());
   return 0;
+}
+
+bool nonfin_word(Ctx *c) {
+  const bool fresh = !c->nonfin.p;
+  if (!ensure(c, c->nonfin, 16, "non-finite input word")) return false;
+  if (fresh && hipMemsetAsync(c->nonfin.p, 0, 16, c->stream) != hipSuccess) {
+    fail(c, "zeroing the non-finite input word failed");
+    return false;
+  }
+  return true;
 }
 
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
@@ -2504,6 +2542,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        c->sim_prep_key[0] == rpz && c->sim_prep_key[1] == hpz && c->sim_prep_key[2] == tla &&
                        c->sim_prep_key[3] == (double)mid && c->sim_prep_n == n;
   c->sim_prepped = false;
+  // non-finite tcpa inputs: this detect's epoch (the prepped records carry K4''s)
+  if (!nonfin_word(c)) return -1;
+  NfArgs nfa{(unsigned long long *)c->nonfin.p, prepped ? c->nf_prep_epoch : ++c->nf_counter, nullptr};
   // K0z skipped: the last detect's K2 (k_rank_rows) zeroed this detect's
   // counter block (double-buffered), dequeue words and per-row counts, and
   // writes inconf / tcpamax of every row itself; the prepped tile boxes are
@@ -2659,10 +2700,12 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const PFRec *pfrow = shared ? (const PFRec *)c->pfcol.p + roff : (const PFRec *)c->pfrow.p;
   const PFVel *pfvrow = shared ? (const PFVel *)c->pfvcol.p + roff : (const PFVel *)c->pfvrow.p;
   const float4 *pfprow = shared ? (const float4 *)c->pfpcol.p + roff : (const float4 *)c->pfprow.p;
-  if (!shared) {
+  if (!shared) {  // (rows that are columns: the column word covers them)
+    if (!ensure(c, c->rownf, (size_t)nrows, "row non-finite flags")) return -1;
+    nfa.rowbad = (const uint8_t *)c->rownf.p;
     hipLaunchKernelGGL(k_prep_rows, dim3(blocks_for(nrows, 256)), dim3(256), 0, c->stream, (int)nrows,
                        perm_r, own, intr, rpz, hpz, tla, (RowRec *)c->rowrec.p, (PFRec *)c->pfrow.p,
-                       (PFVel *)c->pfvrow.p, (float4 *)c->pfprow.p, mid);
+                       (PFVel *)c->pfvrow.p, (float4 *)c->pfprow.p, mid, (uint8_t *)c->rownf.p, (int)rb);
     BSA_HIP(c, hipGetLastError());
   }
   // K0c for the columns is fused into K0b unless the candidate list is reused
@@ -2736,7 +2779,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                      c->stream, (int)n, perm_c, home ? 1 : 0, recs ? 1 : 0, own,
                      intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs,
-                     halo ? a0 : 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, tck);
+                     halo ? a0 : 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, tck, nfa);
   BSA_HIP(c, hipGetLastError());
   if (halo) {
     HaloUnpack hu{};
@@ -2749,7 +2792,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)c->halo_hl), dim3(kTile), 0, c->stream, (int)n, perm_c, 1,
                          recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                          (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, 0,
-                         (const int *)c->h_hl.p, hu, dcnt, TprCheck{});
+                         (const int *)c->h_hl.p, hu, dcnt, TprCheck{}, nfa);
       BSA_HIP(c, hipGetLastError());
     }
   }
@@ -2941,7 +2984,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                         (int *)c->out_ci.p, (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p,
                         (int *)c->out_lj.p, (unsigned long long *)c->stats.p, gate, build, mf,
                         (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
-                        (Counters *)c->counters2.p, (unsigned long long *)c->workq2.p};
+                        (Counters *)c->counters2.p, (unsigned long long *)c->workq2.p, nfa};
     if (c->k24_want) {  // bsa_sim_step launches it fused with K4' (k24_launch)
       c->k24_blob.resize(sizeof rl);
       memcpy(c->k24_blob.data(), &rl, sizeof rl);
@@ -2957,7 +3000,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (const unsigned *)c->cval2.p, (const double *)c->cpay.p,
                        (const unsigned long long *)c->lkey2.p, (int)rb, (int *)c->out_ci.p, (int *)c->out_cj.p,
                        (double *)c->out_pay.p, (int *)c->out_li.p, (int *)c->out_lj.p,
-                       (unsigned long long *)c->stats.p, gate, build, mf);
+                       (unsigned long long *)c->stats.p, gate, build, mf, nfa, (unsigned long long *)c->tcpamax.p);
   }
   BSA_HIP(c, hipGetLastError());
   if (!c->k24_pending && mark(4)) return -1;

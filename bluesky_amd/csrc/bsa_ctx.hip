@@ -487,7 +487,7 @@ void bsa_destroy(bsa_ctx *c) {
                         &c->tilepairs, &c->scan_ws, &c->snap_build, &c->snap_cur, &c->reuse_ctl, &c->reuse_use,
                         &c->geo_in, &c->geo_pts, &c->geo_out, &c->wfield,
                         &c->hv_cost, &c->hv_flag, &c->hv_list[0], &c->hv_list[1], &c->hv_list[2], &c->hv_list[3],
-                        &c->hv_cnt};
+                        &c->hv_cnt, &c->nonfin, &c->rownf};
   for (auto *b : all) bsa::release(*b);
   bsa::sim_release(c);
   bsa::feed_release(c);

@@ -110,7 +110,12 @@ constexpr int kEvSets = 4096;    // detect timing event sets kept between resets
 #define BSA_CAND_SHARDS 8
 #endif
 constexpr int kCandShards = BSA_CAND_SHARDS;  // candidate list shards (one counter each, 128 B apart)
-constexpr unsigned kDangling = 0xffffffffu;  // resopairs column of a deleted intruder (sorts last in a row)
+constexpr unsigned kDangling = 0xffffffffu;
+// gate[0] of the resident step (all-reduced max over ranks): 0 nothing, 1 a
+// non-finite tcpa input in some rank's columns (every row's tcpamax is NaN),
+// >= 2 abort the step (2 candidate / row-bucket overflow, 3 resopairs overflow)
+constexpr unsigned long long kGateNonfinite = 1, kGateOverflow = 2, kGateBkOverflow = 3;
+constexpr unsigned long long kNanBits = 0x7ff8000000000000ull;  // (a quiet NaN)  // resopairs column of a deleted intruder (sorts last in a row)
 
 // counters block on the device
 constexpr int kFuseRecsMax = 64;  // fused K1b: mid-sweep flush records per prefilter wave (LDS)
@@ -311,7 +316,14 @@ struct Ctx {
   DevBuf s_aptrk, s_aptas, s_apalt, s_apvs, s_selalt, s_bank, s_eps, s_accel;  // frozen
   DevBuf s_atrk, s_atas, s_avs, s_aalt, s_ase, s_asn, s_active;  // ASAS (full n)
   DevBuf g_send, g_recv;                                    // all-gather staging
-  DevBuf sim_ctl;  // [0,16) gate {overflow, P}; [16,20) sticky abort; [24,32) steps done;
+  // Non-finite tcpa inputs (StateBasedCD.py:90: tcpamax = np.max(tcpa *
+  // swconfl) is NaN on every row once one tcpa is NaN): nonfin[0] = the epoch
+  // of the last column records holding a non-finite lat / lon / u / v (its
+  // producers store the epoch, K2 compares; no zeroing, no atomics)
+  DevBuf nonfin;
+  DevBuf rownf;  // rows of their own (not columns): per row (index order), its position / velocity is not finite
+  unsigned long long nf_counter = 0, nf_prep_epoch = 0;  // epochs (K0b: a new one; K4' prep: the next detect's)
+  DevBuf sim_ctl;  // [0,16) gate {abort / non-finite, P}; [16,20) sticky abort; [24,32) steps done;
                    // [32,40) resopairs demand on a bookkeeping overflow; [40,48) pair-key
                    // block demand (several ranks)
   // ASAS bookkeeping (bsa_asas.hip, resume_nav = 1): resopairs CSR over own
@@ -502,6 +514,7 @@ int sim_adopt_pairs(Ctx *c);  // after resident steps: the last CD call's pairs 
 // detect entry points (bsa_cd.hip): detect = enqueue + finish (+ retries)
 int detect(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
            int64_t *n_conf, int64_t *n_los);
+bool nonfin_word(Ctx *c);  // Ctx::nonfin allocated (zeroed when new)
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
                    unsigned long long *gate);
 int detect_finish(Ctx *c, bool *retry);

@@ -59,8 +59,8 @@ __global__ __launch_bounds__(256) void k_mvp_pair(int rb, bsa_mvp_params p, MvpI
 __global__ __launch_bounds__(256) void k_mvp_row(int rb, bsa_mvp_params p, MvpIn in) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (in.gate) {
-    const bool abort = in.sticky[0] != 0 || in.gate[0] != 0;
-    if (r == 0 && in.gate[0] != 0) in.sticky[0] = 1u;
+    const bool abort = in.sticky[0] != 0 || in.gate[0] >= kGateOverflow;
+    if (r == 0 && in.gate[0] >= kGateOverflow) in.sticky[0] = 1u;
     if (abort) return;
   }
   if (r >= in.nrows) return;
@@ -130,6 +130,8 @@ int mvp_device(Ctx *c, const bsa_mvp_params &p, const MvpDev &d, const unsigned 
   in.active = active;
   in.nrows = (int)nrows;
   in.resolve = resolve ? 1 : 0;
+  // several ranks: the gate's non-finite word reaches every rank's tcpamax here
+  in.tcpamax = gate && comm_multi(c) ? (unsigned long long *)c->tcpamax.p : nullptr;
   if (!resolve && (!gate || !d.aptrk || !d.aptas || !d.apalt))
     return fail(c, "CR OFF (DoNothing) needs the resident step's autopilot targets");
   if (!pairs_done && resolve) {  // else K2 of the same step already wrote pdv / pfl (k_rank)

@@ -37,10 +37,13 @@ struct MvpIn {
   uint8_t *active;
   int nrows;
   int resolve;                                           // 0: CR OFF (DoNothing.py), resident step only
+  // rows [rb, re) or NULL: NaN when the (all-reduced) gate says some rank's
+  // columns hold a non-finite tcpa input (several ranks: K2 knew its own only)
+  unsigned long long *tcpamax;
 };
 
 __device__ __forceinline__ bool mvp_aborted(const MvpIn &in) {
-  return in.gate && (in.sticky[0] != 0 || in.gate[0] != 0);
+  return in.gate && (in.sticky[0] != 0 || in.gate[0] >= kGateOverflow);
 }
 
 // The dv fold of one row over its pairs in confpair order (MVP.py:44-61):
@@ -122,6 +125,7 @@ __device__ __forceinline__ MvpRowOut mvp_row(int rb, int r, const bsa_mvp_params
     apalt1 = in.apalt[id1];
   }
   if (in.gate) {
+    if (in.tcpamax && in.gate[0] == kGateNonfinite) in.tcpamax[r] = kNanBits;  // (StateBasedCD.py:90)
     if (in.inconf) {  // stand-in for ResumeNav unless resume_nav
       in.active[id1] = inc;
       res.act_valid = true;

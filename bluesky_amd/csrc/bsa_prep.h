@@ -137,6 +137,13 @@ __device__ __forceinline__ ColRec col_record_v(double la, double lo, double trkd
   return c;
 }
 
+// the column's inputs to every tcpa of its column (position, velocity) are
+// finite: else every tcpa[i, j] is NaN (StateBasedCD.py:58-72) and so is every
+// row's tcpamax (:90) -- Ctx::nonfin
+__device__ __forceinline__ bool col_tcpa_finite(const ColRec &c) {
+  return isfinite(c.lat) && isfinite(c.lon) && isfinite(c.u) && isfinite(c.v);
+}
+
 __device__ __forceinline__ ColRec col_record(const SoA6 &own, const SoA6 &intr, int o) {
   return col_record_v(intr.lat[o], intr.lon[o], own.trk[o], own.gs[o], own.alt[o], own.vs[o], own.lat[o]);
 }
@@ -152,9 +159,11 @@ struct PrepOut {
 };
 __device__ __forceinline__ PFRec prep_home_record(int k, double la, double lo, double trk, double gs, double alt,
                                                   double vs, double rpz, double hpz, double tla, int mid, int rec,
-                                                  const PrepOut &out) {
+                                                  const PrepOut &out, unsigned long long *nfw,
+                                                  unsigned long long nfe) {
   const double tlap = tla > 0.0 ? tla : 0.0;
   const ColRec c = col_record_v(la, lo, trk, gs, alt, vs, la);
+  if (nfw && !col_tcpa_finite(c)) *nfw = nfe;
   if (rec) out.C[k] = c;
   const double sinl = c.sinlat, cosl = c.coslat;
   const double lor = c.lon * kD2R;

@@ -48,8 +48,8 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
                                                          double vwe, WindField wf, SimDev d, MvpIn mv,
                                                          bsa_mvp_params mp, PrepArgs pa) {
   if (FUSE) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && mv.gate[0] != 0) mv.sticky[0] = 1u;
-    if (*d.sticky || mv.gate[0] != 0) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && mv.gate[0] >= kGateOverflow) mv.sticky[0] = 1u;
+    if (*d.sticky || mv.gate[0] >= kGateOverflow) return;
   } else if (*d.sticky) {
     return;
   }
@@ -674,6 +674,9 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
         pa.tla = c->simp.tla;
         pa.mid = bsa::stage1_mid(0, false, 0);
         pa.n = (int)n;
+        if (!bsa::nonfin_word(c)) return -1;
+        pa.nf = (unsigned long long *)c->nonfin.p;  // the next detect's records: a fresh epoch
+        pa.nfe = c->nf_prep_epoch = ++c->nf_counter;
         if (c->tpr_valid && c->tpr_snap.p && c->tpr_ctl.p && c->tpr_n == n) {  // the kept list's budgets
           pa.snap = (const bsa::PFRec *)c->tpr_snap.p;
           pa.tpr_ctl = (unsigned long long *)c->tpr_ctl.p;

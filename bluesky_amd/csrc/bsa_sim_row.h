@@ -42,6 +42,8 @@ struct PrepArgs {
   const PFRec *snap;
   unsigned long long *tpr_ctl;
   float dx, ds, dv;
+  unsigned long long *nf;  // non-finite tcpa inputs: the epoch stored (Ctx::nonfin), or NULL
+  unsigned long long nfe;
 };
 
 // one row of K4' (below).  The row's state is loaded before K3's part runs
@@ -130,7 +132,9 @@ __device__ __forceinline__ PFRec pilot_kin_row(int rb, int k, double simdt, int 
   d.gsn_w[k] = o.gsnorth;
   d.altprev[k] = s.alt;
   d.ax[k] = o.ax;
-  if (PREP) return prep_home_record(k, o.lat, o.lon, o.trk, o.gs, o.alt, o.vs, pa.rpz, pa.hpz, pa.tla, pa.mid, pa.rec, pa.out);
+  if (PREP)
+    return prep_home_record(k, o.lat, o.lon, o.trk, o.gs, o.alt, o.vs, pa.rpz, pa.hpz, pa.tla, pa.mid, pa.rec, pa.out,
+                            pa.nf, pa.nfe);
   return PFRec{};
 }
 

@@ -238,3 +238,46 @@ def test_fused_exact_out_of_records_retries_unfused():
         if a[k] is not None:
             assert np.array_equal(a[k], b[k]), k
             assert np.array_equal(a[k], d[k]), k
+
+
+@pytest.mark.parametrize('field,value', [('lat', np.nan), ('lon', np.nan), ('gs', np.nan), ('trk', np.nan),
+                                         ('alt', np.nan), ('vs', np.nan), ('gs', np.inf), ('alt', np.inf)])
+def test_nonfinite_aircraft(ctx, field, value):
+    """One aircraft with a non-finite state value (a null / erased field): the
+    reference's pairs are the finite aircraft's (every comparison with NaN is
+    false), and tcpamax = np.max(tcpa * swconfl, axis=1) (StateBasedCD.py:90)
+    is NaN on EVERY row once one tcpa is NaN -- an aircraft with a non-finite
+    lat / lon / gs / trk makes its whole column NaN."""
+    t = synth.box(600, 40.0, seed=23)
+    getattr(t, field)[7] = value
+    exp = ocd.detect_arrays(t, t, RPZ, HPZ, TLA)
+    try:
+        for width in (8, 0):   # row buckets (K2 = k_rank_rows) and the scatter path (k_rank)
+            ctx.set_row_bucket(width)
+            got = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=ctx)
+            util.assert_detect_equal(got, exp, RPZ, TLA)
+    finally:
+        ctx.set_row_bucket(8)
+
+
+def test_nonfinite_intruder_and_ownship_sets(ctx):
+    """Distinct ownship / intruder sets (equal sizes: the reference's
+    column-indexed lat == 0 term broadcasts ownship against intruder,
+    geo.py:128): the column of aircraft j reads intruder lat / lon and
+    ownship gs / trk, its row ownship lat / lon and intruder gs / trk -- a NaN
+    in a column input poisons every row's tcpamax, one in a row input only
+    that row's."""
+    own = synth.box(400, 40.0, seed=29)
+    intr = synth.box(400, 40.0, seed=31)
+    for who, arr, k in ((own, 'lat', 4), (own, 'gs', 6), (intr, 'lat', 8), (intr, 'trk', 9)):
+        t2 = synth.Traffic(*(getattr(who, f).copy() for f in ('lat', 'lon', 'alt', 'trk', 'gs', 'vs')))
+        getattr(t2, arr)[k] = np.nan
+        o, i = (t2, intr) if who is own else (own, t2)
+        exp = ocd.detect_arrays(o, i, RPZ, HPZ, TLA)
+        try:
+            for width in (8, 0):
+                ctx.set_row_bucket(width)
+                got = statebased.detect_indices(o, i, RPZ, HPZ, TLA, ctx=ctx)
+                util.assert_detect_equal(got, exp, RPZ, TLA)
+        finally:
+            ctx.set_row_bucket(8)

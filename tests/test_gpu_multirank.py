@@ -613,3 +613,31 @@ def test_probe_rank_step_runs_one_rank_share():
         assert (sim.stats()['row_begin'], sim.stats()['row_end']) == (0, t.ntraf)
     finally:
         c.close()
+
+
+def test_sharded_nonfinite_aircraft_equal_world1(ctx):
+    """A NaN ground speed on one aircraft (one rank's row): every rank's
+    tcpamax is NaN (the gate's non-finite word, all-reduced), as at world 1,
+    and the sharded state equals the one-rank state (NaN where it is NaN)."""
+    t = synth.box(3001, 100.0, seed=67)
+    t.gs[1234] = np.nan
+    init = resident.initial_state(t)
+    p = resident.params(cd_every=1)
+    ref = world1(init, p, 3, ctx)
+    exp, exp_st = ref.read(), ref.stats()
+    exp_pairs = ctx.fetch_pairs(exp_st['n_conf'], exp_st['n_los'])
+    assert np.isnan(exp_pairs['tcpamax']).all()
+
+    def rank(r, c, g):
+        sim = resident.ResidentSim(init, p, ctx=c, rank=r, world=2, group=g)
+        sim.step(3)
+        return sim.read(), sim.gather_pairs(root=0)
+
+    res = run_ranks(2, rank)
+    for r, (got, _) in enumerate(res):
+        for k in exp:
+            assert np.array_equal(got[k], exp[k], equal_nan=got[k].dtype.kind == 'f'), 'rank %d %s' % (r, k)
+    pairs = res[0][1]
+    for k in ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'li', 'lj', 'inconf'):
+        assert np.array_equal(pairs[k], exp_pairs[k]), k
+    assert np.isnan(pairs['tcpamax']).all()

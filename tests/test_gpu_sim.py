@@ -475,3 +475,30 @@ def test_resident_atmosphere_outputs(ctx):
     ctx.sim_set_atmos(False)
     with pytest.raises(_lib.AccelError):
         ctx.sim_read_atmos()
+
+
+@pytest.mark.parametrize('field', ['gs', 'lat'])
+def test_resident_nonfinite_aircraft(ctx, field):
+    """An aircraft with a NaN state value in the resident step: the CD call's
+    pairs are the finite aircraft's, every row's tcpamax is NaN as np.max makes
+    it (StateBasedCD.py:90 -- the next detect's records are K4''s), and the
+    step's state equals the oracle step's (NaN where the reference has NaN)."""
+    t = synth.box(1500, 60.0, seed=41)
+    getattr(t, field)[11] = np.nan
+    init = resident.initial_state(t)
+    p = resident.params(cd_every=1)
+    sim = resident.ResidentSim(init, p, ctx=ctx)
+    op = oracle_params(p)
+    prev = dict(init)
+    prev.update(asas_trk=init['trk'].copy(), asas_tas=init['tas'].copy(),
+                asas_vs=np.zeros(t.ntraf), active=np.zeros(t.ntraf, bool))
+    for k in range(3):   # the first detect from K0b's records, the next ones from K4''s
+        exp = ostep.sim_step(prev, op, do_cd=True)
+        sim.step(1)
+        st = sim.stats()
+        assert st['n_conf'] == exp['n_conf']
+        pairs = ctx.fetch_pairs(st['n_conf'], st['n_los'])
+        assert np.isnan(pairs['tcpamax']).all(), 'step %d' % k
+        got = full_state(init, sim.read())
+        compare(got, exp, k)
+        prev = got
