@@ -33,8 +33,9 @@ def test_prefilter_is_exact_safe_on_golden(ctx, path):
                                   ctx=ctx, stage1_t0=True)
     for k in a:
         if a[k] is not None:
-            assert np.array_equal(a[k], b[k]), k
-            assert np.array_equal(a[k], c[k]), k
+            nan = a[k].dtype.kind == 'f'   # (tcpamax of the non-finite cases)
+            assert np.array_equal(a[k], b[k], equal_nan=nan), k
+            assert np.array_equal(a[k], c[k], equal_nan=nan), k
 
 
 def test_midpoint_stage1_stress_sets_vs_oracle(ctx):

@@ -20,6 +20,8 @@ and outputs as small ``.npz`` files under ``tests/golden/``:
                          envelope (perfoap.py:211-262) and acceleration()
                          (perfoap.py:271-280) with the reference's own coefficient
                          tables (data/performance/OpenAP)
+* ``cd_nonfin_<case>.npz`` -- ``StateBasedCD.detect`` with a non-finite input
+                         (``--nonfinite-only`` writes only these)
 * ``cdkwik_<case>.npz`` -- the opt-in KWIK variant: ``StateBasedCD.detect`` with
                          ``geo.qdrdist_matrix`` swapped for ``geo.kwikqdrdist_matrix``
                          (geo.py:347-363), its metre distance handed over / nm
@@ -126,6 +128,26 @@ def cd_cases():
     return cases
 
 
+def nonfinite_cases():
+    """Non-finite inputs (a null / erased field): the pairs of the finite
+    aircraft, tcpamax NaN on every row (a non-finite column input) or on one
+    row (a row input) -- StateBasedCD.py:90's np.max propagating the NaN."""
+    cases = {}
+    t = synth.box(400, 40.0, seed=43)
+    t.gs[7] = np.nan
+    cases['nonfin_gs400'] = (t, None)
+    t = synth.box(400, 40.0, seed=47)
+    t.lat[3] = np.inf
+    t.alt[11] = np.nan
+    cases['nonfin_lat_alt400'] = (t, None)
+    own = synth.box(300, 40.0, seed=53)
+    intr = synth.box(300, 40.0, seed=59)
+    own.lat[4] = np.nan       # a row input: row 4 only
+    intr.trk[9] = np.nan      # a row input (the intruder velocity is row-indexed): row 9 only
+    cases['nonfin_own_ne_int300'] = (own, intr)
+    return cases
+
+
 def ids_to_idx(pairs, idmap):
     if not pairs:
         return np.zeros(0, np.int64), np.zeros(0, np.int64)
@@ -146,7 +168,9 @@ def run_cd(name, own, intr):
                  ('inconf', np.asarray(inconf)), ('tcpamax', np.asarray(tcpamax)),
                  ('qdr', np.asarray(qdr)), ('dist', np.asarray(dist)),
                  ('tcpa', np.asarray(tcpa)), ('tinconf', np.asarray(tin))):
-        ok = np.array_equal(o[k], v) if k != 'tcpamax' else np.all(o[k] == v)
+        # (tcpamax: +-0 compare equal; NaN where a non-finite input made it NaN)
+        ok = (np.array_equal(o[k], v) if k != 'tcpamax' else
+              np.all((o[k] == v) | (np.isnan(o[k]) & np.isnan(np.asarray(v, dtype=float)))))
         assert ok, 'oracle != reference for %s/%s' % (name, k)
     d = dict(lat=own.lat, lon=own.lon, alt=own.alt, trk=own.trk, gs=own.gs, vs=own.vs,
              same=np.array(intr is None), rpz=RPZ, hpz=HPZ, tla=TLA,
@@ -184,7 +208,9 @@ def run_kwik(name, own, intr):
                  ('inconf', np.asarray(inconf)), ('tcpamax', np.asarray(tcpamax)),
                  ('qdr', np.asarray(qdr)), ('dist', np.asarray(dist)),
                  ('tcpa', np.asarray(tcpa)), ('tinconf', np.asarray(tin))):
-        ok = np.array_equal(o[k], v) if k != 'tcpamax' else np.all(o[k] == v)
+        # (tcpamax: +-0 compare equal; NaN where a non-finite input made it NaN)
+        ok = (np.array_equal(o[k], v) if k != 'tcpamax' else
+              np.all((o[k] == v) | (np.isnan(o[k]) & np.isnan(np.asarray(v, dtype=float)))))
         assert ok, 'oracle != reference for kwik %s/%s' % (name, k)
     d = dict(lat=own.lat, lon=own.lon, alt=own.alt, trk=own.trk, gs=own.gs, vs=own.vs,
              same=np.array(intr is None), rpz=RPZ, hpz=HPZ, tla=TLA,
@@ -580,6 +606,11 @@ KWIK_CASES = ('box500', 'equator1500', 'antimeridian800', 'polar400', 'edge', 'o
 def main():
     os.makedirs(OUT, exist_ok=True)
     cds = cd_cases()
+    if '--nonfinite-only' in sys.argv:
+        with np.errstate(invalid='ignore'):
+            for name, (own, intr) in nonfinite_cases().items():
+                run_cd(name, own, intr)
+        return
     if '--kwik-only' in sys.argv:
         for name in KWIK_CASES:
             run_kwik(name, *cds[name])
@@ -607,6 +638,9 @@ def main():
     results = {}
     for name, (own, intr) in cds.items():
         results[name] = run_cd(name, own, intr)
+    with np.errstate(invalid='ignore'):
+        for name, (own, intr) in nonfinite_cases().items():
+            run_cd(name, own, intr)
     for name in ('box64', 'box500', 'box2000', 'edge', 'equator1500'):
         run_mvp(name, cds[name][0], results[name])
     run_kin('nowind2000', 2000, 31, 0.05)
