@@ -410,8 +410,8 @@ def main():
         roof['lds_bank_conflict_rate'] = pf['lds_bank_conflict_rate']
     kin = pmc.get('k_sim_pilot_kin', {})
     kin_kernel, kin_note = 'k_sim_pilot_kin', None
-    fused = world == 1 and os.environ.get('BSA_K24', '1') != '0'
-    if not kin.get('dur_ns') and fused and pmc.get('k_rank_rows', {}).get('dur_ns'):
+    k24 = world == 1 and os.environ.get('BSA_K24', '1') != '0'   # (K2 fused with K4')
+    if not kin.get('dur_ns') and k24 and pmc.get('k_rank_rows', {}).get('dur_ns'):
         # one rank: K4' runs inside K2's launch (k_rank_rows<true>)
         kin = pmc['k_rank_rows']
         kin_kernel = "k_rank_rows<true> (K2 fused with K4')"
