@@ -108,7 +108,10 @@ int bsa_detect(bsa_ctx *ctx, double rpz, double hpz, double tla, int flags,
  *   dcpa[m] (n_conf, may be NULL; needs BSA_FLAG_WITH_DCPA)
  *   li, lj                                                n_los entries each
  *   inconf (uint8 0/1), tcpamax[s]                        row_end-row_begin entries
- * Any pointer may be NULL to skip that output. */
+ * Any pointer may be NULL to skip that output.  Non-finite inputs follow the
+ * reference (StateBasedCD.py:90): tcpamax is NaN on every row when some
+ * column's position / velocity is not finite, and on one row when only that
+ * row's is; the pairs are the finite aircraft's. */
 int bsa_fetch_pairs(bsa_ctx *ctx,
                     int32_t *ci, int32_t *cj, double *qdr, double *dist,
                     double *tcpa, double *tinconf, double *dcpa,
