@@ -2004,17 +2004,13 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
 // per-row counts: bcnt[b], bcnt[nb + b]); one wave per block, kRankRows / 64
 // rows per lane (one load round trip; an overflowed detect's sums are never
 // read: k_rank_rows checks the overflow itself)
-// four row blocks per 256-lane workgroup (one wave each): a quarter of the
-// workgroups to dispatch, the heavy-item listing's extra ones included
-constexpr int kRowblkWaves = 4;
-constexpr unsigned kHeavyBlocks = 256;  // k_rowblk's extra workgroups for the heavy-item listing
-__global__ __launch_bounds__(64 * kRowblkWaves) void k_rowblk(int nrows, unsigned *__restrict__ rowcnt, HeavyNext hn) {
+constexpr unsigned kHeavyBlocks = 1024;  // k_rowblk's extra one-wave blocks for the heavy-item listing
+__global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__ rowcnt, HeavyNext hn) {
   // (K1b fused into the prefilter: the next detect's listed items here, on
-  // every lane of the grid -- the host adds kHeavyBlocks workgroups past the
-  // row blocks' for them, ~1 slot per lane at the 100k box)
+  // every lane of the grid -- the host adds kHeavyBlocks blocks past the nb
+  // row blocks for them, ~1 slot per lane at the 100k box)
   if (hn.cost) heavy_next(hn);
-  const int nb = rank_blocks(nrows), b = blockIdx.x * kRowblkWaves + (int)(threadIdx.x >> 6),
-            lane = threadIdx.x & 63;
+  const int nb = rank_blocks(nrows), b = blockIdx.x, lane = threadIdx.x;
   if (b >= nb) return;
   unsigned c = 0, l = 0;
 #pragma unroll
@@ -2981,10 +2977,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   }
   if (B) {
     const bool hl = fuse && hn.cost;  // the heavy-item listing moves here from K1b
-    hipLaunchKernelGGL(k_rowblk,
-                       dim3((unsigned)((rank_blocks((int)nrows) + kRowblkWaves - 1) / kRowblkWaves) +
-                            (hl ? kHeavyBlocks : 0u)),
-                       dim3(64 * kRowblkWaves), 0,
+    hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows) + (hl ? kHeavyBlocks : 0u)), dim3(64), 0,
                        c->stream, (int)nrows, (unsigned *)c->rowcnt.p, hl ? hn : HeavyNext{});
     const RankLaunch rl{(unsigned)rank_blocks((int)nrows), (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p,
                         (unsigned *)c->rowcnt.p, (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb,
