@@ -315,6 +315,9 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=60)
     ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--settle', type=int, default=300,
+                    help='untimed steps before the W warm-up steps, so the timed batch sees the GPU at its '
+                         'steady clocks (DESIGN.md 5: a cold device is ~15%% slower over its first ~25 ms)')
     ap.add_argument('--n', type=int, default=100000)
     ap.add_argument('--workload', default='box100k', choices=['box10k', 'box100k', 'global1m'])
     ap.add_argument('--cd-every', type=int, default=1)
@@ -353,6 +356,10 @@ def main():
     sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=args.cd_every),
                                ctx=ctx, rank=rank, world=world)
 
+    if args.settle > 0:          # same count on every rank (the halo step exchanges)
+        sim.step(1)              # the first batch grows the candidate buffers and re-runs: keep it short
+        sim.step(args.settle - 1)
+        ctx.sync()
     sim.step(args.warmup)
     ctx.allreduce_max([0.0])     # barrier
     ctx.sync()
@@ -373,7 +380,8 @@ def main():
     tile_reuse = dict(builds=tr['builds'] - tr0['builds'], detects=tr['detects'] - tr0['detects'],
                       note='K0d tile-pair list rebuilt on the device when a record left its drift budget')
 
-    cd_steps = sum(1 for k in range(args.warmup, args.warmup + args.steps) if k % args.cd_every == 0)
+    k0 = max(args.settle, 0) + args.warmup   # sim step index of the timed batch's first step
+    cd_steps = sum(1 for k in range(k0, k0 + args.steps) if k % args.cd_every == 0)
     pairs = float(n) * n * cd_steps
     value = pairs / dt
     pf_s = tm['prefilter'] * 1e-3
@@ -448,6 +456,7 @@ def main():
                           peak_TFLOPs=FP64_PEAK_TFLOPS)
     out = dict(metric='CD pair-evals/s at 100k aircraft (GPU-resident sim step, ASAS every step)',
                value=value, unit='pair-evals/s', n_gpus=world, steps=args.steps, warmup=args.warmup,
+               settle_steps=max(args.settle, 0),
                ms_per_step=dt / args.steps * 1e3, higher_is_better=True, scaling='strong',
                vs_baseline=None, dtype='f64', data='synthetic',
                config=dict(workload='%s N=%d (seed 7, density-matched box)' % (args.workload, n),

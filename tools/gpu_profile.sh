@@ -13,7 +13,9 @@ if [ "${PYTEST:-1}" = 1 ]; then
   [ $rc -eq 0 ] || exit $rc
 fi
 # (PMC passes: 8 steps after 4 warm-up ones, so the prefilter's listed items
-# -- built from the previous detect -- are in steady state.)
+# -- built from the previous detect -- are in steady state; every bench run
+# here also takes bench.py's default --settle steps first, as the driver's
+# does, so the per-launch averages are those of a device at steady clocks.)
 # The profiled runs skip the bench's secondary lines (--no-variants): their
 # gated / cadence-skipped launches would otherwise dilute the per-launch
 # averages of the headline workload's kernels.
