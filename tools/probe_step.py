@@ -2,10 +2,12 @@
 the resident step of one rank of R -- its detect (own tiles, halo plan, halo
 tiles: bsa_sim_detect_rows' one-GPU halo mode), K2, K3 and K4' on its home
 rows -- with no collective (bsa_sim_probe_rank), timed as one batch of STEPS
-steps (one host synchronisation at its end, no stage events).  Collectives
+steps (one host synchronisation at its end, no stage events) after SETTLE
+untimed ones (the device at steady clocks, as bench.py's --settle).  Collectives
 (box all-gather, halo send / recv, gate all-reduce) are excluded: they need
 the 8-GPU node.  Prints every rank's ms per step and the slowest.
-Usage: python tools/probe_step.py [WORKLOAD [R [STEPS [RANK]]]]  (RANK: that rank of R only)"""
+Usage: python tools/probe_step.py [WORKLOAD [R [STEPS [RANK [SETTLE]]]]]  (RANK: that rank of R
+only, -1 all; SETTLE default 200)"""
 import json
 import os
 import sys
@@ -19,7 +21,8 @@ def main():
     name = sys.argv[1] if len(sys.argv) > 1 else 'global1m'
     R = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 40
-    only = int(sys.argv[4]) if len(sys.argv) > 4 else None
+    only = int(sys.argv[4]) if len(sys.argv) > 4 and int(sys.argv[4]) >= 0 else None
+    settle = int(sys.argv[5]) if len(sys.argv) > 5 else 200
     t = synth.workload(name)
     ctx = _lib.Context(0)
     ctx.set_timing_sample(0)
@@ -31,6 +34,9 @@ def main():
             ctx.sim_probe_rank(r, ranks)
             sim.step(5)                      # warm-up: this rank's plan / lists / buffers
             ctx.sync()
+            if settle > 0:
+                sim.step(settle)
+                ctx.sync()
             t0 = time.perf_counter()
             sim.step(steps)
             ctx.sync()
@@ -40,7 +46,7 @@ def main():
                                                                       st['row_end'], per[-1]), flush=True)
         out['R=%d' % ranks] = dict(slowest_ms=max(per), per_rank_ms=[round(x, 4) for x in per])
     ctx.sim_probe_rank(0, 1)
-    print(json.dumps(dict(workload=name, steps=steps, **out)), flush=True)
+    print(json.dumps(dict(workload=name, steps=steps, settle=settle, **out)), flush=True)
 
 
 if __name__ == '__main__':

@@ -5,6 +5,8 @@ own column tiles, the halo plan and the halo tiles it would receive
  -- for R = 1, 2, 4, 8, on the box100k and global1m workloads.
 Reports the slowest rank's stages (the step waits for it) and the largest
 halo (tiles a rank receives; bytes at 6 fp64 arrays x 512 rows per tile).
+Before each rank's detects the device runs BSA_SETTLE (200) untimed sim steps,
+so the stage events see it at steady clocks (bench.py's --settle).
 Usage: python tools/rowslice_probe.py [workload ...]"""
 import json
 import os
@@ -16,6 +18,7 @@ from bluesky_amd import _lib, resident, synth  # noqa: E402
 
 def main():
     names = sys.argv[1:] or ['box100k', 'global1m']
+    settle = int(os.environ.get('BSA_SETTLE', '200'))
     ctx = _lib.Context(0)
     ctx.set_timing_sample(1)
     for name in names:
@@ -29,6 +32,8 @@ def main():
                 rb, re = min(n, r * rpr), min(n, (r + 1) * rpr)
                 if re <= rb:
                     continue
+                if settle > 0:
+                    sim.step(settle)
                 for _ in range(2):
                     ctx.sim_detect_rows(rb, re)
                 ctx.timing_reset()
