@@ -2385,15 +2385,19 @@ static int next_events(Ctx *c, hipEvent_t **ev) {
 // reuse, BSA_FLAG_STAGE1_T0 or the BSA_STAGE1_T0 environment variable
 // home mode: K1b reads stored fp64 column records (else builds them from the
 // state arrays); BSA_HOME_REC=0/1 overrides (see detect_enqueue)
-// By the rows of the detect: a rank's K1b on stored records runs 4 waves per
-// SIMD (on records rebuilt from the state, 2); writing the records costs its
-// K0b 128 B per column.  Measured per rank (tools/rowslice_probe.py,
-// BSA_HOME_REC): one rank of 8 at 1M 0.1415 -> 0.1377 ms and of 4 / 8 at the
-// 100k box -2.4 / -2.3 us with records; 500k and 1M rows slower with them.
+// One rank below 163 840 rows stores them (K1b then runs fused into the
+// prefilter, on stored records; 500k and 1M rows are slower with them).  A
+// rank of a row-sharded step (halo mode) does not: its two K0b launches (own
+// and halo tiles) would write 128 B per column, and its K1b runs unfused
+// anyway.  Measured with the whole rank step (tools/probe_step.py, 200 settle
+// steps, slowest rank, BSA_HOME_REC=1 -> 0, A/B x 2): global1m R = 8 0.1175 /
+// 0.1175 -> 0.1115 / 0.1127 ms, box100k R = 8 0.0822 / 0.0827 -> 0.0806 /
+// 0.0800, R = 4 0.0966 / 0.0974 -> 0.0945 / 0.0939, R = 2 0.1092 / 0.1088 ->
+// 0.1109 / 0.1082 (an older detect-only probe with per-stage events had
+// favoured the records by ~4 us).
 bool home_records(const Ctx *c, int64_t nrows) {
   static const int home_rec_env = getenv("BSA_HOME_REC") ? atoi(getenv("BSA_HOME_REC")) : -1;
-  (void)c;
-  return home_rec_env >= 0 ? home_rec_env == 1 : nrows <= 163840;
+  return home_rec_env >= 0 ? home_rec_env == 1 : c->halo_mode == 0 && nrows <= 163840;
 }
 
 int stage1_mid(int flags, bool reuse, int kwik) {
