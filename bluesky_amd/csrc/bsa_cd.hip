@@ -2848,8 +2848,10 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // from 250k rows up, where 2 cost +15 us.  Round 5, with the longest-items
   // listing and the fused K1b: 1 piece from 64k rows up -- the 100k box
   // 0.1204 / 0.1212 -> 0.1185 / 0.1181 ms per step, one rank of 8 at 1M
-  // 0.1130 / 0.1117 -> 0.1118 / 0.1112; tools/gpu_ab.sh, BSA_PF_PIECES=1)
-  kn.pieces = nrows >= (1 << 16) ? 1 : (nrows >= (1 << 15) ? 2 : 4);
+  // 0.1130 / 0.1117 -> 0.1118 / 0.1112; tools/gpu_ab.sh, BSA_PF_PIECES=1),
+  // 2 from 16k rows: one rank of 4 at the 100k box (25k rows) 0.0942 / 0.0938
+  // -> 0.0925 / 0.0912 (tools/probe_step.py), of 8 (12.8k rows) stays at 4
+  kn.pieces = nrows >= (1 << 16) ? 1 : (nrows >= (1 << 14) ? 2 : 4);
   if (pieces_env == 1 || pieces_env == 2 || pieces_env == 4 || pieces_env == 8) kn.pieces = pieces_env;
   static const int pnear_env = getenv("BSA_PF_PIECES_NEAR") ? atoi(getenv("BSA_PF_PIECES_NEAR")) : 0;
   kn.pnear = kn.pieces;
