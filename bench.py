@@ -310,6 +310,56 @@ def geo_matrix_line(ctx, t, m=8192):
     return out
 
 
+def spawn_ranks(n, argv, cmd=None):
+    """``bench.py --gpus N`` (N > 1) started without torch.distributed.run
+    starts its N ranks itself: N fresh child processes, one per GPU, with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment.  This process has
+    not touched HIP (the library loads lazily, _lib.load), and the children are
+    started, never exec'd into.  Rank 0's JSON line reaches stdout through the
+    inherited descriptor; the exit code is the first failing rank's, and a
+    failing rank ends the others (they would wait in a collective forever)."""
+    import subprocess
+    base = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1',
+                MASTER_PORT=os.environ.get('MASTER_PORT', str(29500 + os.getpid() % 1000)),
+                TORCHELASTIC_RUN_ID='bench%d' % os.getpid())   # the RCCL id file's key (dist._rdv_path)
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + list(argv)
+    procs = [subprocess.Popen(cmd, env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rc = 0
+    try:
+        while None in [p.poll() for p in procs]:   # (a list: every child is polled)
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            time.sleep(0.1)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc or next((p.returncode for p in procs if p.returncode), 0)
+
+
+def resolve_world(gpus):
+    """(rank, world, local) of this process, or ('spawn', n) when this process
+    must start the ranks itself; a launcher world that disagrees with --gpus
+    is an error (a silent world-1 line for --gpus 8 would mislabel the run)."""
+    if 'WORLD_SIZE' not in os.environ:
+        if gpus > 1:
+            return 'spawn', gpus
+        return dist.env_rank_world()
+    rank, world, local = dist.env_rank_world()
+    if world != gpus:
+        raise SystemExit('bench.py: WORLD_SIZE=%d from the launcher but --gpus %d; refusing to run'
+                         % (world, gpus))
+    return rank, world, local
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -330,11 +380,19 @@ def main():
     ap.add_argument('--parity-steps', type=int, default=2,
                     help='with several GPUs: steps of the sharded run checked bitwise against one GPU first '
                          '(0: skip)')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='resolve the ranks (spawning them if needed), report them, touch no GPU (launcher test)')
     args = ap.parse_args()
 
-    rank, world, local = dist.env_rank_world()
-    if world != args.gpus:
-        world = max(world, 1)
+    rw = resolve_world(args.gpus)
+    if rw[0] == 'spawn':
+        sys.exit(spawn_ranks(rw[1], sys.argv[1:]))
+    rank, world, local = rw
+    if args.dry_run:
+        print('bench.py dry run: rank %d of %d (local %d)' % (rank, world, local), file=sys.stderr, flush=True)
+        if rank == 0:
+            print(json.dumps(dict(dry_run=True, n_gpus=world, rank=rank)), flush=True)
+        return
     ctx = _lib.Context(local)
     # HIP-event stage timing of one detect in TIMING_SAMPLE, inside the timed
     # region (each event record leaves a ~5 us gap before the next kernel)
@@ -355,8 +413,11 @@ def main():
             sys.exit(3)
     sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=args.cd_every),
                                ctx=ctx, rank=rank, world=world)
+    comm = ctx.comm_info()       # with RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice
+    if world > 1 and (comm['transport'] != 'rccl' or comm['ranks'] != world or comm['rank'] != rank):
+        raise SystemExit('bench.py: rank %d of %d but the communicator reports %s' % (rank, world, comm))
 
-    if args.settle > 0:          # same count on every rank (the halo step exchanges)
+    if args.settle > 0:         # same count on every rank (the halo step exchanges)
         sim.step(1)              # the first batch grows the candidate buffers and re-runs: keep it short
         sim.step(args.settle - 1)
         ctx.sync()
@@ -397,18 +458,30 @@ def main():
     # fused kernel -- the sweep itself is fp32); weighted by the fp32 / fp64 peak
     # ratio, both kinds of work count as time at the vector peak
     ex64 = pf.get('fp64_flops') if fused else None
+    n_exact = ts['candidates'] / max(ts['detects'], 1)      # K1b evaluates every candidate pair exactly
+    w64 = FP32_PEAK_TFLOPS / FP64_PEAK_TFLOPS
+    # algorithmic work: 9 fp32 flops per stage-1 test; fused, also
+    # 110 fp64 ops per exact evaluation -- each kind priced at its own vector
+    # peak (fp64 ops x the fp32 / fp64 peak ratio in fp32-equivalent flops)
+    alg = stage1 + (n_exact * OPS_PER_PAIR * w64 if fused else 0.0)
     roof = dict(bound='valu', kernel=('k_prefilter with K1b fused (fp32 packed VALU stage-1 test + fp64 exact '
                                       'evaluation, dominant)' if fused else
                                       'k_prefilter (fp32 packed VALU stage-1 test, dominant)'),
-                achieved=(stage1 + (ex64 or 0.0) * FP32_PEAK_TFLOPS / FP64_PEAK_TFLOPS) / pf_s / 1e12,
+                achieved=alg / pf_s / 1e12,
                 peak=FP32_PEAK_TFLOPS, unit='TFLOP/s' + (' (fp32-equivalent)' if fused else ''))
     roof['frac'] = roof['achieved'] / roof['peak']
     roof['stage1_TFLOPs'] = stage1 / pf_s / 1e12
+    roof['duration_us'] = pf_s * 1e6
     if fused:
-        roof['exact_fp64_flops'] = ex64
-        roof['note'] = ('fused launch: achieved = (stage-1 fp32 flops + K1b fp64 flops x %.1f) / the launch\'s '
-                        'event-timed duration; fp64 flops from the PMC passes of this library (None: not profiled)'
-                        % (FP32_PEAK_TFLOPS / FP64_PEAK_TFLOPS))
+        roof['exact_evaluations'] = n_exact
+        roof['exact_fp64_flops_pmc'] = ex64
+        pmc_ach = (stage1 + ex64 * w64) / pf_s / 1e12 if ex64 else None
+        roof['achieved_pmc_flops'] = pmc_ach
+        roof['frac_pmc_flops'] = pmc_ach / FP32_PEAK_TFLOPS if pmc_ach else None
+        roof['note'] = ('fused launch: achieved = (stage-1 tests x %d fp32 flops + exact evaluations x %d fp64 ops '
+                        '(SURVEY 8d) x %.1f) / the launch\'s event-timed duration; *_pmc_flops: the same with the '
+                        'PMC-counted fp64 flops of the launch (ocml expansions included) instead of the 110 '
+                        'algorithmic ops' % (PF_FLOPS_PER_PAIR, OPS_PER_PAIR, w64))
     roof['traffic'] = (pf['hbm_read_bytes'] + pf['hbm_write_bytes']) if 'hbm_write_bytes' in pf else None
     roof['traffic_source'] = ('rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch, from_profile (the '
                               'committed passes of this bench on this very library)' if pmc else
@@ -475,11 +548,14 @@ def main():
                tile_reuse_rank0=tile_reuse,
                tile_pairs_rank0=ts['tiles'] / max(ts['detects'], 1),
                n_conf=int(counts[0]), n_los=int(counts[1]), n_candidates=int(counts[2]),
-               cd_effective_frac_fp64=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),
+               # N^2 x 110 fp64 ops / fp64 peak: what culling buys over evaluating every
+               # pair at the ALUs' peak -- a property of the algorithm, not a fraction of peak
+               n2_equivalent_speedup_over_fp64_peak=value * OPS_PER_PAIR / (FP64_PEAK_TFLOPS * 1e12),
                propagation=propagation, exact_fp64=exact_fp64,
                build=dict(lib_path=os.path.relpath(lib_path, REPO), lib_sha256=lib_sha),
                parity_vs_world1=None if parity is None else parity['ok'],
-               parity=parity)
+               parity=parity,
+               rccl_ranks=comm['ranks'] if comm['transport'] == 'rccl' else None, comm=comm)
     if world > 1:   # the halo exchange that replaced the full-state all-gather
         out['halo'] = halo_line(ctx, sim, cd_steps)
     if world > 1:   # C2: the last CD call's pair lists of all ranks to rank 0's host

@@ -150,6 +150,7 @@ SIGNATURES.update({
     'bsa_comm_init': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     'bsa_comm_allreduce_max': (ctypes.c_int, [_vp, _c_dp, ctypes.c_int]),
     'bsa_comm_allreduce_sum': (ctypes.c_int, [_vp, _c_dp, ctypes.c_int]),
+    'bsa_comm_info': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     'bsa_sim_init': (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.POINTER(SimState),
                                     ctypes.POINTER(SimParams)]),
     'bsa_sim_step': (ctypes.c_int, [_vp, ctypes.c_int]),
@@ -546,6 +547,14 @@ class Context:
         self.check(self.lib.bsa_comm_init_group(self.h, group.h, int(rank)), 'bsa_comm_init_group')
         self.comm_rank_world = (rank, group.nranks)
         self.gen += 1
+
+    def comm_info(self):
+        """The communicator as its transport reports it (bsa_comm_info): with
+        RCCL, ranks / rank / device are ncclCommCount / ncclCommUserRank /
+        ncclCommCuDevice."""
+        v = (ctypes.c_int * 4)()
+        self.check(self.lib.bsa_comm_info(self.h, v), 'bsa_comm_info')
+        return dict(transport=('none', 'rccl', 'group')[v[0]], ranks=v[1], rank=v[2], device=v[3])
 
     def gather_pairs(self, root=0, with_dcpa=False):
         """C2: every rank's last detect gathered to ``root`` in rank order

@@ -2410,7 +2410,7 @@ static SoA6 soa(const DevBuf *a) {
               (const double *)a[3].p, (const double *)a[4].p, (const double *)a[5].p};
 }
 
-int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla) {
+int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla, unsigned long long nf_epoch) {
   const int64_t n = c->n;
   if (n <= 0) return 0;
   const int nct = (int)((n + kTile - 1) / kTile);
@@ -2429,7 +2429,7 @@ int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla) {
                      (const unsigned *)c->h2id.p, 1, 0, own, own, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, stage1_mid(0, false, 0),
                      ReuseParams{}, fb, zs, 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, TprCheck{},
-                     NfArgs{});
+                     NfArgs{nf_epoch ? (unsigned long long *)c->nonfin.p : nullptr, nf_epoch, nullptr});
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -2548,7 +2548,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   c->sim_prepped = false;
   // non-finite tcpa inputs: this detect's epoch (the prepped records carry K4''s)
   if (!nonfin_word(c)) return -1;
-  NfArgs nfa{(unsigned long long *)c->nonfin.p, prepped ? c->nf_prep_epoch : ++c->nf_counter, nullptr};
+  NfArgs nfa{(unsigned long long *)c->nonfin.p,
+             prepped ? c->nf_prep_epoch : (c->nf_force_epoch ? c->nf_force_epoch : ++c->nf_counter), nullptr};
   // K0z skipped: the last detect's K2 (k_rank_rows) zeroed this detect's
   // counter block (double-buffered), dequeue words and per-row counts, and
   // writes inconf / tcpamax of every row itself; the prepped tile boxes are
@@ -3050,29 +3051,25 @@ int detect_finish(Ctx *c, bool *retry) {
     return 0;
   }
   c->zeroed_rows = -1;  // (a retry zeroes everything again; so does any host-side recovery)
+  // every cause of a retry is fixed before the one retry (not one per retry)
   if (h.fuse_ovf) {  // a wave flushed more blocks than the fused K1b records: K1b as its own launch
     c->fuse_skip = true;
     c->fuse_retries++;
     *retry = true;
-    return 0;
   }
   if (h.k2_demand) {  // a K2 row bucket was full: nothing was written (the
     grow_k2_bucket(c, h.k2_demand);  // candidate list itself is complete: a reusable one stays valid)
     *retry = true;
-    return 0;
   }
-  unsigned long long worst = 0, total = 0;
-  for (int q = 0; q < kCandShards; ++q) {
-    worst = std::max(worst, h.cshard[q][0]);
-    total += h.cshard[q][0];
-  }
-  total = h.cand;  // (the list is dense: the shard counts equal the candidates written, K2 summed them)
+  unsigned long long worst = 0;
+  for (int q = 0; q < kCandShards; ++q) worst = std::max(worst, h.cshard[q][0]);
+  const unsigned long long total = h.cand;  // (the list is dense: K2 summed the shard counts)
   if (worst > c->cand_cap / kCandShards) {
     c->cand_cap = (unsigned long long)kCandShards * (worst + worst / 4 + 1024);
     c->reuse_valid = false;
     *retry = true;
-    return 0;
   }
+  if (*retry) return 0;
   const int64_t nrows = c->last_re - c->last_rb;
   c->last_cand = (int64_t)total;
   c->last_tiles = (int64_t)h.tiles;

@@ -623,4 +623,26 @@ int bsa_comm_allreduce_sum(bsa_ctx *cc, double *values, int count) {
   return bsa::comm_allreduce_host(c, values, count, false);
 }
 
+int bsa_comm_info(bsa_ctx *cc, int *info4) {
+  Ctx *c = (Ctx *)cc;
+  if (!c || !info4) return -1;
+  info4[0] = 0;
+  info4[1] = c->nranks;
+  info4[2] = c->rank;
+  info4[3] = c->device;
+  if (c->comm) {  // RCCL's own view of the communicator
+    int n = 0, r = 0, d = 0;
+    BSA_NCCL(c, ncclCommCount((ncclComm_t)c->comm, &n));
+    BSA_NCCL(c, ncclCommUserRank((ncclComm_t)c->comm, &r));
+    BSA_NCCL(c, ncclCommCuDevice((ncclComm_t)c->comm, &d));
+    info4[0] = 1;
+    info4[1] = n;
+    info4[2] = r;
+    info4[3] = d;
+  } else if (c->group) {
+    info4[0] = 2;
+  }
+  return 0;
+}
+
 }  // extern "C"

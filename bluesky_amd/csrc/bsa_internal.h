@@ -110,12 +110,12 @@ constexpr int kEvSets = 4096;    // detect timing event sets kept between resets
 #define BSA_CAND_SHARDS 8
 #endif
 constexpr int kCandShards = BSA_CAND_SHARDS;  // candidate list shards (one counter each, 128 B apart)
-constexpr unsigned kDangling = 0xffffffffu;
+constexpr unsigned kDangling = 0xffffffffu;  // resopairs column of a deleted intruder (sorts last in a row)
 // gate[0] of the resident step (all-reduced max over ranks): 0 nothing, 1 a
 // non-finite tcpa input in some rank's columns (every row's tcpamax is NaN),
 // >= 2 abort the step (2 candidate / row-bucket overflow, 3 resopairs overflow)
 constexpr unsigned long long kGateNonfinite = 1, kGateOverflow = 2, kGateBkOverflow = 3;
-constexpr unsigned long long kNanBits = 0x7ff8000000000000ull;  // (a quiet NaN)  // resopairs column of a deleted intruder (sorts last in a row)
+constexpr unsigned long long kNanBits = 0x7ff8000000000000ull;  // (a quiet NaN)
 
 // counters block on the device
 constexpr int kFuseRecsMax = 64;  // fused K1b: mid-sweep flush records per prefilter wave (LDS)
@@ -323,6 +323,8 @@ struct Ctx {
   DevBuf nonfin;
   DevBuf rownf;  // rows of their own (not columns): per row (index order), its position / velocity is not finite
   unsigned long long nf_counter = 0, nf_prep_epoch = 0;  // epochs (K0b: a new one; K4' prep: the next detect's)
+  unsigned long long nf_force_epoch = 0;  // != 0: the epoch the next detects take (bsa_sim_detect_rows: the
+                                         // records of every tile, prepared first, carry it)
   DevBuf sim_ctl;  // [0,16) gate {abort / non-finite, P}; [16,20) sticky abort; [24,32) steps done;
                    // [32,40) resopairs demand on a bookkeeping overflow; [40,48) pair-key
                    // block demand (several ranks)
@@ -462,7 +464,9 @@ const uint8_t *halo_present(const Ctx *c);  // the received-tile mask of the las
 const unsigned *halo_list_count(const Ctx *c);  // the probe's halo list length (device), else NULL
 // K0b over every column tile (fused boxes, no per-detect zeroing): the halo
 // plan's view of all tile boxes when every rank's state is on this GPU (bsa_cd.hip)
-int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla);
+// every column tile's records and boxes (one K0b); nf_epoch != 0: non-finite
+// columns store it into Ctx::nonfin (the detect that takes that epoch sees them)
+int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla, unsigned long long nf_epoch = 0);
 
 // exclusive prefix sum of n words, one launch (bsa_cd.hip)
 int scan_excl(Ctx *c, const unsigned *in, unsigned *out, int n);

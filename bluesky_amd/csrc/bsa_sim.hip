@@ -918,12 +918,19 @@ int bsa_sim_detect_rows(bsa_ctx *cc, int64_t row_begin, int64_t row_end, int64_t
   if (bsa::sim_gather(c)) return -1;
   // as one rank of a sharded step: own tiles, halo plan, halo tiles (the
   // boxes of every tile, which the other ranks would send, are prepared
-  // first, outside the detect's timed stages)
-  if (bsa::prep_all_tiles(c, c->simp.rpz, c->simp.hpz, c->simp.tla)) return -1;
+  // first, outside the detect's timed stages).  Those records carry the
+  // detect's non-finite epoch: a NaN column outside this share's halo makes
+  // every row's tcpamax NaN, as in the whole detect (StateBasedCD.py:90; the
+  // sharded step carries it through the gate all-reduce instead)
+  if (!bsa::nonfin_word(c)) return -1;
+  const unsigned long long e = ++c->nf_counter;
+  if (bsa::prep_all_tiles(c, c->simp.rpz, c->simp.hpz, c->simp.tla, e)) return -1;
   const int hm = c->halo_mode;
   c->halo_mode = 2;
   c->det_home = true;
+  c->nf_force_epoch = e;  // (retries of the detect too)
   const int r = bsa::detect(c, c->simp.rpz, c->simp.hpz, c->simp.tla, 0, row_begin, row_end, n_conf, n_los);
+  c->nf_force_epoch = 0;
   c->det_home = false;
   c->halo_mode = hm;
   return r;

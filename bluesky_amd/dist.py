@@ -94,6 +94,7 @@ def init_comm(ctx, rank, world):
 
 
 PAIR_KEYS = {'ci': ('ci', 'cj', 'qdr', 'dist', 'tcpa', 'tinconf', 'dcpa'), 'li': ('li', 'lj')}
+ROW_KEYS = ('inconf', 'tcpamax')   # per-row arrays, in each rank's row order
 
 
 def merge_rank_pairs(parts, rows=None):
@@ -102,7 +103,14 @@ def merge_rank_pairs(parts, rows=None):
     into the global row-major result.  ``rows``: each rank's row ids (the
     per-row arrays inconf / tcpamax are in that order); their union must be
     every row once.  Pair arrays are concatenated in rank order and stably
-    sorted by row index (a row belongs to one rank, so its pairs stay in order)."""
+    sorted by row index (a row belongs to one rank, so its pairs stay in order).
+    Keys other than PAIR_KEYS' and ROW_KEYS are an error; a key some rank left
+    as None is left out."""
+    known = set(ROW_KEYS).union(*PAIR_KEYS.values())
+    for p in parts:
+        extra = set(p) - known
+        if extra:
+            raise ValueError('merge_rank_pairs: unknown keys %s' % sorted(extra))
     out = {}
     for lead, keys in PAIR_KEYS.items():
         if lead not in parts[0]:
@@ -116,9 +124,11 @@ def merge_rank_pairs(parts, rows=None):
         n = len(ids)
         if not np.array_equal(np.sort(ids), np.arange(n)):
             raise ValueError('rank rows do not partition 0..%d' % (n - 1))
-        for k in parts[0]:
-            if k in out or parts[0][k] is None or len(parts[0][k]) != len(rows[0]):
+        for k in ROW_KEYS:
+            if not all(p.get(k) is not None for p in parts):
                 continue
+            if any(len(p[k]) != len(r) for p, r in zip(parts, rows)):
+                raise ValueError('merge_rank_pairs: %s does not have one entry per rank row' % k)
             v = np.concatenate([p[k] for p in parts])
             full = np.empty(n, dtype=v.dtype)
             full[ids] = v

@@ -328,6 +328,11 @@ int bsa_comm_init_group(bsa_ctx *ctx, bsa_group *g, int rank);
 int bsa_comm_allreduce_max(bsa_ctx *ctx, double *values, int count);
 /* Collective: element-wise sum of `count` host doubles over all ranks. */
 int bsa_comm_allreduce_sum(bsa_ctx *ctx, double *values, int count);
+/* The communicator as its transport sees it (not collective): info4 =
+ * {transport (0 none, 1 RCCL, 2 in-process group), ranks, this rank, device}.
+ * With RCCL the ranks / rank / device come from RCCL itself (ncclCommCount,
+ * ncclCommUserRank, ncclCommCuDevice), so a report of N ranks is RCCL's. */
+int bsa_comm_info(bsa_ctx *ctx, int *info4);
 
 /* C2 pair gather ("pair lists are gathered to the host").
  * Collective over the ranks' last detect (bsa_detect on each rank's row

@@ -97,6 +97,21 @@ def test_merge_rank_pairs_interleaved_rows():
         assert np.array_equal(merged[k], full[k]), k
 
 
+def test_merge_rank_pairs_keys_are_explicit():
+    """Per-row arrays are named (ROW_KEYS), never inferred from a length: an
+    unknown key, or a per-row array of the wrong length, is an error, and a
+    pair array some rank left as None is left out rather than scattered."""
+    t = synth.box(300, 30.0, seed=3)
+    rows = [np.arange(0, 300, 2), np.arange(1, 300, 2)]
+    parts = [ocd.detect_arrays(t, t, synth.RPZ, synth.HPZ, synth.TLOOKAHEAD, rows=r) for r in rows]
+    with pytest.raises(ValueError, match='unknown keys'):
+        dist.merge_rank_pairs([dict(p, extra=np.zeros(len(r))) for p, r in zip(parts, rows)], rows=rows)
+    with pytest.raises(ValueError, match='one entry per rank row'):
+        dist.merge_rank_pairs([dict(p, inconf=p['inconf'][:-1]) for p in parts], rows=rows)
+    half = [dict(parts[0], dcpa=None), dict(parts[1], dcpa=np.zeros(len(parts[1]['ci'])))]
+    assert 'dcpa' not in dist.merge_rank_pairs(half, rows=rows)
+
+
 def _rdv_worker(rank, world, rdv_dir, q):
     os.environ['BSACCEL_RDV_DIR'] = rdv_dir
     uid = dist.rendezvous_unique_id(rank, world, lambda: bytes(range(128)), timeout=60)

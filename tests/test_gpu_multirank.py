@@ -498,6 +498,38 @@ def test_halo_probe_shares_equal_full_detect(ctx):
     assert sim.stats()['steps'] == 0
 
 
+def test_halo_probe_shares_nonfinite_column_outside_halo(ctx):
+    """a rank's share (bsa_sim_detect_rows, halo mode) equals the
+    whole detect also when the one non-finite column is outside the share's
+    halo: tcpamax = max_j(tcpa * swconfl) is NaN on EVERY row
+    (StateBasedCD.py:90), whichever tiles the share holds."""
+    t = synth.box(20000, 1000.0, seed=73)
+    t.gs[5] = np.nan
+    n, R = t.ntraf, 8
+    c2 = _lib.Context(0)
+    try:
+        full = statebased.detect_indices(t, t, RPZ, HPZ, TLA, ctx=c2)
+    finally:
+        c2.close()
+    assert np.isnan(full['tcpamax']).all() and len(full['ci']) > 0
+    resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
+    rpr = ((n + R - 1) // R + 511) // 512 * 512
+    nct = (n + 511) // 512
+    parts, partial = [], 0
+    for r in range(R):
+        rb, re = r * rpr, min(n, (r + 1) * rpr)
+        nc, nl = ctx.sim_detect_rows(rb, re)
+        got = ctx.fetch_pairs(nc, nl)
+        parts.append(got)
+        assert np.isnan(got['tcpamax']).all(), r
+        partial += ctx.sim_halo_stats()['tiles'] < nct - (re - rb + 511) // 512
+    assert partial == R          # no share holds every tile: the NaN column is outside some halos
+    i = np.concatenate([p['ci'] for p in parts])
+    j = np.concatenate([p['cj'] for p in parts])
+    o = np.lexsort((j, i))
+    assert np.array_equal(i[o], full['ci']) and np.array_equal(j[o], full['cj'])
+
+
 # ---------------------------------------------------------------- create / delete while sharded
 def test_sharded_create_delete_equal_world1(ctx):
     """Traffic.delete / create during a sharded run (traffic.py:192-378,
