@@ -413,7 +413,9 @@ def main():
             sys.exit(3)
     sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=args.cd_every),
                                ctx=ctx, rank=rank, world=world)
-    comm = ctx.comm_info()       # with RCCL: ncclCommCount / ncclCommUserRank / ncclCommCuDevice
+    comm = (ctx.comm_info() if hasattr(ctx.lib, 'bsa_comm_info') else   # with RCCL: ncclCommCount /
+            dict(transport='unknown (older build, BSACCEL_AB=1)', ranks=world, rank=rank, device=local))
+    # ncclCommUserRank / ncclCommCuDevice
     if world > 1 and (comm['transport'] != 'rccl' or comm['ranks'] != world or comm['rank'] != rank):
         raise SystemExit('bench.py: rank %d of %d but the communicator reports %s' % (rank, world, comm))
 

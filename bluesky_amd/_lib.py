@@ -59,6 +59,8 @@ SIGNATURES = {
     'bsa_reuse_stats': (ctypes.c_int, [_vp, _c_i64p, _c_i64p]),
     'bsa_set_tile_reuse': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double, ctypes.c_double]),
     'bsa_tile_reuse_stats': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_set_hk': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double]),
+    'bsa_hk_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_reuse_budget_use': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_timing_reset': (ctypes.c_int, [_vp]),
@@ -465,6 +467,16 @@ class Context:
         v = np.zeros(2, np.int64)
         self.check(self.lib.bsa_tile_reuse_stats(self.h, ptr(v, _c_i64p)), 'bsa_tile_reuse_stats')
         return dict(builds=int(v[0]), detects=int(v[1]))
+
+    def set_hk(self, on=True, f=0.75):
+        """Host-known tile-pair list decisions of the resident step (bsa_set_hk)."""
+        self.check(self.lib.bsa_set_hk(self.h, 1 if on else 0, float(f)), 'bsa_set_hk')
+
+    def hk_stats(self):
+        v = np.zeros(6, np.int64)
+        self.check(self.lib.bsa_hk_stats(self.h, ptr(v, _c_i64p)), 'bsa_hk_stats')
+        return dict(keeps=int(v[0]), builds=int(v[1]), waits=int(v[2]), stale_aborts=int(v[3]),
+                    cooldown=int(v[4]), on=bool(v[5]))
 
     def reuse_stats(self):
         b, d = ctypes.c_int64(), ctypes.c_int64()

@@ -25,6 +25,9 @@
 // of separation, and K1b evaluates the survivors exactly.
 #include <hipcub/hipcub.hpp>
 
+#include <chrono>
+#include <thread>
+
 #include "bsa_box.h"
 #include "bsa_geo_math.h"
 #include "bsa_halo.h"
@@ -267,6 +270,10 @@ struct TprCheck {
   const PFRec *snap;
   unsigned *flag;
   float dx, ds, dv;
+  // HK (Ctx::hk_*): the prediction word of this detect, raised when a record
+  // left f x every budget (the list is rebuilt two detects on), or NULL
+  unsigned long long *pred;
+  float f;
 };
 
 // Column records: intruder[j] geometry, own[j] velocity / altitude.
@@ -286,21 +293,27 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(6))) void
                                                      PFVel *__restrict__ PV, float4 *__restrict__ PP, int mid,
                                                      ReuseParams rz, FusedBoxes fb, ZeroArgs zs, int tile_base,
                                                      const int *__restrict__ tile_list, HaloUnpack hu,
-                                                     Counters *__restrict__ hcnt, TprCheck tck, NfArgs nf) {
+                                                     Counters *__restrict__ hcnt, TprCheck tck, NfArgs nf, int nown) {
   __shared__ TileBox fgb[kTile / 64];
   // K0z (fused): nothing here reads that state
   if (zs.cnt) zero_state(zs, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
-  int tile = hu.count && blockIdx.x >= *hu.count ? -1
-             : (tile_list ? tile_list[blockIdx.x] : tile_base + (int)blockIdx.x);
+  // workgroups [0, nown): tiles tile_base + b; the rest: slots b - nown of
+  // tile_list (the halo K0b's received tiles; one launch with the own tiles
+  // when the host kept the plan, HK)
+  const int b = (int)blockIdx.x;
+  const bool mine = b < nown;
+  const int slot = b - nown;
+  int tile = mine ? tile_base + b : (hu.count && slot >= (int)*hu.count ? -1 : tile_list[slot]);
   // halo exchange: this slot's received tile rows first (each thread writes
   // the row it prepares below), checked against this rank's plan
-  if (hu.rbuf) tile = halo_unpack_tile(hu, (int)blockIdx.x, tile, hcnt);
+  if (!mine && hu.rbuf) tile = halo_unpack_tile(hu, slot, tile, hcnt);
   if (tile < 0) return;  // (the whole workgroup: no barrier is skipped by part of it)
   const int k = tile * kTile + (int)threadIdx.x;
   bool over = false;       // reuse: this aircraft overran a budget
   float use_h = 0.f, use_v = 0.f;
   PFRec pk{}, pb{};        // this lane's record (the fused boxes take it from registers), its build's
-  if (tck.snap && k < cnt) pb = tck.snap[k];
+  const bool check = tck.snap && mine;  // (the own tiles' records: the halo tiles' are their owners' to check)
+  if (check && k < cnt) pb = tck.snap[k];
   if (k < cnt) {
     const int o = presorted ? k : (int)perm[k];
     const double tlap = tla > 0.0 ? tla : 0.0;
@@ -381,9 +394,13 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(6))) void
       rz.use[2 * wv + 1] = use_v;
     }
   }
-  if (tck.snap) {  // plan reuse: one flag store per wave whose records left their budgets
+  if (check) {  // plan reuse: one flag store per wave whose records left their budgets
     const bool out = k < cnt && !pf_within(pk, pb, tck.dx, tck.ds, tck.dv);
     if (__ballot(out) && (threadIdx.x & 63) == 0) *tck.flag = 1u;
+    if (tck.pred) {  // HK: ... or f x the budgets (a rebuild two detects on)
+      const bool near = k < cnt && !pf_within(pk, pb, tck.f * tck.dx, tck.f * tck.ds, tck.f * tck.dv);
+      if (__ballot(near) && (threadIdx.x & 63) == 0) *tck.pred = 1ull;
+    }
   }
   // K0c (fused): this thread wrote PC[k] above, every thread reaches the barrier
   if (fb.gbox) tile_boxes_v(cnt, tile, pk, fgb, fb.sbox, fb.gbox, fb.tbox);
@@ -603,6 +620,12 @@ struct TprArgs {
   const PFRec *pc;  // this detect's column records (rows = columns)
   PFRec *snap;
   unsigned *myflag;  // several ranks / the probe: the rank's rebuild flag, cleared here (the plan read it)
+  // HK keep (the host kept the list; K0d is not launched): the prefilter takes
+  // the kept item counts from ctl[1], ctl[2] and aborts the step
+  // (Counters::tpr_stale) when the records' violation word vflag is set
+  int keep;
+  const unsigned *vflag;
+  unsigned long long *stale;  // ... and records it for the batch (sim_ctl, kSimCtlStale)
 };
 
 // Halo mode (hl != NULL): the columns are this rank's own tiles [p0, p1) and
@@ -1060,8 +1083,19 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   __shared__ unsigned char sgs[PF_WAVES][kSubsPerBatch];  // the next batch's sub-groups (tile-local)
   __shared__ uint2 cst[PF_WAVES][PF_RES];   // staged candidates (row, column) of the wave
   if (build && !build[0]) return;  // reused candidate list
+  if (tp.keep && *tp.vflag != 0u) {  // HK: a record left the kept list's budgets -- the step re-runs
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      cnt->tpr_stale = 1ull;
+      if (tp.stale) *tp.stale = 1ull;  // (the batch's own record: later detects' counters may not show it)
+    }
+    // (the next detect's listed-item counts start at zero as in a sweep:
+    // this detect's K2 still lists items for it, and a stale count would
+    // sweep old slots twice)
+    if (hv.list[0] && blockIdx.x == 0 && threadIdx.x < 2) hv.count_next[threadIdx.x] = 0u;
+    return;
+  }
   if (tp.ctl && blockIdx.x == 0 && threadIdx.x == 0) {  // tile-pair list reuse: K0d is complete here
-    if (tp.force || tp.ctl[0] != 0ull) {  // it built: keep the list's counts, clear the flag
+    if (!tp.keep && (tp.force || tp.ctl[0] != 0ull)) {  // it built: keep the list's counts, clear the flag
       tp.ctl[1] = work[1];
       tp.ctl[2] = work[2];
       tp.ctl[0] = 0ull;
@@ -1109,8 +1143,9 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   // (32-bit unit arithmetic, powers of two: the 64-bit forms with a run-time
   // divisor expanded into ~50 scalar instructions per unit)
   const unsigned lnear = (unsigned)__builtin_ctz((unsigned)kn.pnear), lpc = (unsigned)__builtin_ctz((unsigned)kn.pieces);
-  const unsigned inear = (unsigned)work[1], unear = inear << lnear;
-  const unsigned nfar = (unsigned)work[2];
+  // (HK keep: no K0d copied the kept list's counts into the dequeue words)
+  const unsigned inear = (unsigned)(tp.keep ? tp.ctl[1] : work[1]), unear = inear << lnear;
+  const unsigned nfar = (unsigned)(tp.keep ? tp.ctl[2] : work[2]);
   const unsigned nreg = unear + (nfar << lpc);
   unsigned nh0 = 0, nh1 = 0;
   if (hv.list[0]) {
@@ -1692,6 +1727,7 @@ __device__ __forceinline__ bool cand_overflow(const Counters *cnt, unsigned long
   bool o = cnt->k2_demand != 0;  // a K2 row bucket was full: retried with wider buckets
   o |= cnt->halo_ovf != 0 || cnt->halo_miss != 0;  // halo tiles missing: the step is re-run
   o |= cnt->fuse_ovf != 0;  // fused K1b out of flush records: re-run with K1b's own launch
+  o |= cnt->tpr_stale != 0;  // a host-kept tile-pair list that no longer covers the records: re-run, rebuilt
 #pragma unroll
   for (int q = 0; q < kCandShards; ++q) o |= cnt->cshard[q][0] > ccap;
   return o;
@@ -1945,6 +1981,7 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
     if (gate) {
       gate[0] = ovf ? kGateOverflow : (nfcol ? kGateNonfinite : 0);
       gate[1] = ovf ? 0 : P;
+      gate[2] = 1ull;  // (HK: no prediction from this K2 form -- rebuild, the safe side)
     }
   }
   if (ovf) return;
@@ -2044,7 +2081,7 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
                                                          unsigned long long *__restrict__ tcpamax_bits,
                                                          Counters *__restrict__ cnext,
                                                          unsigned long long *__restrict__ wnext, K24Args ka,
-                                                         NfArgs nf) {
+                                                         NfArgs nf, unsigned long long *__restrict__ hkp) {
   constexpr int W = kRankThreads / 64;
   __shared__ unsigned red[4][W];
   __shared__ unsigned soff[2][kRankRows + 1];  // the block's rows' exclusive offsets (conf, LoS), + total
@@ -2134,7 +2171,13 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
     if (gate) {
       gate[0] = ovf ? kGateOverflow : (nfcol ? kGateNonfinite : 0);
       gate[1] = ovf ? 0 : P;
+      gate[2] = hkp && *hkp ? 1ull : 0ull;  // HK: this detect's prediction, all-reduced with the gate
     }
+    if (hkp) *hkp = 0ull;  // (the word's next writer is two detects on)
+    // HK, fused K4' (one rank): this detect's prediction to the host, before
+    // any return (the host may be waiting for it); here rather than at the
+    // kernel's start, where its loads cost every workgroup ~5 us
+    if (K24) hk_publish(ka.pub, [&] { return ovf || *ka.d.sticky != 0u; });
   }
   // fused K4' (K24): an aborted step (this detect overflowed, or an earlier
   // step of the batch did) keeps every row's state -- including the double
@@ -2285,6 +2328,11 @@ __global__ __launch_bounds__(kRankThreads) void k_rank_rows(int nrows, Counters 
       if (ka.pa.snap) {
         const bool outb = live && !pf_within(pr, pb, ka.pa.dx, ka.pa.ds, ka.pa.dv);
         if (__ballot(outb) && lane == 0) ka.pa.tpr_ctl[0] = 1ull;
+        if (ka.pa.pred) {  // HK: ... or f x the budgets (a rebuild two detects on)
+          const float f = ka.pa.pf;
+          const bool nearb = live && !pf_within(pr, pb, f * ka.pa.dx, f * ka.pa.ds, f * ka.pa.dv);
+          if (__ballot(nearb) && lane == 0) *ka.pa.pred = 1ull;
+        }
       }
     } else if (live) {
       pilot_kin_row<true, false>(rb, k, ka.simdt, ka.winddim, ka.vwn, ka.vwe, ka.wf, ka.d, mv, ka.mp, ka.pa);
@@ -2429,7 +2477,7 @@ int prep_all_tiles(Ctx *c, double rpz, double hpz, double tla, unsigned long lon
                      (const unsigned *)c->h2id.p, 1, 0, own, own, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                      (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, stage1_mid(0, false, 0),
                      ReuseParams{}, fb, zs, 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, TprCheck{},
-                     NfArgs{nf_epoch ? (unsigned long long *)c->nonfin.p : nullptr, nf_epoch, nullptr});
+                     NfArgs{nf_epoch ? (unsigned long long *)c->nonfin.p : nullptr, nf_epoch, nullptr}, nct);
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -2458,12 +2506,13 @@ struct RankLaunch {
   Counters *cnext;
   unsigned long long *wnext;
   NfArgs nf;
+  unsigned long long *hkp;  // HK: the prediction word K2 moves into gate[2] (NULL: none / fused K4' publishes it)
 };
 static int rank_launch(Ctx *c, const RankLaunch &a, bool k24, const K24Args &ka) {
   const auto K = k24 ? k_rank_rows<true> : k_rank_rows<false>;
   hipLaunchKernelGGL(K, dim3(a.grid), dim3(kRankThreads), 0, c->stream, a.nrows, a.cnt, a.cap, a.rowoff, a.rowcnt,
                      a.kb, a.B, a.cpay, a.rb, a.ci, a.cj, a.out, a.li, a.lj, a.stats, a.gate, a.build, a.mf,
-                     a.inconf, a.tcpamax, a.cnext, a.wnext, ka, a.nf);
+                     a.inconf, a.tcpamax, a.cnext, a.wnext, ka, a.nf, k24 ? nullptr : a.hkp);
   BSA_HIP(c, hipGetLastError());
   return 0;
 }
@@ -2476,6 +2525,32 @@ bool nonfin_word(Ctx *c) {
     return false;
   }
   return true;
+}
+
+// HK: wait until the step of detect m published its prediction (ring slot m
+// % kHkRing holds (m + 1) << 2 | flags); the device runs the step before the
+// one being enqueued, so this normally returns at once or after part of a step
+static int hk_wait(Ctx *c, int64_t m, unsigned long long *v) {
+  volatile unsigned long long *p = c->hk_host + (m % kHkRing);
+  const unsigned long long want = (unsigned long long)(m + 1);
+  if ((*p >> 2) == want) {
+    *v = *p;
+    return 0;
+  }
+  c->hk_waits++;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0;; ++spin) {
+    const unsigned long long x = __atomic_load_n(p, __ATOMIC_ACQUIRE);
+    if ((x >> 2) == want) {
+      *v = x;
+      return 0;
+    }
+    if ((spin & 1023u) == 1023u) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+        return fail(c, "HK: the device did not publish detect %lld's prediction within 60 s", (long long)m);
+      std::this_thread::yield();
+    }
+  }
 }
 
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
@@ -2556,8 +2631,71 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // derived from the group boxes by K0d (direct form only)
   static const bool tp_super = getenv("BSA_TP_SUPER") && atoi(getenv("BSA_TP_SUPER")) == 1;  // (A/B)
   static const bool zero_env = getenv("BSA_K0Z") && atoi(getenv("BSA_K0Z")) == 1;           // (A/B)
-  const bool nozero = prepped && !zero_env && !tp_super && c->k2_bucket > 0 && c->zeroed_rows == nrows &&
-                      (n + kTile - 1) / kTile <= kTPDirectMax;
+  // ---- tile-pair list reuse: the resident step's detects of
+  // a rank's rows -- one rank: records prepared (and checked) by K4'; several
+  // ranks or the probe: the halo plan is kept with the list.  Any other detect
+  // of this context invalidates the kept list.  Halo mode: K0d sweeps the
+  // present column tiles only (own + received, the flat halo list;
+  // BSA_TP_HALO_ALL=1 sweeps all tiles for A/B).
+  static const bool tp_all = getenv("BSA_TP_HALO_ALL") && atoi(getenv("BSA_TP_HALO_ALL")) == 1;
+  const bool tp_list = halo && !tp_all && !tp_super;
+  static const bool tpr_env = !(getenv("BSA_TPR") && atoi(getenv("BSA_TPR")) == 0);
+  const bool tpr = tpr_env && c->tpr_on && home && !reuse && flags == 0 && !tp_super &&
+                   ((!halo && prepped && (n + kTile - 1) / kTile <= kTPDirectMax) || tp_list);
+  const double tkey[6] = {rpz, hpz, tla, (double)mid, (double)rb, (double)re};
+  const bool tvalid = tpr && c->tpr_valid && c->tpr_n == n && memcmp(tkey, c->tpr_key, sizeof tkey) == 0;
+  // Who decides a rebuild.  HK (the resident step, Ctx::hk_*): the host, before
+  // enqueuing -- a kept list then launches no K0d and, several ranks, no box
+  // all-gather, no halo plan and one K0b for own + halo tiles.  Every rank
+  // takes the same decision from the same inputs (the host-side invalidations
+  // are collective events, the prediction is all-reduced with the gate).
+  // Otherwise the device: the records' preparers raise a flag, K0d / the plan
+  // read it (round-5 behaviour).
+  bool hk = false, hkeep = false;
+  int64_t hm = 0;
+  if (tpr && c->hk_req && c->hk_on && !c->simp.resume_nav && c->hk_hdev) {
+    if (c->hk_cool > 0) {  // after a stale abort: device-decided for a while
+      c->hk_cool--;
+      c->hk_ok = false;
+    } else {
+      hk = true;
+      hm = c->hk_m++;
+      const int nf = (c->simp.winddim == 0 && c->sim_gs_derivable) ? 6 : 8;  // (halo_mid's field count)
+      bool build = !tvalid || !c->hk_ok || (c->halo_mode == 1 && nf != c->halo_fields);
+      // a build one or two detects ago: its snapshot is fresh enough (the
+      // prediction covers two steps of drift); else the prediction made from
+      // the records of detect hm - 2, published by that step's K4'
+      if (!build && !c->hk_built[(hm + 3) & 3] && !c->hk_built[(hm + 2) & 3]) {
+        unsigned long long v = 0;
+        if (hk_wait(c, hm - 2, &v)) return -1;
+        build = (v & 3ull) != 0;  // predicted, or that step aborted (its retry rebuilds anyway)
+      }
+      c->hk_built[hm & 3] = build;
+      c->hk_ok = true;
+      hkeep = !build;
+      (build ? c->hk_builds : c->hk_keeps)++;
+      static const bool trace = getenv("BSA_HK_TRACE") && atoi(getenv("BSA_HK_TRACE")) == 1;  // (diagnostics)
+      if (trace)
+        fprintf(stderr, "[bsa hk] rank %d detect %lld: %s (tvalid %d, step %lld)\n", c->rank, (long long)hm,
+                build ? "build" : "keep", tvalid ? 1 : 0, (long long)c->sim_steps);
+    }
+  } else if (tpr) {
+    c->hk_ok = false;  // a device-decided detect: the build history is no longer the host's
+  }
+  c->hk_cur = hk;
+  c->hk_keep = hkeep;
+  c->hk_last = hm;
+  if (tpr) {  // (every rank, also one without rows: the kept state stays collective)
+    c->tpr_valid = true;  // (an aborted step or any state change clears it)
+    memcpy(c->tpr_key, tkey, sizeof tkey);
+    c->tpr_n = n;
+  } else {
+    c->tpr_valid = false;
+  }
+  // (HK keep, halo mode: K2 zeroed this detect's counters too, or K0z runs as
+  // its own launch -- not inside the merged K0b, whose halo workgroups write Counters)
+  const bool nozero = ((prepped && (n + kTile - 1) / kTile <= kTPDirectMax) || (hkeep && halo)) && !zero_env &&
+                      !tp_super && c->k2_bucket > 0 && c->zeroed_rows == nrows;
   c->zeroed_rows = -1;
   if (nozero) {
     std::swap(c->counters, c->counters2);
@@ -2587,17 +2725,19 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   };
   if (n == 0 || nrows == 0) {
     if (zero(false, nullptr, 0)) return -1;
-    if (halo) {  // a rank without rows still takes part in the exchange
+    if (halo) {  // a rank without rows still takes part in the exchange (HK keep: no box all-gather)
       HaloPre hp;
       HaloUnpack hu;
       if (halo_pre(c, rb, re, &hp)) return -1;
-      for (int r = 0; r < 3; ++r)
-        if (hp.zn[r]) BSA_HIP(c, hipMemsetAsync(hp.z[r], 0, (size_t)hp.zn[r] * 4, c->stream));
-      // (its plan-reuse flag stays clear: it holds no records that could drift)
-      if (unsigned *f = halo_flag_word(c)) BSA_HIP(c, hipMemsetAsync(f, 0, 4, c->stream));
-      if (halo_mid(c, rb, re, &hu)) return -1;
+      if (!hkeep) {
+        for (int r = 0; r < 3; ++r)
+          if (hp.zn[r]) BSA_HIP(c, hipMemsetAsync(hp.z[r], 0, (size_t)hp.zn[r] * 4, c->stream));
+        // (its plan-reuse flag stays clear: it holds no records that could drift)
+        if (unsigned *f = halo_flag_word(c)) BSA_HIP(c, hipMemsetAsync(f, 0, 4, c->stream));
+      }
+      if (halo_mid(c, rb, re, &hu, nullptr, hkeep)) return -1;
     }
-    if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, 16, c->stream));
+    if (gate) BSA_HIP(c, hipMemsetAsync(gate, 0, kGateWords * 8, c->stream));
     for (int e = 1; e < 5; ++e)
       if (mark(e)) return -1;
     c->ev_valid = c->ev_valid || timed;
@@ -2724,20 +2864,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       !ensure(c, c->sbox_c, nsc * sizeof(TileBox), "column sub-group boxes") ||
       !ensure(c, c->tilepairs, (size_t)ntp * kSlicesPerTile * sizeof(uint2), "prefilter items"))
     return -1;
-  // halo mode: K0d sweeps the present column tiles only (own + received, the
-  // flat halo list; BSA_TP_HALO_ALL=1 sweeps all tiles for A/B)
-  static const bool tp_all = getenv("BSA_TP_HALO_ALL") && atoi(getenv("BSA_TP_HALO_ALL")) == 1;
-  const bool tp_list = halo && !tp_all && !tp_super;
-  // tile-pair list reuse: the resident step's detects of a
-  // rank's rows -- one rank: records prepared (and checked) by K4'; several
-  // ranks or the probe: the halo plan is kept with the list, checked by the
-  // own-tile K0b and decided from flags gathered with the boxes.  Any other
-  // detect of this context invalidates the kept list.
-  static const bool tpr_env = !(getenv("BSA_TPR") && atoi(getenv("BSA_TPR")) == 0);
+  // tile-pair list reuse (decided above): the list's buffers and budgets
   TprArgs tp{};
   HaloTpr ht{};
-  const bool tpr = tpr_env && c->tpr_on && home && !reuse && flags == 0 && !tp_super &&
-                   ((!halo && prepped && nct <= kTPDirectMax) || tp_list);
   if (tpr) {
     if (!ensure(c, c->tpr_snap, (size_t)n * sizeof(PFRec), "tile-pair list snapshot")) return -1;
     const bool fresh = !c->tpr_ctl.p;
@@ -2748,16 +2877,13 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
       c->tpr_dx = (float)(sh_env / 6.3e6);
       c->tpr_ds = (float)(sh_env / 6.3e6 / 20);
     }
-    const double key[6] = {rpz, hpz, tla, (double)mid, (double)rb, (double)re};
-    const bool valid = c->tpr_valid && c->tpr_n == n && memcmp(key, c->tpr_key, sizeof key) == 0;
-    ht = HaloTpr{halo ? 1 : 0, valid ? 0 : 1, c->tpr_dx, c->tpr_ds, c->tpr_dv, (unsigned long long *)c->tpr_ctl.p,
+    const bool force = hk ? !hkeep : !tvalid;  // (HK: the host's decision; a kept list launches no plan)
+    ht = HaloTpr{halo ? 1 : 0, force ? 1 : 0, c->tpr_dx, c->tpr_ds, c->tpr_dv, (unsigned long long *)c->tpr_ctl.p,
                  nullptr};
-    c->tpr_valid = true;  // (an aborted step or any state change clears it)
-    memcpy(c->tpr_key, key, sizeof key);
-    c->tpr_n = n;
-  } else {
-    c->tpr_valid = false;
   }
+  // HK: the prediction word of this detect's records (raised by their
+  // preparer -- K4' one step ago, or the own tiles' K0b here)
+  unsigned long long *hk_word = hk ? (unsigned long long *)c->tpr_ctl.p + 6 + (hm & 1) : nullptr;
   FusedBoxes fb{nullptr, nullptr, nullptr, nullptr, 0};
   ZeroArgs zs{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
   // halo mode: the plan's buffers are zeroed and the own tile boxes written
@@ -2769,7 +2895,8 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   TprCheck tck{};
   if (tpr && halo) {
     ht.myflag = halo_flag_word(c);
-    if (!ht.force) tck = TprCheck{(const PFRec *)c->tpr_snap.p, ht.myflag, c->tpr_dx, c->tpr_ds, c->tpr_dv};
+    if (!ht.force)
+      tck = TprCheck{(const PFRec *)c->tpr_snap.p, ht.myflag, c->tpr_dx, c->tpr_ds, c->tpr_dv, hk_word, c->hk_f};
   }
   if (!reuse) {
     fb = FusedBoxes{(TileBox *)c->sbox_c.p, (TileBox *)c->gbox_c.p, (TileBox *)c->tbox_c.p, hp.blk, hp.blk_base};
@@ -2777,27 +2904,42 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                   (unsigned long long *)c->tcpamax.p, (unsigned *)c->rowcnt.p, {hp.z[0], hp.z[1], hp.z[2]},
                   {hp.zn[0], hp.zn[1], hp.zn[2]}};
   }
+  const int na = halo ? a1 - a0 : 0;
   if (prepped) {  // K0b + K0c ran in the previous step's K4': K0z + the tile boxes here
     if (!nozero && zero(false, nullptr, 0, true)) return -1;
-  } else
-  hipLaunchKernelGGL(k_prep_cols, dim3(halo ? (unsigned)(a1 - a0) : blocks_for(n, kTile)), dim3(kTile), 0,
-                     c->stream, (int)n, perm_c, home ? 1 : 0, recs ? 1 : 0, own,
-                     intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla, (ColRec *)c->colrec.p,
-                     (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb, zs,
-                     halo ? a0 : 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, tck, nfa);
+  } else if (!(halo && hkeep)) {  // (HK keep, several ranks: the own tiles go with the halo tiles below)
+    const unsigned g = halo ? (unsigned)na : blocks_for(n, kTile);
+    hipLaunchKernelGGL(k_prep_cols, dim3(g), dim3(kTile), 0, c->stream, (int)n, perm_c, home ? 1 : 0,
+                       recs ? 1 : 0, own, intr, distinct ? 1 : 0, shared ? 1 : 0, rpz, hpz, tla,
+                       (ColRec *)c->colrec.p, (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid,
+                       rz, fb, zs, halo ? a0 : 0, (const int *)nullptr, HaloUnpack{}, (Counters *)nullptr, tck, nfa,
+                       (int)g);
+  }
   BSA_HIP(c, hipGetLastError());
   if (halo) {
     HaloUnpack hu{};
-    if (halo_mid(c, rb, re, &hu, tpr ? &ht : nullptr)) return -1;
-    if (c->halo_hl > 0) {  // the received tiles: unpacked (exchange), records and boxes (no zeroing here)
-      const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
-      FusedBoxes fb2 = fb;
-      fb2.blk = nullptr;
-      hu.count = halo_list_count(c);
+    if (halo_mid(c, rb, re, &hu, tpr ? &ht : nullptr, hkeep)) return -1;
+    const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
+    FusedBoxes fb2 = fb;
+    fb2.blk = nullptr;
+    hu.count = halo_list_count(c);
+    if (hkeep) {
+      // HK keep: no plan, so the own tiles wait for nothing before the
+      // exchange -- ONE K0b for them and the received tiles (workgroups [0, na)
+      // the own tiles with their budget checks, the rest the halo list's
+      // slots); K0z is K2's (double-buffered counters) or its own launch,
+      // never inside it (its halo workgroups write Counters)
+      if (!nozero && zero(false, nullptr, 0)) return -1;
+      hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)(na + c->halo_hl)), dim3(kTile), 0, c->stream, (int)n, perm_c,
+                         1, recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
+                         (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, a0,
+                         (const int *)c->h_hl.p, hu, dcnt, tck, nfa, na);
+      BSA_HIP(c, hipGetLastError());
+    } else if (c->halo_hl > 0) {  // the received tiles: unpacked (exchange), records and boxes (no zeroing here)
       hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)c->halo_hl), dim3(kTile), 0, c->stream, (int)n, perm_c, 1,
                          recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
                          (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, 0,
-                         (const int *)c->h_hl.p, hu, dcnt, TprCheck{}, nfa);
+                         (const int *)c->h_hl.p, hu, dcnt, TprCheck{}, nfa, 0);
       BSA_HIP(c, hipGetLastError());
     }
   }
@@ -2818,8 +2960,12 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   const unsigned long long icap = (unsigned long long)ntp * kSlicesPerTile;  // items: 8 slices per tile pair
   if (tpr)  // (after halo_mid, which may have forced the rebuild)
     tp = TprArgs{(unsigned long long *)c->tpr_ctl.p, ht.force, c->tpr_dx, c->tpr_ds, c->tpr_dv,
-                 (const PFRec *)c->pfcol.p + roff, (PFRec *)c->tpr_snap.p + roff, halo ? ht.myflag : nullptr};
-  if ((nct <= kTPDirectMax || tp_list) && !tp_super)
+                 (const PFRec *)c->pfcol.p + roff, (PFRec *)c->tpr_snap.p + roff, halo ? ht.myflag : nullptr,
+                 hkeep ? 1 : 0, hkeep ? (halo ? ht.myflag : (const unsigned *)c->tpr_ctl.p) : nullptr,
+                 hkeep && c->sim_ctl.p ? (unsigned long long *)((char *)c->sim_ctl.p + kSimCtlStale) : nullptr};
+  if (hkeep) {
+    // HK keep: no K0d -- the prefilter takes the kept list's counts from the control words
+  } else if ((nct <= kTPDirectMax || tp_list) && !tp_super)
     hipLaunchKernelGGL(k_tilepairs_direct, dim3((unsigned)nrt), dim3(kTPDirectThreads), 0, c->stream, nrt, nct,
                        (int)nrows, tbox_r, gbox_r, (const TileBox *)c->tbox_c.p, noprune, (uint2 *)c->tilepairs.p,
                        icap, dcnt, (unsigned long long *)c->workq.p, build, halo ? halo_present(c) : nullptr, a0,
@@ -2895,7 +3041,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     hn = HeavyNext{(unsigned *)c->hv_cost.p, {(unsigned *)c->hv_list[2 * b].p, (unsigned *)c->hv_list[2 * b + 1].p},
                    cn + 2 * b, (unsigned *)c->hv_flag.p, E + 1,
                    {(unsigned)std::min(c->hv_us * x * 100.0, 4e9), (unsigned)std::min(c->hv_us * 100.0, 4e9)},
-                   (const unsigned long long *)c->workq.p, icap};
+                   // the list's item counts: ctl[1], ctl[2] (the prefilter publishes a built list's there;
+                   // an HK-kept detect fills no dequeue words)
+                   (const unsigned long long *)c->tpr_ctl.p, icap};
   }
   // K2 row buckets (B pairs per row per list; a fuller row retries wider, then without)
   const int B = c->k2_bucket;
@@ -2994,7 +3142,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                         (int *)c->out_ci.p, (int *)c->out_cj.p, (double *)c->out_pay.p, (int *)c->out_li.p,
                         (int *)c->out_lj.p, (unsigned long long *)c->stats.p, gate, build, mf,
                         (unsigned char *)c->inconf.p, (unsigned long long *)c->tcpamax.p,
-                        (Counters *)c->counters2.p, (unsigned long long *)c->workq2.p, nfa};
+                        (Counters *)c->counters2.p, (unsigned long long *)c->workq2.p, nfa, hk_word};
     if (c->k24_want) {  // bsa_sim_step launches it fused with K4' (k24_launch)
       c->k24_blob.resize(sizeof rl);
       memcpy(c->k24_blob.data(), &rl, sizeof rl);

@@ -459,6 +459,13 @@ bsa_ctx *bsa_create(int device) {
   if (const char *v = getenv("BSA_PF_HEAVY_US")) c->hv_us = atof(v);
   if (getenv("BSA_PF_HEAVY") && atoi(getenv("BSA_PF_HEAVY")) == 0) c->hv_us = -1.0;
   if (const char *v = getenv("BSA_PF_HEAVY_X")) c->hv_x = atof(v);
+  // host-known tile-pair list decisions (Ctx::hk_*; BSA_HK=0 off, BSA_HK_F the
+  // prediction fraction); results never depend on them
+  if (getenv("BSA_HK") && atoi(getenv("BSA_HK")) == 0) c->hk_on = false;
+  if (const char *v = getenv("BSA_HK_F")) {
+    const float f = (float)atof(v);
+    if (f > 0.f && f <= 1.f) c->hk_f = f;
+  }
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     bsa::fail(nullptr, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -474,6 +481,8 @@ void bsa_destroy(bsa_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->pin) (void)hipHostFree(c->pin);
   if (c->pin_ev) (void)hipEventDestroy(c->pin_ev);
+  if (c->hk_host) (void)hipHostFree(c->hk_host);
+  c->hk_host = c->hk_hdev = nullptr;
   c->pin = nullptr;
   c->pin_ev = nullptr;
   bsa::DevBuf *all[] = {&c->rowrec, &c->colrec, &c->pfrow, &c->pfcol, &c->counters, &c->cand,
@@ -719,6 +728,26 @@ int bsa_tile_reuse_stats(bsa_ctx *c, int64_t *out2) {
   }
   out2[0] = (int64_t)w[3];
   out2[1] = (int64_t)w[4];
+  return 0;
+}
+
+int bsa_set_hk(bsa_ctx *c, int on, double f) {
+  if (!c) return -1;
+  if (!(f > 0.0 && f <= 4.0)) return bsa::fail(c, "HK prediction fraction must be in (0, 4]");
+  c->hk_on = on != 0;
+  c->hk_f = (float)f;
+  c->hk_ok = false;  // (the next host-decided detect builds)
+  return 0;
+}
+
+int bsa_hk_stats(bsa_ctx *c, int64_t *out6) {
+  if (!c || !out6) return -1;
+  out6[0] = c->hk_keeps;
+  out6[1] = c->hk_builds;
+  out6[2] = c->hk_waits;
+  out6[3] = c->hk_stale;
+  out6[4] = c->hk_cool;
+  out6[5] = c->hk_on ? 1 : 0;
   return 0;
 }
 

@@ -389,12 +389,18 @@ static int plan_local(Ctx *c, int a0, int a1, int tpr, const HaloTpr *ht) {
   return 0;
 }
 
-int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht) {
+int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht, bool hkeep) {
   hu->rbuf = nullptr;
   const int nct = nct_of(c);
   const int a0 = tile_lo(rb), a1 = tile_hi(rb, re), na = a1 - a0;
   if (c->halo_mode == 2) {
     c->halo_fields = 0;
+    if (hkeep) {  // HK: the kept plan's dense list (its length stays in h_dem)
+      const int tpr = std::max(na, 1), Rp = (nct + tpr - 1) / tpr;
+      c->halo_hl = (int64_t)Rp * tpr;
+      c->halo_tot_word = 2 * Rp;
+      return 0;
+    }
     return plan_local(c, a0, a1, std::max(na, 1), ht);
   }
   // ---- exchange mode (several ranks); halo_pre's buffers, zeroed by the own-tile K0b
@@ -408,17 +414,19 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht) {
   unsigned *req = (unsigned *)((char *)c->h_blk.p + (size_t)tpr * sizeof(TileBox));
   const bool keep = ht && ht->tpr;
   // the fields per halo row fix the regions' layout (the kept send headers sit
-  // at its offsets): a change of it is a rebuild on every rank alike
+  // at its offsets): a change of it is a rebuild on every rank alike (HK: the
+  // host checked it before it kept the plan)
   const int nf = (c->simp.winddim == 0 && c->sim_gs_derivable) ? 6 : 8;
+  if (hkeep && nf != c->halo_fields) return fail(c, "internal: HK kept the halo plan across a field-count change");
   if (keep && nf != c->halo_fields) ht->force = 1;
-  if (c->simp.resume_nav && c->bk_ready && na > 0) {
+  if (!hkeep && c->simp.resume_nav && c->bk_ready && na > 0) {
     hipLaunchKernelGGL(k_halo_req, dim3(64), dim3(256), 0, s, (int)(c->sim_re - c->sim_rb),
                        (const unsigned *)c->bk_rptr.p, (const unsigned *)c->bk_rcol.p, (const unsigned *)c->id2h.p,
                        a0, a1, req, keep ? (const uint8_t *)c->h_present.p : (const uint8_t *)nullptr,
                        keep ? ht->myflag : (unsigned *)nullptr);
     BSA_HIP(c, hipGetLastError());
   }
-  if (comm_allgather(c, c->h_blk.p, c->h_gblk.p, bb)) return -1;
+  if (!hkeep && comm_allgather(c, c->h_blk.p, c->h_gblk.p, bb)) return -1;
   // capacities and offsets of this rank's regions
   HaloCaps cp{};
   size_t roff = 0;
@@ -451,9 +459,11 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht) {
               (unsigned *)c->h_dem.p, (Counters *)c->counters.p};
   const int ny = std::max(1, std::min(na, kPlanRows));
   const unsigned gx = (unsigned)std::max((std::max(nct, R * na) + 255) / 256, R);
-  hipLaunchKernelGGL(k_halo_plan, dim3(gx, (unsigned)(ny + 3)), dim3(256), 0, s, pa, ny, ny + 2, la, cp, R,
-                     h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, plan_done_word(c, nct, R, tpr));
-  BSA_HIP(c, hipGetLastError());
+  if (!hkeep) {  // (HK: the kept plan's send headers and halo list stay as they are)
+    hipLaunchKernelGGL(k_halo_plan, dim3(gx, (unsigned)(ny + 3)), dim3(256), 0, s, pa, ny, ny + 2, la, cp, R,
+                       h.tpr ? (uint8_t *)c->h_present.p : (uint8_t *)nullptr, plan_done_word(c, nct, R, tpr));
+    BSA_HIP(c, hipGetLastError());
+  }
   HaloFields fl{};
   DevBuf *src[8] = {&c->own[0], &c->own[1], &c->own[2], &c->own[3], &c->own[4], &c->own[5], &c->s_gse, &c->s_gsn};
   for (int f = 0; f < 8; ++f) fl.f[f] = (double *)src[f]->p;

@@ -115,7 +115,32 @@ constexpr unsigned kDangling = 0xffffffffu;  // resopairs column of a deleted in
 // non-finite tcpa input in some rank's columns (every row's tcpamax is NaN),
 // >= 2 abort the step (2 candidate / row-bucket overflow, 3 resopairs overflow)
 constexpr unsigned long long kGateNonfinite = 1, kGateOverflow = 2, kGateBkOverflow = 3;
+// gate[2]: the HK prediction of this CD call (some rank's records left kHkPredict of their budgets)
+constexpr int kGateWords = 3;
+constexpr int kSimCtlSticky = 24, kSimCtlSteps = 32, kSimCtlDemand = 40, kSimCtlKdemand = 48, kSimCtlStale = 56;
+// (sim_ctl bytes; [24, 64) are zeroed per batch and read back after it)
+constexpr int kHkRing = 16;  // HK: published predictions (pinned host words), slot m % kHkRing
 constexpr unsigned long long kNanBits = 0x7ff8000000000000ull;  // (a quiet NaN)
+
+// HK publication (Ctx::hk_*): lane 0 of block 0 of a CD step's K4' (or of the
+// fused K2 + K4') stores base | prediction (bit 0) | aborted (bit 1) into the
+// ring slot of the detect, in pinned host memory the host polls (a vector
+// store, system scope; written before any early return of the kernel)
+struct HkPub {
+  unsigned long long *slot;  // device view of hk_host[m % kHkRing], or NULL (no publication)
+  unsigned long long base;   // (m + 1) << 2
+  unsigned long long *src;   // the prediction word (gate[2] after the all-reduce, or the rank's own word)
+  int zero;                  // zero *src once read (the rank's own word: its next user is two detects on)
+};
+// (relaxed: the host reads this one word; a release at system scope would
+// write back the whole L2 first -- buffer_wbl2 -- under the other waves' feet)
+template <typename Aborted>
+__device__ __forceinline__ void hk_publish(const HkPub &p, Aborted aborted) {
+  if (!p.slot) return;
+  const unsigned long long v = p.base | (p.src && *p.src ? 1ull : 0ull) | (aborted() ? 2ull : 0ull);
+  if (p.zero && p.src) *p.src = 0ull;
+  __hip_atomic_store(p.slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // counters block on the device
 constexpr int kFuseRecsMax = 64;  // fused K1b: mid-sweep flush records per prefilter wave (LDS)
@@ -127,7 +152,7 @@ struct Counters {
   unsigned long long tiles;
   unsigned long long groups;  // (64-row x 8-column) blocks swept by the prefilter
   unsigned long long tiles_near;  // of `tiles`: pairs whose boxes overlap (listed first, swept first)
-  unsigned long long pad[1];      // (far tile pairs, counted from the list's end)
+  unsigned long long tpr_stale;   // a host-kept tile-pair list (HK) whose records left their budgets: re-run
   unsigned long long k2_demand;   // K2 row buckets: the largest row count beyond Ctx::k2_bucket (0: fit)
   unsigned long long halo_ovf;    // halo exchange: more tiles to send / receive than the capacities
   unsigned long long halo_miss;   // halo exchange inconsistent (a kept tile pair without its data): bug
@@ -240,7 +265,31 @@ struct Ctx {
   int64_t tpr_n = -1;
   float tpr_dx = 3.2e-4f, tpr_ds = 1.6e-5f, tpr_dv = 300.f;  // ~2 km, ~100 m of reach, 300 m
   DevBuf tpr_snap;                     // PFRec per aircraft at the last build
-  DevBuf tpr_ctl;                      // u64: [0] build flag, [1] near items, [2] far items, [3] builds, [4] detects
+  DevBuf tpr_ctl;                      // u64: [0] build flag, [1] near items, [2] far items, [3] builds, [4] detects,
+                                       // [5] the probe's rebuild flag, [6 + (m & 1)] HK prediction of detect m
+  // Host-known list decisions (HK, round 6): in the resident
+  // step the host decides build / keep BEFORE it enqueues a detect, so a kept
+  // list launches no K0d (and, several ranks, no box all-gather, no halo plan
+  // and one K0b for own + halo tiles).  Detect m keeps when neither m-1 nor
+  // m-2 built and the device's prediction for m -- the records of detect m-2
+  // within kHkPredict of every budget, over all ranks -- says so; the step's
+  // K4' publishes that prediction into a pinned host ring (hk_host), so the
+  // host waits at most for the work of the step before.  The kept detect still
+  // checks every record against the full budgets: one outside aborts the step
+  // (Counters::tpr_stale) and it re-runs with a build.
+  bool hk_on = true;                   // BSA_HK=0: the device decides (round-5 behaviour)
+  bool hk_req = false;                 // bsa_sim_step: the detect being enqueued may be host-decided
+  bool hk_ok = false;                  // the build history below is this sim's
+  bool hk_built[4] = {false, false, false, false};  // build decisions of detects m & 3
+  bool hk_cur = false, hk_keep = false;  // the last detect_enqueue was host-decided / kept its list
+  int64_t hk_m = 0;                    // index of the next host-decided detect
+  int64_t hk_last = 0;                 // ... of the last one (its K4' publishes slot hk_last % kHkRing)
+  int64_t hk_cool = 0;                 // after a stale abort: device-decided detects left
+  int64_t hk_cool_len = 32;            // ... the next such stretch (doubles per stale abort, <= 4096):
+                                       // a workload whose lists go stale often ends up device-decided
+  int64_t hk_keeps = 0, hk_builds = 0, hk_stale = 0, hk_waits = 0;  // statistics
+  float hk_f = 0.75f;                  // prediction fraction of the budgets (BSA_HK_F)
+  unsigned long long *hk_host = nullptr, *hk_hdev = nullptr;  // pinned ring (host / device view)
   // longest items first (bsa_cd.hip HeavyArgs): per list slot cost / flag, two item lists and counts
   DevBuf hv_cost, hv_flag, hv_list[4], hv_cnt;  // lists: [parity][tier]
   unsigned long long hv_icap = 0;
@@ -325,9 +374,9 @@ struct Ctx {
   unsigned long long nf_counter = 0, nf_prep_epoch = 0;  // epochs (K0b: a new one; K4' prep: the next detect's)
   unsigned long long nf_force_epoch = 0;  // != 0: the epoch the next detects take (bsa_sim_detect_rows: the
                                          // records of every tile, prepared first, carry it)
-  DevBuf sim_ctl;  // [0,16) gate {abort / non-finite, P}; [16,20) sticky abort; [24,32) steps done;
-                   // [32,40) resopairs demand on a bookkeeping overflow; [40,48) pair-key
-                   // block demand (several ranks)
+  DevBuf sim_ctl;  // [0,24) gate {abort / non-finite, P, HK prediction}; [24,28) sticky abort; [32,40) steps
+                   // done; [40,48) resopairs demand on a bookkeeping overflow; [48,56) pair-key
+                   // block demand (several ranks); [56,64) an HK-kept list went stale in the batch
   // ASAS bookkeeping (bsa_asas.hip, resume_nav = 1): resopairs CSR over own
   // rows (+ next), per-row kept counts, LoS row pointers of the last call,
   // previous call's conflict / LoS CSR (one rank), stats

@@ -46,13 +46,13 @@ namespace bsa {
 template <bool FUSE, bool PREP>
 __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double simdt, int winddim, double vwn,
                                                          double vwe, WindField wf, SimDev d, MvpIn mv,
-                                                         bsa_mvp_params mp, PrepArgs pa) {
-  if (FUSE) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && mv.gate[0] >= kGateOverflow) mv.sticky[0] = 1u;
-    if (*d.sticky || mv.gate[0] >= kGateOverflow) return;
-  } else if (*d.sticky) {
-    return;
+                                                         bsa_mvp_params mp, PrepArgs pa, HkPub pub) {
+  const bool stop = *d.sticky != 0u || (FUSE && mv.gate[0] >= kGateOverflow);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (FUSE && mv.gate[0] >= kGateOverflow) mv.sticky[0] = 1u;
+    hk_publish(pub, [&] { return stop; });  // HK: the CD step's prediction to the host (also when it aborts)
   }
+  if (stop) return;
   const int k = rb + blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x == 0) *d.steps_done += 1;
   if (PREP) {  // every lane reaches the wave's group reduction (its record from registers)
@@ -63,6 +63,10 @@ __global__ __launch_bounds__(256) void k_sim_pilot_kin(int rb, int re, double si
     if (pa.snap) {
       const bool out = k < re && !pf_within(p, b, pa.dx, pa.ds, pa.dv);
       if (__ballot(out) && (threadIdx.x & 63) == 0) pa.tpr_ctl[0] = 1ull;
+      if (pa.pred) {  // HK: ... or pf x the budgets (a rebuild two detects on)
+        const bool near = k < re && !pf_within(p, b, pa.pf * pa.dx, pa.pf * pa.ds, pa.pf * pa.dv);
+        if (__ballot(near) && (threadIdx.x & 63) == 0) *pa.pred = 1ull;
+      }
     }
     return;
   }
@@ -134,8 +138,8 @@ static SimDev sim_dev(Ctx *c) {
   d.avs = (const double *)c->s_avs.p;
   d.aalt = (const double *)c->s_aalt.p;
   d.active = (const uint8_t *)c->s_active.p;
-  d.sticky = (const unsigned *)((char *)c->sim_ctl.p + 16);
-  d.steps_done = (unsigned long long *)((char *)c->sim_ctl.p + 24);
+  d.sticky = (const unsigned *)((char *)c->sim_ctl.p + bsa::kSimCtlSticky);
+  d.steps_done = (unsigned long long *)((char *)c->sim_ctl.p + kSimCtlSteps);
   return d;
 }
 
@@ -417,7 +421,7 @@ static int sim_cd(Ctx *c, bool allow_defer) {
   c->fuse_noreso = nullptr;
   if (de) return -1;
   c->sim_cd_calls++;
-  unsigned *sticky = (unsigned *)((char *)c->sim_ctl.p + 16);
+  unsigned *sticky = (unsigned *)((char *)c->sim_ctl.p + bsa::kSimCtlSticky);
   BkDev bk;
   bk.lat = (const double *)c->own[0].p;
   bk.lon = (const double *)c->own[1].p;
@@ -430,11 +434,11 @@ static int sim_cd(Ctx *c, bool allow_defer) {
   bk.dropped = (uint8_t *)c->s_dropped.p;
   bk.gate = gate;
   bk.sticky = sticky;
-  bk.demand = (unsigned long long *)((char *)c->sim_ctl.p + 32);
-  bk.kdemand = (unsigned long long *)((char *)c->sim_ctl.p + 40);
+  bk.demand = (unsigned long long *)((char *)c->sim_ctl.p + kSimCtlDemand);
+  bk.kdemand = (unsigned long long *)((char *)c->sim_ctl.p + kSimCtlKdemand);
   // ASAS bookkeeping, first half: kept-pair counts (may flag a resopairs overflow in the gate)
   if (p.resume_nav && bk_count(c, bk)) return -1;
-  if (comm_allreduce_max_u64(c, gate, 2)) return -1;
+  if (comm_allreduce_max_u64(c, gate, kGateWords)) return -1;
   const int64_t rb = c->sim_rb;
   MvpDev d;
   d.gseast = (const double *)c->s_gse.p;
@@ -496,8 +500,17 @@ static int grow_after_abort(Ctx *c, const unsigned long long *ctl) {
   // pair keys outgrew their all-gather block on some rank: the block width is
   // part of the all-gather's layout, so every rank grows to the same width
   // (max-all-reduced demand; collective, every rank aborted at this step)
-  double kdem = (double)ctl[3];
-  if (comm_multi(c) && comm_allreduce_host(c, &kdem, 1, true)) return -1;
+  // (with HK's stale flag: the device-decided stretch after a stale abort must
+  // be the same on every rank -- the kept and the rebuilt plans issue
+  // different collectives)
+  double agree[2] = {(double)ctl[3], ctl[4] ? 1.0 : 0.0};
+  if (comm_multi(c) && comm_allreduce_host(c, agree, 2, true)) return -1;
+  const double kdem = agree[0];
+  if (agree[1] > 0.0) {  // an HK-kept list no longer covered some rank's records: device-decided for a while
+    c->hk_stale++;
+    c->hk_cool = c->hk_cool_len;
+    c->hk_cool_len = std::min<int64_t>(2 * c->hk_cool_len, 4096);
+  }
   if (kdem > 0)
     c->bk_kw = std::max<unsigned long long>(2 * c->bk_kw, (unsigned long long)kdem + (unsigned long long)kdem / 4 + 1024);
   // candidate overflow on this rank: enough for the last detect's demand (its
@@ -505,6 +518,10 @@ static int grow_after_abort(Ctx *c, const unsigned long long *ctl) {
   // abort ran on the same, unchanged state)
   Counters h;
   BSA_HIP(c, hipMemcpy(&h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
+  static const bool trace = getenv("BSA_HK_TRACE") && atoi(getenv("BSA_HK_TRACE")) == 1;  // (diagnostics)
+  if (trace)
+    fprintf(stderr, "[bsa hk] rank %d abort at step %lld: stale %d k2 %llu fuse %llu halo %llu/%llu\n", c->rank,
+            (long long)c->sim_steps, ctl[4] ? 1 : 0, h.k2_demand, h.fuse_ovf, h.halo_ovf, h.halo_miss);
   if (h.k2_demand) grow_k2_bucket(c, h.k2_demand);  // a K2 row bucket was full on this rank
   if (h.fuse_ovf) {  // fused K1b out of flush records: the re-run's detect unfused
     c->fuse_skip = true;
@@ -601,6 +618,18 @@ int bsa_sim_init(bsa_ctx *cc, int64_t n, const bsa_sim_state *s, const bsa_sim_p
   c->sim_gathered = true;
   c->sim_prepped = false;
   c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
+  c->hk_ok = false;      // (HK: no build history yet)
+  c->hk_cool = 0;
+  c->hk_cool_len = 32;
+  if (!c->hk_host) {     // HK: the pinned ring the steps' K4' publish their predictions into
+    void *hp = nullptr;
+    BSA_HIP(c, hipHostMalloc(&hp, (size_t)bsa::kHkRing * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    memset(hp, 0, (size_t)bsa::kHkRing * 8);
+    c->hk_host = (unsigned long long *)hp;
+    void *dp = nullptr;
+    BSA_HIP(c, hipHostGetDevicePointer(&dp, hp, 0));
+    c->hk_hdev = (unsigned long long *)dp;
+  }
   c->sim_gs_derivable = false;  // gseast / gsnorth are the host's until K4' runs
   if (c->feed_pending) {  // a snapshot of the previous sim is dropped
     BSA_HIP(c, hipEventSynchronize(c->feed_ev));
@@ -625,8 +654,9 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     if (attempt > 6) return bsa::fail(c, "candidate buffer overflow in the resident step (retries exhausted)");
     const int64_t base = c->sim_steps, base_cd = c->sim_cd_calls;
     const bool derivable0 = c->sim_gs_derivable;
-    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 32, c->stream));  // sticky, steps_done, demands
+    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + bsa::kSimCtlSticky, 0, 40, c->stream));  // sticky, steps_done, demands, stale
     while (c->sim_steps < target) {
+      bool cd_step = false;
       if (c->sim_steps % c->simp.cd_every == 0) {
         // one rank: K2 and this step's K4' as one launch (k24_launch below;
         // BSA_K24=0 off) -- K4' then starts on each workgroup's rows as soon as
@@ -634,12 +664,16 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
         static const bool k24_env = !(getenv("BSA_K24") && atoi(getenv("BSA_K24")) == 0);
         c->k24_want = k24_env && c->nranks == 1 && c->halo_mode == 0 && !c->simp.resume_nav && re > rb &&
                       c->k2_bucket > 0;
+        c->hk_req = true;  // (HK: this detect's list decision may be the host's)
         const int r = bsa::sim_cd(c, true);
+        c->hk_req = false;
         c->k24_want = false;
         if (r) {
           c->k24_pending = false;
+          c->hk_ok = false;  // (a detect may have been enqueued without its step's publication)
           return -1;
         }
+        cd_step = true;
       }
       // K4' workgroup size: one wave (at 100k rows 256-lane groups left half the
       // CUs one group short, 391 groups on 256 CUs: 0.1753 -> 0.1718 ms per
@@ -683,12 +717,28 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
           pa.dx = c->tpr_dx;
           pa.ds = c->tpr_ds;
           pa.dv = c->tpr_dv;
+          // HK: the prediction word of the next detect (index hk_m, if it is host-decided)
+          pa.pred = (unsigned long long *)c->tpr_ctl.p + 6 + (c->hk_m & 1);
+          pa.pf = c->hk_f;
         }
       }
       const int blk = k4b;  // (PREP: whole waves = whole groups, rb = 0)
       const int64_t nb = std::max<int64_t>(1, (re - rb + blk - 1) / blk);
       bsa::MvpIn mv{};
       if (c->mvp_deferred) memcpy(&mv, c->mvp_defer.data(), sizeof(mv));
+      // HK: the CD step's K4' (or K2 + K4') publishes the detect's prediction --
+      // the rank's own word with K2 fused, else gate[2] after K2 and the all-reduce
+      bsa::HkPub pub{};
+      if (cd_step && c->hk_cur) {
+        pub.slot = c->hk_hdev + (c->hk_last % bsa::kHkRing);
+        pub.base = (unsigned long long)(c->hk_last + 1) << 2;
+        if (c->k24_pending) {
+          pub.src = (unsigned long long *)c->tpr_ctl.p + 6 + (c->hk_last & 1);
+          pub.zero = 1;
+        } else {
+          pub.src = (unsigned long long *)c->sim_ctl.p + 2;
+        }
+      }
       if (c->k24_pending) {  // K2 of this step's detect, fused with K4' (double-buffered alt / vs / gse / gsn)
         const int64_t n = c->n;
         if (!c->mvp_deferred) return bsa::fail(c, "internal: fused K2 + K4' without the deferred MVP rows");
@@ -701,7 +751,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
         d.gse_w = (double *)c->nx_gse.p;
         d.gsn_w = (double *)c->nx_gsn.p;
         const bsa::K24Args ka{d, mv, c->simp.mvp, pa, bsa::wind_field(c), c->simp.simdt, c->simp.windnorth,
-                              c->simp.windeast, c->simp.winddim, prep ? 1 : 0};
+                              c->simp.windeast, c->simp.winddim, prep ? 1 : 0, pub};
         if (bsa::k24_launch(c, ka)) return -1;
         std::swap(c->own[4], c->nx_alt);
         std::swap(c->own[5], c->nx_vs);
@@ -712,7 +762,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
                                         : (prep ? bsa::k_sim_pilot_kin<false, true> : bsa::k_sim_pilot_kin<false, false>);
         hipLaunchKernelGGL(K4, dim3((unsigned)nb), dim3(blk), 0, c->stream, (int)rb, (int)re, c->simp.simdt,
                            c->simp.winddim, c->simp.windnorth, c->simp.windeast, bsa::wind_field(c), bsa::sim_dev(c),
-                           mv, c->simp.mvp, pa);
+                           mv, c->simp.mvp, pa, pub);
       }
       c->mvp_deferred = false;
       c->sim_prepped = prep;
@@ -732,8 +782,8 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
       c->sim_steps++;
     }
     // the batch's only host synchronisation: did every step complete?
-    unsigned long long ctl[4] = {0, 0, 0, 0};
-    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 32, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long ctl[5] = {0, 0, 0, 0, 0};
+    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + bsa::kSimCtlSticky, 40, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
     if ((unsigned)ctl[0] == 0) break;
     // aborted at step base + done: the state is that of the step's start.  The
@@ -743,6 +793,7 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     c->reuse_valid = false;  // the re-run rebuilds any reused candidate list
     c->sim_prepped = false;  // (an aborted K4' prepared nothing)
     c->tpr_valid = false;  // (tile-pair list / halo plan reuse: rebuilt at the next detect)
+    c->hk_ok = false;      // (HK: the decisions of the aborted steps never took effect)
     const int64_t done = (int64_t)ctl[1];
     c->sim_steps = base + done;
     c->sim_gs_derivable = done > 0 ? c->simp.winddim == 0 : derivable0;  // K4' ran for the completed steps only
@@ -1072,10 +1123,10 @@ int bsa_sim_cd(bsa_ctx *cc) {
   for (int attempt = 0;; ++attempt) {
     if (attempt > 6) return bsa::fail(c, "candidate buffer overflow in the CD call (retries exhausted)");
     const int64_t base_cd = c->sim_cd_calls;
-    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + 16, 0, 32, c->stream));  // sticky, steps_done, demands
+    BSA_HIP(c, hipMemsetAsync((char *)c->sim_ctl.p + bsa::kSimCtlSticky, 0, 40, c->stream));  // sticky, steps_done, demands, stale
     if (bsa::sim_cd(c, false)) return -1;
-    unsigned long long ctl[4] = {0, 0, 0, 0};
-    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + 16, 32, hipMemcpyDeviceToHost, c->stream));
+    unsigned long long ctl[5] = {0, 0, 0, 0, 0};
+    BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + bsa::kSimCtlSticky, 40, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
     if ((unsigned)ctl[0] == 0) break;
     // aborted: nothing persistent was written (the state did not move, so

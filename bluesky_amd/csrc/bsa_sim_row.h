@@ -44,6 +44,10 @@ struct PrepArgs {
   float dx, ds, dv;
   unsigned long long *nf;  // non-finite tcpa inputs: the epoch stored (Ctx::nonfin), or NULL
   unsigned long long nfe;
+  // HK (Ctx::hk_*): the next detect's prediction word, raised when a record
+  // left pf x every budget (the list is rebuilt two detects on), or NULL
+  unsigned long long *pred;
+  float pf;
 };
 
 // one row of K4' (below).  The row's state is loaded before K3's part runs
@@ -149,6 +153,7 @@ struct K24Args {
   WindField wf;
   double simdt, vwn, vwe;
   int winddim, prep;
+  HkPub pub;          // HK: this detect's prediction to the host (slot NULL: none)
 };
 int k24_launch(Ctx *c, const K24Args &ka);  // the deferred K2 launch of the last detect, fused (bsa_cd.hip)
 

@@ -174,6 +174,16 @@ int bsa_set_tile_reuse(bsa_ctx *ctx, int on, double sigma_h, double sigma_v);
 /* [0] tile-pair list builds, [1] detects that used the kept or a fresh list,
  * since the sim's first such detect (device counters). */
 int bsa_tile_reuse_stats(bsa_ctx *ctx, int64_t *out2);
+/* Host-known list decisions in the resident step (HK): on =
+ * 0 lets the device decide every rebuild (the round-5 behaviour, one K0d /
+ * halo plan launch per detect); f in (0, 4] is the fraction of the drift
+ * budgets past which the device predicts a rebuild two detects ahead (f > 1:
+ * predictions come late, kept lists go stale and their steps re-run -- a
+ * testing knob).  Results never depend on either. */
+int bsa_set_hk(bsa_ctx *ctx, int on, double f);
+/* out6 = {host-kept detects, host-built detects, waits for a prediction,
+ * stale aborts (re-run steps), device-decided detects after them, on} */
+int bsa_hk_stats(bsa_ctx *ctx, int64_t *out6);
 
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
  * bounding-box cull, the total number of tile pairs, and the number of

@@ -66,10 +66,17 @@ def test_tile_reuse_builds_rarely_at_the_bench_cadence(ctx):
     _, a0 = run(ctx, init, p, 0, (2016.0, 300.0))
     _, a = run(ctx, init, p, 30, (2016.0, 300.0))
     builds, detects = a['builds'] - a0['builds'], a['detects'] - a0['detects']
-    assert detects == 29 and 1 <= builds <= 8, a        # (the first detect is K0b's: no list)
+    # (the first detect is K0b's: no list; HK rebuilds at 0.75 of the budgets, and the first
+    # steps of the sim are its vertical transient -- aircraft levelling off -- so a few more)
+    assert detects == 29 and 1 <= builds <= 12, a
     _, b0 = run(ctx, init, resident.params(simdt=1.0), 0, (1.0, 1.0))
+    h0 = ctx.hk_stats()
     _, b = run(ctx, init, resident.params(simdt=1.0), 10, (1.0, 1.0))
-    assert b['builds'] - b0['builds'] == b['detects'] - b0['detects'] == 9, b
+    # (HK: the host keeps the list right after a build; that step finds it stale and
+    # re-runs without a list -- the re-run counts no list detect -- then the device
+    # decides for a while: a rebuild at every other detect)
+    stale = ctx.hk_stats()['stale_aborts'] - h0['stale_aborts']
+    assert b['builds'] - b0['builds'] == b['detects'] - b0['detects'] == 9 - stale, (b, stale)
 
 
 @pytest.mark.parametrize('us', ['0', '20', '1e9'])
@@ -89,6 +96,54 @@ def test_longest_items_first_is_bitwise(monkeypatch, us):
         got, st = run(c, init, p, 12, (2016.0, 300.0))
         same(got, exp)
         assert sum(len(x[1]['ci']) for x in exp) > 0
-        assert st['detects'] >= 11
+        assert st['detects'] >= 9   # (11 list detects, less an HK-kept one gone stale and re-run without a list)
     finally:
         c.close()
+
+
+# ---------------------------------------------------------------- host-known decisions (HK)
+def run_batch(ctx, init, p, batches, hk, f=0.75):
+    """The resident sim in batches of steps (one bsa_sim_step call each, so the
+    host enqueues ahead of the device and waits on the published predictions),
+    with HK on / off; the state and pair lists after every batch."""
+    ctx.set_hk(hk, f)
+    try:
+        sim = resident.ResidentSim(init, p, ctx=ctx)
+        h0 = ctx.hk_stats()
+        out = []
+        for k in batches:
+            sim.step(k)
+            st = sim.stats()
+            out.append((sim.read(), ctx.fetch_pairs(st['n_conf'], st['n_los'])))
+        h = ctx.hk_stats()
+        return out, {k: h[k] - h0[k] for k in ('keeps', 'builds', 'waits', 'stale_aborts')}
+    finally:
+        ctx.set_hk(True, 0.75)
+
+
+@pytest.mark.parametrize('simdt, f, horiz', [
+    (0.05, 0.75, True),    # the bench's cadence and MVP: kept lists, the host waits on the predictions
+    (0.05, 0.75, False),   # vertical MVP: vs jumps move the midpoint altitudes (budget 300 m) at once
+    (1.0, 0.75, False),    # 250 m per step: predicted rebuilds every few detects
+    (1.0, 4.0, False),     # predictions far too late: kept lists go stale, their steps re-run rebuilt
+])
+def test_host_known_decisions_are_bitwise(ctx, simdt, f, horiz):
+    """HK: the host decides each detect's rebuild before it
+    enqueues the detect, from a prediction the device published two detects
+    earlier; a kept detect launches no K0d.  A kept list that no longer covers
+    the records aborts its step (Counters::tpr_stale), which re-runs with a
+    build.  Neither changes a result: bitwise the device-decided run."""
+    t = synth.box(20000, 300.0, seed=113)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=simdt, swresohoriz=horiz)
+    batches = [1, 5, 30, 1, 20]
+    exp, h_off = run_batch(ctx, init, p, batches, False)
+    got, h = run_batch(ctx, init, p, batches, True, f)
+    same(got, exp)
+    assert h_off['keeps'] == h_off['builds'] == 0
+    assert sum(len(x[1]['ci']) for x in exp) > 0
+    assert h['keeps'] > 0 and h['builds'] >= 1, h
+    if f > 1.0:
+        assert h['stale_aborts'] >= 1, h
+    elif horiz:   # (no vertical MVP jumps: the predictions come in time -- the first steps' levelling-off
+        assert h['stale_aborts'] == 0 and h['keeps'] > h['builds'], h   # transient still rebuilds often)
