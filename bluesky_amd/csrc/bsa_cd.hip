@@ -3186,6 +3186,24 @@ void grow_k2_bucket(Ctx *c, unsigned long long demand) {
   c->k2_bucket = b > 64 ? 0 : b;
 }
 
+#ifdef BSA_PF_TRACE
+// diagnostic builds: the last prefilter's item timeline to $BSA_PF_TRACE_FILE
+// (tools/pf_trace.py; detect_finish, and bsa_sim_step after each batch)
+int pf_trace_dump(Ctx *c, unsigned long long groups, unsigned long long tiles) {
+  const char *fn = getenv("BSA_PF_TRACE_FILE");
+  if (!fn || !c->trace_buf) return 0;
+  std::vector<unsigned long long> t(kTraceRecs * 4);
+  BSA_HIP(c, hipMemcpy(t.data(), c->trace_buf, t.size() * 8, hipMemcpyDeviceToHost));
+  if (FILE *f = fopen(fn, "ab")) {
+    const unsigned long long hdr[4] = {0xfeedull, (unsigned long long)(t.size() / 4), groups, tiles};
+    fwrite(hdr, 8, 4, f);
+    fwrite(t.data(), 8, t.size(), f);
+    fclose(f);
+  }
+  return 0;
+}
+#endif
+
 // Wait for the enqueued detect and read its totals.  *retry is set (and the
 // candidate capacity grown) when the candidate list overflowed.
 int detect_finish(Ctx *c, bool *retry) {
@@ -3227,16 +3245,7 @@ int detect_finish(Ctx *c, bool *retry) {
   c->last_los = (int64_t)h.los;
   c->have_pairs = true;
 #ifdef BSA_PF_TRACE
-  if (const char *fn = getenv("BSA_PF_TRACE_FILE")) {
-    std::vector<unsigned long long> t(kTraceRecs * 4);
-    BSA_HIP(c, hipMemcpy(t.data(), c->trace_buf, t.size() * 8, hipMemcpyDeviceToHost));
-    if (FILE *f = fopen(fn, "ab")) {
-      const unsigned long long hdr[4] = {0xfeedull, (unsigned long long)(t.size() / 4), h.groups, h.tiles};
-      fwrite(hdr, 8, 4, f);
-      fwrite(t.data(), 8, t.size(), f);
-      fclose(f);
-    }
-  }
+  if (pf_trace_dump(c, h.groups, h.tiles)) return -1;
 #endif
 #ifdef BSA_PF_STAMPS
   fprintf(stderr, "[bsa stamps] prefilter wave-cycles: setup %.4g stage1 %.4g drain %.4g flush %.4g | "

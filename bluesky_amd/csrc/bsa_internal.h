@@ -571,6 +571,9 @@ bool nonfin_word(Ctx *c);  // Ctx::nonfin allocated (zeroed when new)
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
                    unsigned long long *gate);
 int detect_finish(Ctx *c, bool *retry);
+#ifdef BSA_PF_TRACE
+int pf_trace_dump(Ctx *c, unsigned long long groups, unsigned long long tiles);  // (diagnostic builds)
+#endif
 void grow_k2_bucket(Ctx *c, unsigned long long demand);
 
 }  // namespace bsa

@@ -785,6 +785,9 @@ int bsa_sim_step(bsa_ctx *cc, int nsteps) {
     unsigned long long ctl[5] = {0, 0, 0, 0, 0};
     BSA_HIP(c, hipMemcpyAsync(ctl, (char *)c->sim_ctl.p + bsa::kSimCtlSticky, 40, hipMemcpyDeviceToHost, c->stream));
     BSA_HIP(c, hipStreamSynchronize(c->stream));
+#ifdef BSA_PF_TRACE
+    if (bsa::pf_trace_dump(c, 0, 0)) return -1;  // (diagnostic builds: the batch's last prefilter)
+#endif
     if ((unsigned)ctl[0] == 0) break;
     // aborted at step base + done: the state is that of the step's start.  The
     // gate is all-reduced, so every rank aborted at the same step; each rank

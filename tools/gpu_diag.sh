@@ -9,9 +9,9 @@ if [ "${STAMPS:-1}" = 1 ]; then
   rc=$?; cat $OUT/stamps.log; [ $rc -eq 0 ] || exit $rc
 fi
 export BSACCEL_AB=1 BSACCEL_LIB=$PWD/bluesky_amd/libbsaccel_trace.so
-echo "${TRACES:-box100k 1}" | tr ';' '\n' | while read wl r; do
+echo "${TRACES:-box100k 1}" | tr ";" "\n" | while read wl r rk; do
   [ -n "$wl" ] || continue
-  BSA_PF_TRACE_FILE=$OUT/tr.bin timeout -k 10 120 python tools/pf_trace.py run $wl $r || exit 1
+  BSA_PF_TRACE_FILE=$OUT/tr.bin timeout -k 10 120 python tools/pf_trace.py run $wl $r ${rk:-0} || exit 1
   python tools/pf_trace.py show $OUT/tr.bin > $OUT/show_${wl}_$r.txt; echo "== trace $wl R=$r"; head -24 $OUT/show_${wl}_$r.txt
   rm -f $OUT/tr.bin
 done

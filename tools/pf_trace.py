@@ -16,7 +16,23 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def run(name, div):
+def run_sim(name, steps):
+    """The resident step itself (the bench's detects: HK, the kept list, the
+    listed longest items): one record set per batch -- its last prefilter."""
+    from bluesky_amd import _lib, resident, synth
+    t = synth.workload(name)
+    ctx = _lib.Context(0)
+    sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
+    path = os.environ.pop('BSA_PF_TRACE_FILE')
+    sim.step(1)
+    sim.step(steps)   # settle: the list and its listed items in steady state
+    os.environ['BSA_PF_TRACE_FILE'] = path
+    for _ in range(3):
+        sim.step(5)
+    ctx.sync()
+
+
+def run(name, div, rank=0):
     from bluesky_amd import _lib, resident, synth
     t = synth.workload(name)
     ctx = _lib.Context(0)
@@ -25,7 +41,7 @@ def run(name, div):
     n = t.ntraf
     rpr = ((n + div - 1) // div + 511) // 512 * 512
     for _ in range(2):
-        ctx.sim_detect_rows(0, min(n, rpr))
+        ctx.sim_detect_rows(rank * rpr, min(n, (rank + 1) * rpr))
     ctx.sync()
 
 
@@ -68,7 +84,9 @@ def show(fn):
 
 
 if __name__ == '__main__':
-    if sys.argv[1] == 'run':
-        run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+    if sys.argv[1] == 'sim':
+        run_sim(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 300)
+    elif sys.argv[1] == 'run':
+        run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1, int(sys.argv[4]) if len(sys.argv) > 4 else 0)
     else:
         show(sys.argv[2])
