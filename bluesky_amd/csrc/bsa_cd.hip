@@ -966,6 +966,7 @@ constexpr int PF_ITEMS_PER_TILE = kTile / PF_WROWS;  // work items per tile pair
 struct PfKnobs {
   int pieces;  // units per item (tile pair, 64-row slice): 1, 2, 4 (or 8, BSA_PF_PIECES)
   int pnear;   // ... per near item (the pair's boxes overlap: the densest items)
+  int t0;      // log2 of the listed top tier's pieces per near item's (HeavyArgs; BSA_PF_HEAVY_T0)
 };
 // Longest items first (a kept tile-pair list): the sweep's
 // span is set by its longest items (a dense item's refine runs up to ~60 us;
@@ -1153,7 +1154,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     nh1 = __builtin_amdgcn_readfirstlane(hv.count[1]);
     if (blockIdx.x == 0 && threadIdx.x < 2) hv.count_next[threadIdx.x] = 0u;
   }
-  const unsigned lh0 = lnear + 1u;
+  const unsigned lh0 = lnear + (unsigned)kn.t0;
   const unsigned hu0 = nh0 << lh0, hunits = hu0 + (nh1 << lnear);
   const unsigned nunits = hunits + nreg;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
@@ -1531,7 +1532,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       const unsigned long long slot = ((unsigned long long)blockIdx.x * PF_WAVES + w) * kTraceWave + tr_n++;
       if (tr_n <= kTraceWave && slot < kTraceRecs) {
         unsigned long long *t = pf_trace + 4 * slot;
-        t[0] = item;
+        t[0] = item | (item < hunits ? (1ull << 63) : 0ull) | ((unsigned long long)npc << 48);  // listed, pieces
         t[1] = ((unsigned long long)blockIdx.x << 2 | w) << 8 | tr_subs;
         t[2] = tr0;
         t[3] = __builtin_amdgcn_s_memrealtime();
@@ -2989,7 +2990,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // pieces: ~8 items per row tile, a few hundred row tiles fill the waves;
   // fewer rows split the items (BSA_PF_PIECES overrides)
   static const int pieces_env = getenv("BSA_PF_PIECES") ? atoi(getenv("BSA_PF_PIECES")) : 0;
-  PfKnobs kn{1, 1};
+  PfKnobs kn{1, 1, 1};
+  static const int t0_env = getenv("BSA_PF_HEAVY_T0") ? atoi(getenv("BSA_PF_HEAVY_T0")) : -1;
+  if (t0_env >= 0 && t0_env <= 3) kn.t0 = t0_env;
   // (measured, tools/gpu_pieces.sh: 2 pieces at the 100k box, 102 -> 97 us; 4 for
   // one rank of 8 there, 36 -> 29 us; 2 at 125k rows of 1M, 65 -> 53 us; 1
   // from 250k rows up, where 2 cost +15 us.  Round 5, with the longest-items

@@ -78,6 +78,18 @@ def show(fn):
             print('  %.0f%% of item-time done by %.1f us' %
                   (frac * 100, np.interp(frac, np.cumsum(np.sort(dur)[::-1]) / dur.sum(), np.sort(en)) if False else
                    en[np.argsort(en)][np.searchsorted(np.cumsum(dur[np.argsort(en)]) / dur.sum(), frac)]))
+        listed = (rec[:, 0] >> np.uint64(63)).astype(bool)
+        npc = ((rec[:, 0] >> np.uint64(48)) & np.uint64(0x7fff)).astype(np.int64)
+        if listed.any():
+            print('  listed units %d (pieces %s): max %.1f us; unlisted max %.1f us (sub-groups %d, pieces %d)' %
+                  (listed.sum(), np.unique(npc[listed]).tolist(), dur[listed].max(), dur[~listed].max(),
+                   subs[~listed][np.argmax(dur[~listed])], npc[~listed][np.argmax(dur[~listed])]))
+            long = dur > 0.6 * dur.max()
+            print('  units above 60%% of the max: %d, listed %d; (pieces, sub-groups, us) of the 6 longest: %s' %
+                  (long.sum(), (long & listed).sum(),
+                   [(int(npc[i]), int(subs[i]), round(float(dur[i]), 1)) for i in np.argsort(-dur)[:6]]))
+        else:
+            print('  no listed units')
         starts = np.sort(st)
         print('  item starts: first %.1f, 50%% by %.1f, last %.1f us' % (starts[0], starts[len(starts) // 2], starts[-1]))
         det += 1
