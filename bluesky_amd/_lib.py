@@ -61,6 +61,8 @@ SIGNATURES = {
     'bsa_tile_reuse_stats': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_set_hk': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double]),
     'bsa_hk_stats': (ctypes.c_int, [_vp, _c_i64p]),
+    'bsa_set_halo_overlap': (ctypes.c_int, [_vp, ctypes.c_int]),
+    'bsa_halo_overlap_count': (ctypes.c_int, [_vp, _c_i64p]),
     'bsa_reuse_budget_use': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_last_timings': (ctypes.c_int, [_vp, _c_dp]),
     'bsa_timing_reset': (ctypes.c_int, [_vp]),
@@ -471,6 +473,16 @@ class Context:
     def set_hk(self, on=True, f=0.75):
         """Host-known tile-pair list decisions of the resident step (bsa_set_hk)."""
         self.check(self.lib.bsa_set_hk(self.h, 1 if on else 0, float(f)), 'bsa_set_hk')
+
+    def set_halo_overlap(self, mode):
+        """Halo exchange overlapped with the own tiles' sweep (bsa_set_halo_overlap):
+        0 off, 1 several ranks, 2 also the one-GPU probe."""
+        self.check(self.lib.bsa_set_halo_overlap(self.h, int(mode)), 'bsa_set_halo_overlap')
+
+    def halo_overlap_count(self):
+        v = np.zeros(1, np.int64)
+        self.check(self.lib.bsa_halo_overlap_count(self.h, ptr(v, _c_i64p)), 'bsa_halo_overlap_count')
+        return int(v[0])
 
     def hk_stats(self):
         v = np.zeros(6, np.int64)

@@ -967,6 +967,10 @@ struct PfKnobs {
   int pieces;  // units per item (tile pair, 64-row slice): 1, 2, 4 (or 8, BSA_PF_PIECES)
   int pnear;   // ... per near item (the pair's boxes overlap: the densest items)
   int t0;      // log2 of the listed top tier's pieces per near item's (HeavyArgs; BSA_PF_HEAVY_T0)
+  // halo overlap (Ctx::ov_mode): 0 every item; 1 the items of the own column
+  // tiles [ca0, ca1); 2 the others (the received tiles), with the dequeue
+  // counters at word 8 of each shard's stride
+  int ph, ca0, ca1;
 };
 // Longest items first (a kept tile-pair list): the sweep's
 // span is set by its longest items (a dense item's refine runs up to ~60 us;
@@ -1095,7 +1099,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     if (hv.list[0] && blockIdx.x == 0 && threadIdx.x < 2) hv.count_next[threadIdx.x] = 0u;
     return;
   }
-  if (tp.ctl && blockIdx.x == 0 && threadIdx.x == 0) {  // tile-pair list reuse: K0d is complete here
+  if (tp.ctl && kn.ph != 2 && blockIdx.x == 0 && threadIdx.x == 0) {  // tile-pair list reuse: K0d is complete here
     if (!tp.keep && (tp.force || tp.ctl[0] != 0ull)) {  // it built: keep the list's counts, clear the flag
       tp.ctl[1] = work[1];
       tp.ctl[2] = work[2];
@@ -1158,7 +1162,7 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
   const unsigned hu0 = nh0 << lh0, hunits = hu0 + (nh1 << lnear);
   const unsigned nunits = hunits + nreg;
   const unsigned shard = blockIdx.x & (kWorkShards - 1);
-  unsigned long long *wq = work + shard * kWorkStride;
+  unsigned long long *wq = work + shard * kWorkStride + (kn.ph == 2 ? 8 : 0);
   // candidates: shard `shard` owns cand[shard * ccap, (shard + 1) * ccap) and
   // its own counter (spreads the flush atomics over kCandShards addresses)
   const unsigned long long ccap = cap / kCandShards;
@@ -1256,6 +1260,8 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
     }
     const unsigned npc = 1u << ls;
     const uint2 it = items[slot];  // (issued with the flag's load: the skip needs both)
+    if (kn.ph && !skip)  // halo overlap: the other launch sweeps it
+      skip = ((it.y - (unsigned)kn.ca0) < (unsigned)(kn.ca1 - kn.ca0)) != (kn.ph == 1);
     do {  // one item; `break` ends it
     if (skip) break;
     // the item: (row tile | slice << 22, column tile)
@@ -2554,6 +2560,14 @@ static int hk_wait(Ctx *c, int64_t m, unsigned long long *v) {
   }
 }
 
+// the halo overlap's second stream and events (Ctx::ov_*), created once
+static int ov_init(Ctx *c) {
+  if (!c->xstream) BSA_HIP(c, hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  for (hipEvent_t &e : c->ov_ev)
+    if (!e) BSA_HIP(c, hipEventCreateWithFlags(&e, c->ov_evflags));
+  return 0;
+}
+
 int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_t rb, int64_t re,
                    unsigned long long *gate) {
   c->fuse_done = false;  // set again only if K2 below evaluates MVP's per-pair vectors
@@ -2906,6 +2920,11 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                   {hp.zn[0], hp.zn[1], hp.zn[2]}};
   }
   const int na = halo ? a1 - a0 : 0;
+  // halo overlap (Ctx::ov_mode): a kept plan of several ranks (mode 2: also the
+  // probe) sweeps the own column tiles on the stream while the exchange, the
+  // received tiles' K0b and their sweep run on xstream
+  const bool ovl = halo && hkeep && !noprune && na > 0 && (c->ov_mode == 2 || (c->ov_mode == 1 && c->halo_mode == 1));
+  if (ovl && ov_init(c)) return -1;
   if (prepped) {  // K0b + K0c ran in the previous step's K4': K0z + the tile boxes here
     if (!nozero && zero(false, nullptr, 0, true)) return -1;
   } else if (!(halo && hkeep)) {  // (HK keep, several ranks: the own tiles go with the halo tiles below)
@@ -2919,12 +2938,37 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   BSA_HIP(c, hipGetLastError());
   if (halo) {
     HaloUnpack hu{};
-    if (halo_mid(c, rb, re, &hu, tpr ? &ht : nullptr, hkeep)) return -1;
+    // (halo overlap: K0z before the pack -- xstream's K0b writes Counters)
+    if (ovl && !nozero && zero(false, nullptr, 0)) return -1;
+    if (halo_mid(c, rb, re, &hu, tpr ? &ht : nullptr, hkeep, ovl && c->halo_mode == 1 ? c->xstream : nullptr))
+      return -1;
     const ZeroArgs zs2{(int)nrows, 1, 0, nullptr, nullptr, nullptr, nullptr, nullptr, {}, {}};
     FusedBoxes fb2 = fb;
     fb2.blk = nullptr;
     hu.count = halo_list_count(c);
-    if (hkeep) {
+    if (ovl) {
+      // the own tiles (budget checks included) on the stream; the received
+      // ones on xstream once the exchange is in (the probe: no exchange, after
+      // K0z), which then waits for the own tiles (its sweep's rows)
+      if (c->halo_mode != 1) {
+        BSA_HIP(c, hipEventRecord(c->ov_ev[0], c->stream));
+        BSA_HIP(c, hipStreamWaitEvent(c->xstream, c->ov_ev[0], 0));
+      }
+      hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)na), dim3(kTile), 0, c->stream, (int)n, perm_c, 1, recs ? 1 : 0,
+                         own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p, (PFRec *)c->pfcol.p,
+                         (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, a0, (const int *)nullptr,
+                         HaloUnpack{}, (Counters *)nullptr, tck, nfa, na);
+      BSA_HIP(c, hipGetLastError());
+      BSA_HIP(c, hipEventRecord(c->ov_ev[1], c->stream));
+      if (c->halo_hl > 0) {
+        hipLaunchKernelGGL(k_prep_cols, dim3((unsigned)c->halo_hl), dim3(kTile), 0, c->xstream, (int)n, perm_c, 1,
+                           recs ? 1 : 0, own, intr, 0, 1, rpz, hpz, tla, (ColRec *)c->colrec.p,
+                           (PFRec *)c->pfcol.p, (PFVel *)c->pfvcol.p, (float4 *)c->pfpcol.p, mid, rz, fb2, zs2, 0,
+                           (const int *)c->h_hl.p, hu, dcnt, TprCheck{}, nfa, 0);
+        BSA_HIP(c, hipGetLastError());
+      }
+      BSA_HIP(c, hipStreamWaitEvent(c->xstream, c->ov_ev[1], 0));
+    } else if (hkeep) {
       // HK keep: no plan, so the own tiles wait for nothing before the
       // exchange -- ONE K0b for them and the received tiles (workgroups [0, na)
       // the own tiles with their budget checks, the rest the halo list's
@@ -2990,7 +3034,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // pieces: ~8 items per row tile, a few hundred row tiles fill the waves;
   // fewer rows split the items (BSA_PF_PIECES overrides)
   static const int pieces_env = getenv("BSA_PF_PIECES") ? atoi(getenv("BSA_PF_PIECES")) : 0;
-  PfKnobs kn{1, 1, 1};
+  PfKnobs kn{1, 1, 1, 0, 0, 0};
   static const int t0_env = getenv("BSA_PF_HEAVY_T0") ? atoi(getenv("BSA_PF_HEAVY_T0")) : -1;
   if (t0_env >= 0 && t0_env <= 3) kn.t0 = t0_env;
   // (measured, tools/gpu_pieces.sh: 2 pieces at the 100k box, 102 -> 97 us; 4 for
@@ -3059,7 +3103,7 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   // BSA_FUSE_EXACT=0/1 overrides (A/B).
   static const int fuse_env = getenv("BSA_FUSE_EXACT") ? atoi(getenv("BSA_FUSE_EXACT")) : -1;
   const bool fuse = fuse_env != 0 && (fuse_env == 1 || !halo) && c->fuse_on && !c->fuse_skip && B > 0 && recs &&
-                    !kwik && !reuse;
+                    !kwik && !reuse && !ovl;
   c->fuse_skip = false;  // (one retry unfused; the next detect fuses again)
   ExactFuse xf{};
   if (fuse)
@@ -3079,11 +3123,28 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
                        (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, TprArgs{},
                        HeavyArgs{}, xf);
   else
-    hipLaunchKernelGGL(k_prefilter<false>, dim3(pf_grid), dim3(PF_BLOCK), 0, c->stream, pfrow, pfvrow, pfprow,
-                       (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
-                       (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
-                       (const uint2 *)c->tilepairs.p, icap, dcnt,
-                       (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kn, diag, tp, hv, xf);
+    for (int ph = ovl ? 1 : 0; ph <= (ovl ? 2 : 0); ++ph) {  // (halo overlap: own tiles here, the others on xstream)
+      PfKnobs kp = kn;
+      kp.ph = ph;
+      kp.ca0 = a0;
+      kp.ca1 = a1;
+      // (the own tiles' sweep leaves half the workgroup slots to the received
+      // tiles' K0b and sweep: 2 of 4 per CU, BSA_OV_GRID_A; probe with the
+      // overlap 0.134 ms per step at 4, 0.121 at 2, 0.104 without it)
+      static const int ga = getenv("BSA_OV_GRID_A") ? atoi(getenv("BSA_OV_GRID_A")) : 2;
+      const unsigned g = ph == 1 && ga > 0 ? std::min<unsigned>(pf_grid, std::max(256u * (unsigned)ga, (unsigned)kWorkShards)) : pf_grid;
+      hipLaunchKernelGGL(k_prefilter<false>, dim3(g), dim3(PF_BLOCK), 0, ph == 2 ? c->xstream : c->stream,
+                         pfrow, pfvrow, pfprow, (int)nrows, (const PFRec *)c->pfcol.p, (const PFVel *)c->pfvcol.p,
+                         (const float4 *)c->pfpcol.p, (int)n, gbox_r, (const TileBox *)c->sbox_c.p, noprune,
+                         (const uint2 *)c->tilepairs.p, icap, dcnt,
+                         (unsigned long long *)c->workq.p, rp, (uint2 *)c->cand.p, cap, build, kp, diag, tp, hv, xf);
+      BSA_HIP(c, hipGetLastError());
+    }
+  if (ovl) {  // join: K1b on waits for the halo tiles' sweep
+    BSA_HIP(c, hipEventRecord(c->ov_ev[2], c->xstream));
+    BSA_HIP(c, hipStreamWaitEvent(c->stream, c->ov_ev[2], 0));
+    c->ov_count++;
+  }
   BSA_HIP(c, hipGetLastError());
   if (mark(2)) return -1;
   // ---- K1b exact evaluation: grid-stride over the device-side count of the

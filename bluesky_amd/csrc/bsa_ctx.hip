@@ -466,6 +466,9 @@ bsa_ctx *bsa_create(int device) {
     const float f = (float)atof(v);
     if (f > 0.f && f <= 1.f) c->hk_f = f;
   }
+  // halo overlap (Ctx::ov_mode): 0 off (default), 1 exchange mode, 2 also the probe
+  if (const char *v = getenv("BSA_HALO_OVERLAP")) c->ov_mode = std::min(std::max(atoi(v), 0), 2);
+  if (const char *v = getenv("BSA_OV_EVFLAGS")) c->ov_evflags = (unsigned)atoi(v);
   e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     bsa::fail(nullptr, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -508,6 +511,12 @@ void bsa_destroy(bsa_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->geo_ev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ov_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->xstream) {
+    (void)hipStreamSynchronize(c->xstream);
+    (void)hipStreamDestroy(c->xstream);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -737,6 +746,19 @@ int bsa_set_hk(bsa_ctx *c, int on, double f) {
   c->hk_on = on != 0;
   c->hk_f = (float)f;
   c->hk_ok = false;  // (the next host-decided detect builds)
+  return 0;
+}
+
+int bsa_set_halo_overlap(bsa_ctx *c, int mode) {
+  if (!c) return -1;
+  if (mode < 0 || mode > 2) return bsa::fail(c, "halo overlap mode must be 0, 1 or 2");
+  c->ov_mode = mode;
+  return 0;
+}
+
+int bsa_halo_overlap_count(bsa_ctx *c, int64_t *out1) {
+  if (!c || !out1) return -1;
+  out1[0] = c->ov_count;
   return 0;
 }
 

@@ -89,9 +89,10 @@ struct HaloTpr {
 // host side (bsa_halo.hip)
 int halo_pre(Ctx *c, int64_t rb, int64_t re, HaloPre *hp, const HaloTpr *ht = nullptr);  // buffers; no launches
 int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht = nullptr,
-             bool hkeep = false);  // plan (+ exchange); hu->rbuf set in mode 1 (may force ht);
-                                   // hkeep (HK kept plan): the exchange only -- no requests, box
-                                   // all-gather or plan
+             bool hkeep = false, hipStream_t xs = nullptr);  // plan (+ exchange); hu->rbuf set in mode 1 (may
+                                   // force ht); hkeep (HK kept plan): the exchange only -- no requests, box
+                                   // all-gather or plan; xs (halo overlap): the send / recv on xs, after
+                                   // the pack (on the context's stream; Ctx::ov_ev[0])
 unsigned *halo_flag_word(Ctx *c);  // this rank's rebuild flag word (box block, or the probe's control word)
 
 }  // namespace bsa

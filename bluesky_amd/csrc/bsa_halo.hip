@@ -389,7 +389,7 @@ static int plan_local(Ctx *c, int a0, int a1, int tpr, const HaloTpr *ht) {
   return 0;
 }
 
-int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht, bool hkeep) {
+int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht, bool hkeep, hipStream_t xs) {
   hu->rbuf = nullptr;
   const int nct = nct_of(c);
   const int a0 = tile_lo(rb), a1 = tile_hi(rb, re), na = a1 - a0;
@@ -485,8 +485,18 @@ int halo_mid(Ctx *c, int64_t rb, int64_t re, HaloUnpack *hu, HaloTpr *ht, bool h
   }
   std::vector<size_t> sof(R);
   for (int q = 0; q < R; ++q) sof[q] = cp.soff[q];
-  if (comm_halo(c, c->h_send.p, sof.data(), slen.data(), stot, c->h_recv.p, rof.data(), rlen.data(), peer.data()))
+  if (xs) {  // halo overlap: the send / recv on xs (the collective runs on whatever stream c->stream names)
+    BSA_HIP(c, hipEventRecord(c->ov_ev[0], s));
+    BSA_HIP(c, hipStreamWaitEvent(xs, c->ov_ev[0], 0));
+    std::swap(c->stream, xs);
+    const int rc = comm_halo(c, c->h_send.p, sof.data(), slen.data(), stot, c->h_recv.p, rof.data(), rlen.data(),
+                             peer.data());
+    std::swap(c->stream, xs);
+    if (rc) return -1;
+  } else if (comm_halo(c, c->h_send.p, sof.data(), slen.data(), stot, c->h_recv.p, rof.data(), rlen.data(),
+                       peer.data())) {
     return -1;
+  }
   hu->rbuf = (const unsigned char *)c->h_recv.p;
   hu->cp = cp;
   hu->fl = fl;

@@ -296,6 +296,21 @@ struct Ctx {
   unsigned hv_epoch = 0;
   double hv_us = 16.0;                 // listing threshold [us] per item (BSA_PF_HEAVY_US at bsa_create; < 0: off)
   double hv_x = 3.0;                   // ... x this: the top tier, twice the pieces (BSA_PF_HEAVY_X; <= 0: one tier)
+  // halo overlap (round 6): on a kept-plan detect of several
+  // ranks the halo send / recv, the halo K0b and the sweep of the halo column
+  // tiles run on xstream while the own tiles' K0b and sweep run on `stream`;
+  // joined by ov_ev[2] before K1b.  ov_mode: 1 exchange mode only (default),
+  // 2 also the one-GPU probe (its cost without an exchange to hide), 0 off
+  // (BSA_HALO_OVERLAP at bsa_create).  Off by default: on one GPU the split
+  // costs ~17 us per step (probe, no exchange to hide: two sweeps' ramps and
+  // tails + cross-stream event waits of ~5-10 us each), more than the ~30 us
+  // exchange it could hide would repay only on the 8-GPU node
+  int ov_mode = 0;
+  hipStream_t xstream = nullptr;
+  hipEvent_t ov_ev[3] = {nullptr, nullptr, nullptr};  // packed / own tiles prepared / halo sweep done
+  int64_t ov_count = 0;                // overlapped detects (statistics)
+  // (device-scope events: the join's wait 13 -> 10 us, the step 0.136 -> 0.134 ms; BSA_OV_EVFLAGS, A/B)
+  unsigned ov_evflags = hipEventDisableTiming | hipEventDisableSystemFence;
 
   // detect timing: one set of 5 events per detect since the last reset
   std::vector<hipEvent_t> evpool;

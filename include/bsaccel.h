@@ -184,6 +184,14 @@ int bsa_set_hk(bsa_ctx *ctx, int on, double f);
 /* out6 = {host-kept detects, host-built detects, waits for a prediction,
  * stale aborts (re-run steps), device-decided detects after them, on} */
 int bsa_hk_stats(bsa_ctx *ctx, int64_t *out6);
+/* Halo overlap of the row-sharded resident step: on a detect
+ * that keeps its halo plan, the halo send / recv, the received tiles' K0b and
+ * the sweep of the halo column tiles run on a second stream while the own
+ * tiles' K0b and sweep run; joined before K1b.  mode 0 off (default), 1
+ * several ranks, 2 also the one-GPU probe (bsa_sim_probe_rank: its cost with
+ * no exchange to hide).  Results never depend on it.  out: overlapped detects. */
+int bsa_set_halo_overlap(bsa_ctx *ctx, int mode);
+int bsa_halo_overlap_count(bsa_ctx *ctx, int64_t *out1);
 
 /* Tile pairs (512 rows x 512 columns) of the last detect that survived the
  * bounding-box cull, the total number of tile pairs, and the number of

@@ -454,6 +454,69 @@ def test_halo_host_known_decisions_equal_world1(ctx, world, f):
         assert hs[0]['stale_aborts'] >= 1, hs
 
 
+@pytest.mark.parametrize('world', [3, 8])
+def test_halo_overlap_equal_world1(ctx, world):
+    """on a kept-plan detect each rank sends / receives
+    its halo, prepares the received tiles and sweeps their items on a second
+    stream while its own tiles are prepared and swept (bsa_set_halo_overlap 1;
+    off by default), joined before K1b.  Bitwise the one-rank run, and every rank
+    overlapped the same detects; with the overlap off, none."""
+    t = synth.box(12000, 200.0, seed=131)
+    init = resident.initial_state(t)
+    p = resident.params(simdt=1.0, swresohoriz=False)
+    batches = [1, 6, 12]
+
+    def steps(sim):
+        out = []
+        for k in batches:
+            sim.step(k)
+            out.append(sim.read())
+        return out
+
+    exp = steps(resident.ResidentSim(init, p, ctx=ctx))
+    for mode in (1, 0):
+        def rank(r, c, g):
+            c.set_halo_overlap(mode)
+            got = steps(resident.ResidentSim(init, p, ctx=c, rank=r, world=world, group=g))
+            return got, c.halo_overlap_count(), c.hk_stats()
+
+        res = run_ranks(world, rank)
+        for r, (got, _, _) in enumerate(res):
+            for k, st in enumerate(exp):
+                for fld, v in st.items():
+                    assert np.array_equal(got[k][fld], v), 'mode %d rank %d batch %d %s' % (mode, r, k, fld)
+        counts = [n for _, n, _ in res]
+        if mode:
+            assert counts[0] > 0 and counts == [counts[0]] * world, (counts, res[0][2])
+        else:
+            assert counts == [0] * world, counts
+
+
+def test_probe_overlap_is_bitwise():
+    """The halo overlap in the one-GPU probe (mode 2, tools/probe_step.py's
+    measurement of its cost): one rank's share stepped with and without it
+    ends in the same state bit for bit."""
+    t = synth.box(20000, 200.0, seed=137)
+    init = resident.initial_state(t)
+    out = []
+    for mode in (2, 0):
+        c = _lib.Context(0)
+        try:
+            c.set_halo_overlap(mode)
+            sim = resident.ResidentSim(init, resident.params(cd_every=1), ctx=c)
+            c.sim_probe_rank(2, 4)
+            sim.step(1)
+            sim.step(20)
+            out.append((sim.read(), c.halo_overlap_count()))
+            c.sim_probe_rank(0, 1)
+        finally:
+            c.close()
+    (a, na), (b, nb) = out
+    assert na > 0 and nb == 0, (na, nb)
+    for fld, v in a.items():
+        assert np.array_equal(v, b[fld]), fld
+
+
 def test_halo_capacity_disagreement_fails_loudly():
     """RCCL's grouped send / recv hangs or truncates when a send
     length differs from its receive length, which only 8 GPUs would show.  The

@@ -1,6 +1,8 @@
 """Prefilter item timeline (diagnostic build `make trace`, libbsaccel_trace.so).
 
 run:     BSACCEL_LIB=.../libbsaccel_trace.so BSA_PF_TRACE_FILE=f python tools/pf_trace.py run WORKLOAD [ROWS_DIV]
+         ... pf_trace.py sim WORKLOAD [SETTLE]  (the resident step)
+         ... pf_trace.py probe WORKLOAD R RANK [SETTLE]  (one rank's share, probe_step.py)
 analyse: python tools/pf_trace.py show f
 
 `run` steps the resident sim (home order) a few times and, with ROWS_DIV = R,
@@ -30,6 +32,25 @@ def run_sim(name, steps):
     for _ in range(3):
         sim.step(5)
     ctx.sync()
+
+
+def run_probe(name, R, rank, steps):
+    """One rank's share of the sharded resident step (tools/probe_step.py's
+    bsa_sim_probe_rank) in steady state: its last prefilter of 3 batches."""
+    from bluesky_amd import _lib, resident, synth
+    t = synth.workload(name)
+    ctx = _lib.Context(0)
+    sim = resident.ResidentSim(resident.initial_state(t), resident.params(cd_every=1), ctx=ctx)
+    path = os.environ.pop('BSA_PF_TRACE_FILE')
+    ctx.sim_probe_rank(rank, R)
+    sim.step(5)
+    sim.step(steps)
+    ctx.sync()
+    os.environ['BSA_PF_TRACE_FILE'] = path
+    for _ in range(3):
+        sim.step(5)
+    ctx.sync()
+    ctx.sim_probe_rank(0, 1)
 
 
 def run(name, div, rank=0):
@@ -98,6 +119,8 @@ def show(fn):
 if __name__ == '__main__':
     if sys.argv[1] == 'sim':
         run_sim(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 300)
+    elif sys.argv[1] == 'probe':
+        run_probe(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]) if len(sys.argv) > 5 else 200)
     elif sys.argv[1] == 'run':
         run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 1, int(sys.argv[4]) if len(sys.argv) > 4 else 0)
     else:
