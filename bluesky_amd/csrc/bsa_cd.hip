@@ -1486,10 +1486,19 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
       load_col(jn, nx, nv, np);
       // sweep only the chunks holding valid slots
       const int nchunk = colmask ? (64 - __builtin_clzll(colmask) + 7) >> 3 : 0;
+      // the survivor bits of chunks 0-3 / 4-7 shift into one word each (four
+      // chunks unrolled: static LDS offsets, and the bit reversal / 64-bit
+      // placement once per four chunks instead of per chunk)
       unsigned long long M = 0;  // this lane's stage-1 survivors of the batch, bit = slot
-      for (int ch = 0; ch < nchunk; ++ch) {
-        const int j0 = ch * 8;
-        unsigned bm = 0;
+#pragma unroll 1
+      for (int hf = 0; hf < 2; ++hf) {
+      const int kc = min(max(nchunk - 4 * hf, 0), 4);
+      if (!kc) break;
+      unsigned bm = 0;
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        if (c4 >= kc) break;
+        const int j0 = (hf * 4 + c4) * 8;
 #pragma unroll
         for (int h = 0; h < 4; h += 2) {
         // two column pairs per load group (register pressure: occupancy)
@@ -1521,8 +1530,9 @@ __global__ __launch_bounds__(PF_BLOCK) PF_OCC void k_prefilter(
         }
         __builtin_amdgcn_sched_barrier(0);
         }
-        // bit 7 - u <-> slot j0 + u: reverse into bit u
-        M |= (unsigned long long)(__builtin_bitreverse32(bm) >> 24) << j0;
+      }
+      // bit 8 kc - 1 - u <-> slot 32 hf + u: reverse into bit u
+      M |= (unsigned long long)(__builtin_bitreverse32(bm) >> (32 - 8 * kc)) << (32 * hf);
       }
       enqueue_batch(M & colmask & (va ? ~0ull : 0ull));
       // refine this batch's survivors while its columns are staged
@@ -3083,11 +3093,15 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
     unsigned *cn = (unsigned *)c->hv_cnt.p;
     const unsigned a = E & 1, b = (E + 1) & 1;  // this detect's / the next one's lists and counts
     const double x = c->hv_x > 0.0 ? c->hv_x : 1e30;  // (tier 0 off: no slot reaches it)
+    // a rank's share (halo mode) sweeps in ~40 us, not ~70: half the threshold
+    // (one rank of 8 at global1m, probe A/B x 3: 0.1010-0.1029 -> 0.1007-0.1009
+    // ms per step at 8 us, 0.0995-0.1010 at 5; box100k unchanged at 16)
+    const double us = halo && !c->hv_us_env ? 0.5 * c->hv_us : c->hv_us;
     hv = HeavyArgs{{(const unsigned *)c->hv_list[2 * a].p, (const unsigned *)c->hv_list[2 * a + 1].p}, cn + 2 * a,
                    cn + 2 * b, (const unsigned *)c->hv_flag.p, (unsigned *)c->hv_cost.p, E};
     hn = HeavyNext{(unsigned *)c->hv_cost.p, {(unsigned *)c->hv_list[2 * b].p, (unsigned *)c->hv_list[2 * b + 1].p},
                    cn + 2 * b, (unsigned *)c->hv_flag.p, E + 1,
-                   {(unsigned)std::min(c->hv_us * x * 100.0, 4e9), (unsigned)std::min(c->hv_us * 100.0, 4e9)},
+                   {(unsigned)std::min(us * x * 100.0, 4e9), (unsigned)std::min(us * 100.0, 4e9)},
                    // the list's item counts: ctl[1], ctl[2] (the prefilter publishes a built list's there;
                    // an HK-kept detect fills no dequeue words)
                    (const unsigned long long *)c->tpr_ctl.p, icap};

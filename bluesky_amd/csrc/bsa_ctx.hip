@@ -456,7 +456,10 @@ bsa_ctx *bsa_create(int device) {
   c->device = device;
   // longest prefilter items first (bsa_cd.hip HeavyArgs): the listing
   // threshold, or off (BSA_PF_HEAVY=0); results never depend on it
-  if (const char *v = getenv("BSA_PF_HEAVY_US")) c->hv_us = atof(v);
+  if (const char *v = getenv("BSA_PF_HEAVY_US")) {
+    c->hv_us = atof(v);
+    c->hv_us_env = true;
+  }
   if (getenv("BSA_PF_HEAVY") && atoi(getenv("BSA_PF_HEAVY")) == 0) c->hv_us = -1.0;
   if (const char *v = getenv("BSA_PF_HEAVY_X")) c->hv_x = atof(v);
   // host-known tile-pair list decisions (Ctx::hk_*; BSA_HK=0 off, BSA_HK_F the

@@ -295,6 +295,7 @@ struct Ctx {
   unsigned long long hv_icap = 0;
   unsigned hv_epoch = 0;
   double hv_us = 16.0;                 // listing threshold [us] per item (BSA_PF_HEAVY_US at bsa_create; < 0: off)
+  bool hv_us_env = false;              // ... set by BSA_PF_HEAVY_US (else halved for a rank's share, bsa_cd.hip)
   double hv_x = 3.0;                   // ... x this: the top tier, twice the pieces (BSA_PF_HEAVY_X; <= 0: one tier)
   // halo overlap (round 6): on a kept-plan detect of several
   // ranks the halo send / recv, the halo K0b and the sweep of the halo column
