@@ -102,11 +102,15 @@ __global__ __launch_bounds__(256) void k_keys(int cnt, int base, const double *_
   if (k >= cnt) return;
   const int o = base + k;
   const double la = lat[o] * kD2R, lo = lon[o] * kD2R;
-  const double cl = cos(la), sl = sin(la), co = cos(lo), so = sin(lo);
+  double cl, sl, co, so;
+  sincos(la, &sl, &cl);
+  sincos(lo, &so, &co);
   double p[3] = {cl * co, cl * so, sl};
   if (f > 0.0) {
     const double t = trk[o] * kD2R, g = gs[o];
-    const double u = g * sin(t), v = g * cos(t);
+    double st, ct;
+    sincos(t, &st, &ct);
+    const double u = g * st, v = g * ct;
     const double m[3] = {p[0] + f * (-u * so - v * sl * co), p[1] + f * (u * co - v * sl * so), p[2] + f * (v * cl)};
     if (isfinite(m[0]) && isfinite(m[1]) && isfinite(m[2]))
       for (int q = 0; q < 3; ++q) p[q] = m[q];
@@ -129,7 +133,8 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   const double tlap = tla > 0.0 ? tla : 0.0;
   const double la = own.lat[o], lo = own.lon[o];
   const double rad = la * kD2R;
-  const double sinl = sin(rad), cosl = cos(rad);
+  double sinl, cosl;
+  sincos(rad, &sinl, &cosl);
   const double trk = intr.trk[o] * kD2R;
   const double gs = intr.gs[o];
   RowRec r;
@@ -138,8 +143,10 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   r.sinlat = sinl;
   r.coslat = cosl;
   r.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);  // geo.py:127
-  r.u = gs * sin(trk);                           // StateBasedCD.py:36-37
-  r.v = gs * cos(trk);
+  double st, ct;
+  sincos(trk, &st, &ct);
+  r.u = gs * st;                                 // StateBasedCD.py:36-37
+  r.v = gs * ct;
   r.alt = intr.alt[o];
   r.vs = intr.vs[o];
   r.pad0 = 0.0;
@@ -147,7 +154,8 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   for (int q = 0; q < 5; ++q) r.pad[q] = 0.0;
   R[k] = r;
   const double lor = lo * kD2R;
-  const double coslo = cos(lor), sinlo = sin(lor);
+  double coslo, sinlo;
+  sincos(lor, &sinlo, &coslo);
   const double px = cosl * coslo, py = cosl * sinlo, pz = sinl;
   const PFRec p = mid ? make_pf_mid(px, py, pz, sinl, cosl, coslo, sinlo, r.u, r.v, gs, r.alt, r.vs, rpz, hpz, tlap)
                       : make_pf(px, py, pz, reach_h(rpz, gs, tlap), r.alt, reach_v(hpz, r.vs, r.alt, tlap));
@@ -326,7 +334,8 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(6))) void
     // when own != intruder (geo.py:128): never prune such a column horizontally
     // nor refine it.
     const bool quirk = distinct && olat == 0.0;
-    const double coslo = cos(lor), sinlo = sin(lor);
+    double coslo, sinlo;
+    sincos(lor, &sinlo, &coslo);
     const double px = cosl * coslo, py = cosl * sinlo, pz = sinl;
     float sv = 0.f, sadd = 0.f;
     if (rz.build) {  // reuse (shared records only): budget check against the last build
@@ -765,8 +774,10 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
   // ---- StateBasedCD.detect (StateBasedCD.py:22-83), off-diagonal entry
   const double dist = dist_nm * kNM + 0.0;
   const double qdrrad = qdr * kD2R;
-  const double dx = dist * sin(qdrrad);
-  const double dy = dist * cos(qdrrad);
+  double sq, cq;
+  sincos(qdrrad, &sq, &cq);
+  const double dx = dist * sq;
+  const double dy = dist * cq;
   const double du = c.u - r.u;  // own.u[j] - int.u[i]
   const double dv = c.v - r.v;
   double dv2 = du * du + dv * dv;

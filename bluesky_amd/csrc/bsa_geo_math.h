@@ -58,8 +58,8 @@ __device__ __forceinline__ double np_rem(double a, double b) {
 __device__ __forceinline__ double rwgs84(double latd) {
   const double a = kWGS84_A, b = kWGS84_B;
   const double lat = latd * kD2R;
-  const double coslat = cos(lat);
-  const double sinlat = sin(lat);
+  double sinlat, coslat;
+  sincos(lat, &sinlat, &coslat);  // (bit for bit sin / cos: tools/sincos_check.hip)
   const double an = (a * a) * coslat;
   const double bn = (b * b) * sinlat;
   const double ad = a * coslat;
@@ -80,8 +80,7 @@ __device__ __forceinline__ GeoPt geo_pt(double lat, double lon) {
   GeoPt p;
   p.lat = lat;
   p.lon = lon;
-  p.sinlat = sin(lat * kD2R);
-  p.coslat = cos(lat * kD2R);
+  sincos(lat * kD2R, &p.sinlat, &p.coslat);
   p.hemA = fabs(lat) * (rwgs84(lat) + kWGS84_A);
   return p;
 }
@@ -103,8 +102,8 @@ __device__ __forceinline__ void qdrdist_entry(double lat1, double lon1, double s
   }
   const double sin1 = (lat2 - lat1) * kD2R;
   const double sin2 = (lon2 - lon1) * kD2R;
-  const double sin21 = sin(sin2);
-  const double cos21 = cos(sin2);
+  double sin21, cos21;
+  sincos(sin2, &sin21, &cos21);
   const double y = sin21 * coslat2;
   const double x1 = coslat1 * sinlat2;
   const double x2 = sinlat1 * coslat2;

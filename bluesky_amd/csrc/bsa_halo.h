@@ -65,8 +65,10 @@ __device__ __forceinline__ int halo_unpack_tile(const HaloUnpack &u, int j, int 
     for (int f = 0; f < u.fl.nf; ++f) u.fl.f[f][row] = src[f * kTile + threadIdx.x];
     if (u.fl.nf == 6) {  // K4' without wind: gseast / gsnorth = gs sin / cos(trk), bitwise the sender's
       const double gs = u.fl.f[3][row], trk = u.fl.f[2][row];
-      u.fl.f[7][row] = gs * cos(trk * kD2R);
-      u.fl.f[6][row] = gs * sin(trk * kD2R);
+      double st, ct;
+      sincos(trk * kD2R, &st, &ct);  // (as K4''s sincos of hdg)
+      u.fl.f[7][row] = gs * ct;
+      u.fl.f[6][row] = gs * st;
     }
   }
   return got;

@@ -189,16 +189,18 @@ __device__ __forceinline__ Out step(const In &s, double simdt, int winddim, doub
   vs = isfinite(vs) ? vs : 0;
 
   // ---- UpdateGroundSpeed (traffic.py:456-476)
+  double sh, ch;
+  sincos(hdg * kD2R, &sh, &ch);
   if (winddim == 0) {
-    o.gsnorth = tas * cos(hdg * kD2R);
-    o.gseast = tas * sin(hdg * kD2R);
+    o.gsnorth = tas * ch;
+    o.gseast = tas * sh;
     o.gs = tas;
     o.trk = hdg;
   } else {
     const double aw = s.alt > 50. * kFT ? 1.0 : 0.0;
     const double naw = 1.0 - aw;
-    o.gsnorth = tas * cos(hdg * kD2R) + wn * aw;
-    o.gseast = tas * sin(hdg * kD2R) + we * aw;
+    o.gsnorth = tas * ch + wn * aw;
+    o.gseast = tas * sh + we * aw;
     o.gs = naw * tas + aw * sqrt(o.gsnorth * o.gsnorth + o.gseast * o.gseast);
     o.trk = naw * hdg + nprem(aw * (atan2(o.gseast, o.gsnorth) * kR2D), 360.);
   }

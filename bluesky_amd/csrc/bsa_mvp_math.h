@@ -25,8 +25,10 @@ __device__ __forceinline__ void mvp_pair(const bsa_mvp_params &p, const MvpPairI
   const double gse1 = in.gseast[id1], gsn1 = in.gsnorth[id1], vs1 = in.vs[id1], alt1 = in.alt[id1];
   // ---- MVP.MVP (MVP.py:149-231)
   const double qdr = qdr_deg * kD2R;
-  const double drel0 = sin(qdr) * dist;
-  const double drel1 = cos(qdr) * dist;
+  double sq, cq;
+  sincos(qdr, &sq, &cq);
+  const double drel0 = sq * dist;
+  const double drel1 = cq * dist;
   const double drel2 = in.alt[id2] - alt1;
   const double vrel0 = in.gseast[id2] - gse1;
   const double vrel1 = in.gsnorth[id2] - gsn1;

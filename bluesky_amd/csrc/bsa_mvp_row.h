@@ -183,8 +183,10 @@ __device__ __forceinline__ MvpRowOut mvp_row(int rb, int r, const bsa_mvp_params
   in.o_trk[r] = newtrack;
   in.o_tas[r] = tas;
   in.o_vs[r] = vsc;
-  in.o_asase[r] = ids ? (float)(tas * sin(newtrack / 180 * kPI)) : 0.0f;
-  in.o_asasn[r] = ids ? (float)(tas * cos(newtrack / 180 * kPI)) : 0.0f;
+  double snt, cnt;
+  sincos(newtrack / 180 * kPI, &snt, &cnt);
+  in.o_asase[r] = ids ? (float)(tas * snt) : 0.0f;
+  in.o_asasn[r] = ids ? (float)(tas * cnt) : 0.0f;
 
   double aalt = aalt0;
   const double signdvs = np_sign(vsc - apvs1 * np_sign(selalt - alt1));

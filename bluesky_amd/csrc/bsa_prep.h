@@ -124,11 +124,12 @@ __device__ __forceinline__ ColRec col_record_v(double la, double lo, double trkd
   ColRec c;
   c.lat = la;
   c.lon = lo;
-  c.sinlat = sin(rad);
-  c.coslat = cos(rad);
+  sincos(rad, &c.sinlat, &c.coslat);
   c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);  // geo.py:127
-  c.u = gs * sin(trk);                          // StateBasedCD.py:31-32
-  c.v = gs * cos(trk);
+  double st, ct;
+  sincos(trk, &st, &ct);
+  c.u = gs * st;                                // StateBasedCD.py:31-32
+  c.v = gs * ct;
   c.alt = alt;
   c.vs = vs;
   c.eps = (olat == 0.0) ? 0.000001 : 0.0;      // geo.py:128 (column-indexed)
@@ -167,7 +168,8 @@ __device__ __forceinline__ PFRec prep_home_record(int k, double la, double lo, d
   if (rec) out.C[k] = c;
   const double sinl = c.sinlat, cosl = c.coslat;
   const double lor = c.lon * kD2R;
-  const double coslo = cos(lor), sinlo = sin(lor);
+  double coslo, sinlo;
+  sincos(lor, &sinlo, &coslo);
   const double px = cosl * coslo, py = cosl * sinlo, pz = sinl;
   const float sadd = 0.f, sv = 0.f;
   const PFRec p = mid ? make_pf_mid(px, py, pz, sinl, cosl, coslo, sinlo, c.u, c.v, gs, c.alt, c.vs, rpz, hpz, tlap)

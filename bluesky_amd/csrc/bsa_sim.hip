@@ -170,8 +170,10 @@ __global__ __launch_bounds__(256) void k_derive_gs(int n, int rb, int re, const 
                                                    double *__restrict__ gsn) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n || (k >= rb && k < re)) return;
-  gsn[k] = gs[k] * cos(trk[k] * kD2R);
-  gse[k] = gs[k] * sin(trk[k] * kD2R);
+  double st, ct;
+  sincos(trk[k] * kD2R, &st, &ct);  // (as K4''s sincos of hdg)
+  gsn[k] = gs[k] * ct;
+  gse[k] = gs[k] * st;
 }
 
 // C1: replicate every rank's rows of the 8 arrays CD and MVP read for any row

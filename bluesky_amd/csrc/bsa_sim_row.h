@@ -89,8 +89,10 @@ __device__ __forceinline__ PFRec pilot_kin_row(int rb, int k, double simdt, int 
   const double ptrk = act ? atrk : aptrk;             // pilot.py:41
   double asastas = atas;                              // pilot.py:37-38: no wind, GS = TAS
   if (winddim > 0) {                                  // pilot.py:31-35: ASAS GS -> TAS
-    const double asastasnorth = atas * cos(atrk * kD2R) - vwn;
-    const double asastaseast = atas * sin(atrk * kD2R) - vwe;
+    double sa, ca;
+    sincos(atrk * kD2R, &sa, &ca);
+    const double asastasnorth = atas * ca - vwn;
+    const double asastaseast = atas * sa - vwe;
     asastas = sqrt(asastasnorth * asastasnorth + asastaseast * asastaseast);
   }
   s.ptas = act ? asastas : aptas;                     // pilot.py:42
