@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void k_prep_rows(int cnt, const unsigned *__re
   r.lon = lo;
   r.sinlat = sinl;
   r.coslat = cosl;
-  r.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);  // geo.py:127
+  r.hemA = fabs(la) * (rwgs84_sc(sinl, cosl) + kWGS84_A);  // geo.py:127
   double st, ct;
   sincos(trk, &st, &ct);
   r.u = gs * st;                                 // StateBasedCD.py:36-37

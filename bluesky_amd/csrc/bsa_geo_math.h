@@ -55,11 +55,9 @@ __device__ __forceinline__ double np_rem(double a, double b) {
 }
 
 // geo.py:32-54 rwgs84_matrix, elementwise, same op order.
-__device__ __forceinline__ double rwgs84(double latd) {
+// rwgs84_sc: the same from sin / cos(radians(latd)) a caller already holds
+__device__ __forceinline__ double rwgs84_sc(double sinlat, double coslat) {
   const double a = kWGS84_A, b = kWGS84_B;
-  const double lat = latd * kD2R;
-  double sinlat, coslat;
-  sincos(lat, &sinlat, &coslat);  // (bit for bit sin / cos: tools/sincos_check.hip)
   const double an = (a * a) * coslat;
   const double bn = (b * b) * sinlat;
   const double ad = a * coslat;
@@ -69,6 +67,11 @@ __device__ __forceinline__ double rwgs84(double latd) {
   const double adad = ad * ad;
   const double bdbd = bd * bd;
   return sqrt((anan + bnbn) / (adad + bdbd));
+}
+__device__ __forceinline__ double rwgs84(double latd) {
+  double sinlat, coslat;
+  sincos(latd * kD2R, &sinlat, &coslat);  // (bit for bit sin / cos: tools/sincos_check.hip)
+  return rwgs84_sc(sinlat, coslat);
 }
 
 // Per-point factors of qdrdist_matrix's broadcasts (geo.py:127,136-140).
@@ -81,7 +84,7 @@ __device__ __forceinline__ GeoPt geo_pt(double lat, double lon) {
   p.lat = lat;
   p.lon = lon;
   sincos(lat * kD2R, &p.sinlat, &p.coslat);
-  p.hemA = fabs(lat) * (rwgs84(lat) + kWGS84_A);
+  p.hemA = fabs(lat) * (rwgs84_sc(p.sinlat, p.coslat) + kWGS84_A);
   return p;
 }
 

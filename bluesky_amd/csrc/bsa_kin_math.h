@@ -155,6 +155,7 @@ struct In {
 struct Out {
   double tas, hdg, alt, vs, lat, lon;       // state after the step
   double ax, delspd, cas, mach, gsnorth, gseast, gs, trk, coslat, az;
+  double sinlat;  // sin(radians(lat)) of the new position (the next records reuse it)
   bool swhdgsel, swaltsel;
 };
 
@@ -208,7 +209,7 @@ __device__ __forceinline__ Out step(const In &s, double simdt, int winddim, doub
   // ---- UpdatePosition (traffic.py:480-483)
   o.alt = o.swaltsel ? s.alt + vs * simdt : s.palt;
   o.lat = s.lat + (simdt * o.gsnorth / kRearth) * kR2D;
-  o.coslat = cos(o.lat * kD2R);
+  sincos(o.lat * kD2R, &o.sinlat, &o.coslat);
   o.lon = s.lon + (simdt * o.gseast / o.coslat / kRearth) * kR2D;
   o.tas = tas;
   o.hdg = hdg;

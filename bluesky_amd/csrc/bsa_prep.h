@@ -117,25 +117,31 @@ struct SoA6 {
 
 // fp64 column record of aircraft o: intruder[o] geometry, own[o] velocity /
 // altitude (the per-aircraft factors of StateBasedCD.py's broadcasts)
-__device__ __forceinline__ ColRec col_record_v(double la, double lo, double trkd, double gs, double alt, double vs,
-                                               double olat) {
-  const double rad = la * kD2R;
-  const double trk = trkd * kD2R;
+// col_record_t: from sin / cos(radians(la)) and u / v a caller already holds
+// (bitwise the values col_record_v computes)
+__device__ __forceinline__ ColRec col_record_t(double la, double lo, double sinlat, double coslat, double u,
+                                               double v, double alt, double vs, double olat) {
   ColRec c;
   c.lat = la;
   c.lon = lo;
-  sincos(rad, &c.sinlat, &c.coslat);
-  c.hemA = fabs(la) * (rwgs84(la) + kWGS84_A);  // geo.py:127
-  double st, ct;
-  sincos(trk, &st, &ct);
-  c.u = gs * st;                                // StateBasedCD.py:31-32
-  c.v = gs * ct;
+  c.sinlat = sinlat;
+  c.coslat = coslat;
+  c.hemA = fabs(la) * (rwgs84_sc(sinlat, coslat) + kWGS84_A);  // geo.py:127 (rwgs84 of the same radians)
+  c.u = u;
+  c.v = v;
   c.alt = alt;
   c.vs = vs;
   c.eps = (olat == 0.0) ? 0.000001 : 0.0;      // geo.py:128 (column-indexed)
   c.olat = olat;
   for (int q = 0; q < 5; ++q) c.pad[q] = 0.0;
   return c;
+}
+__device__ __forceinline__ ColRec col_record_v(double la, double lo, double trkd, double gs, double alt, double vs,
+                                               double olat) {
+  double sl, cl, st, ct;
+  sincos(la * kD2R, &sl, &cl);
+  sincos(trkd * kD2R, &st, &ct);
+  return col_record_t(la, lo, sl, cl, gs * st, gs * ct, alt, vs, olat);  // u, v: StateBasedCD.py:31-32
 }
 
 // the column's inputs to every tcpa of its column (position, velocity) are
@@ -158,12 +164,15 @@ struct PrepOut {
   PFVel *PV;
   float4 *PP;
 };
+// trig (nullable): {sin, cos(radians(la)), gs sin, gs cos(radians(trk))} the
+// caller computed with the same expressions (K4': its step's)
 __device__ __forceinline__ PFRec prep_home_record(int k, double la, double lo, double trk, double gs, double alt,
                                                   double vs, double rpz, double hpz, double tla, int mid, int rec,
                                                   const PrepOut &out, unsigned long long *nfw,
-                                                  unsigned long long nfe) {
+                                                  unsigned long long nfe, const double *trig = nullptr) {
   const double tlap = tla > 0.0 ? tla : 0.0;
-  const ColRec c = col_record_v(la, lo, trk, gs, alt, vs, la);
+  const ColRec c = trig ? col_record_t(la, lo, trig[0], trig[1], trig[2], trig[3], alt, vs, la)
+                        : col_record_v(la, lo, trk, gs, alt, vs, la);
   if (nfw && !col_tcpa_finite(c)) *nfw = nfe;
   if (rec) out.C[k] = c;
   const double sinl = c.sinlat, cosl = c.coslat;

@@ -138,9 +138,19 @@ __device__ __forceinline__ PFRec pilot_kin_row(int rb, int k, double simdt, int 
   d.gsn_w[k] = o.gsnorth;
   d.altprev[k] = s.alt;
   d.ax[k] = o.ax;
-  if (PREP)
+  if (PREP) {
+    // the record's trig from the step's: sin / cos of the new latitude, and
+    // without wind gs sin / cos(trk) = tas sin / cos(hdg) = gseast / gsnorth
+    double trig[4] = {o.sinlat, o.coslat, o.gseast, o.gsnorth};
+    if (winddim != 0) {
+      double st, ct;
+      sincos(o.trk * kD2R, &st, &ct);
+      trig[2] = o.gs * st;
+      trig[3] = o.gs * ct;
+    }
     return prep_home_record(k, o.lat, o.lon, o.trk, o.gs, o.alt, o.vs, pa.rpz, pa.hpz, pa.tla, pa.mid, pa.rec, pa.out,
-                            pa.nf, pa.nfe);
+                            pa.nf, pa.nfe, trig);
+  }
   return PFRec{};
 }
 
