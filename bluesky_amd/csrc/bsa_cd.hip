@@ -1767,30 +1767,48 @@ __device__ __forceinline__ bool cand_overflow(const Counters *cnt, unsigned long
 // grid's last lanes (K1b: the lanes past the candidate count; k_rowblk's extra
 // blocks when K1b is fused into the prefilter -- in K2's launch, whose lanes
 // would have had the time, its code cost K2 +5 us even when skipped).
-// Wave-uniform per loop trip.
+// Called by every thread of a block (block-uniform trips: it synchronises the
+// block).  One returning atomic per tier per BLOCK and trip, the block's
+// waves placed by an LDS prefix (one per wave contended on two words: ~350
+// at the 100k box, serialised at ~88 per us, were most of k_rowblk's 5.7 us).
+constexpr int kHeavyMaxWaves = 16;
 __device__ __forceinline__ void heavy_next(const HeavyNext &hn) {
+  __shared__ unsigned hcnt[2][kHeavyMaxWaves];
+  __shared__ unsigned hbase[2];
   const unsigned long long inear = hn.work[1], m = inear + hn.work[2];
   const unsigned long long nt = (unsigned long long)gridDim.x * blockDim.x;
-  const int lane = threadIdx.x & 63;
-  for (unsigned long long k = nt - 1 - ((unsigned long long)blockIdx.x * blockDim.x + threadIdx.x); k < m; k += nt) {
-    const unsigned long long slot = k < inear ? k : hn.icap - 1 - (k - inear);
-    const unsigned cst = hn.cost[slot];
-    hn.cost[slot] = 0u;
-    const int tier = cst >= hn.thresh[0] ? 0 : (cst >= hn.thresh[1] ? 1 : 2);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const unsigned long long mk = __ballot(tier == q);
-      if (mk) {
-        const int lead = __ffsll((long long)mk) - 1;
-        unsigned base = 0;
-        if (lane == lead) base = atomicAdd(&hn.count[q], (unsigned)__popcll(mk));
-        base = (unsigned)__shfl((int)base, lead);
-        if (tier == q) {
-          hn.list[q][base + lane_prefix(mk)] = (unsigned)slot;
-          hn.flag[slot] = hn.epoch;
-        }
-      }
+  const unsigned long long g0 = (unsigned long long)blockIdx.x * blockDim.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, W = (int)(blockDim.x >> 6);
+  // trip j: lane k = nt - 1 - (g0 + t) + j nt; the block's smallest is nt - g0 - blockDim.x + j nt
+  for (unsigned long long kb = nt - g0 - blockDim.x; kb < m; kb += nt) {
+    const unsigned long long k = kb + (blockDim.x - 1 - threadIdx.x);
+    unsigned long long slot = 0;
+    int tier = 2;
+    if (k < m) {
+      slot = k < inear ? k : hn.icap - 1 - (k - inear);
+      const unsigned cst = hn.cost[slot];
+      hn.cost[slot] = 0u;
+      tier = cst >= hn.thresh[0] ? 0 : (cst >= hn.thresh[1] ? 1 : 2);
     }
+    const unsigned long long mk0 = __ballot(tier == 0), mk1 = __ballot(tier == 1);
+    if (lane == 0) {
+      hcnt[0][w] = (unsigned)__popcll(mk0);
+      hcnt[1][w] = (unsigned)__popcll(mk1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      unsigned tot = 0;
+      for (int v = 0; v < W; ++v) tot += hcnt[threadIdx.x][v];
+      hbase[threadIdx.x] = tot ? atomicAdd(&hn.count[threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    if (tier < 2) {
+      unsigned off = hbase[tier];
+      for (int v = 0; v < w; ++v) off += hcnt[tier][v];
+      hn.list[tier][off + lane_prefix(tier == 0 ? mk0 : mk1)] = (unsigned)slot;
+      hn.flag[slot] = hn.epoch;
+    }
+    __syncthreads();  // (hcnt / hbase of the next trip)
   }
 }
 
@@ -2069,13 +2087,15 @@ __global__ __launch_bounds__(256) void k_rank(int nrows, Counters *__restrict__ 
 // per-row counts: bcnt[b], bcnt[nb + b]); one wave per block, kRankRows / 64
 // rows per lane (one load round trip; an overflowed detect's sums are never
 // read: k_rank_rows checks the overflow itself)
-constexpr unsigned kHeavyBlocks = 1024;  // k_rowblk's extra one-wave blocks for the heavy-item listing
-__global__ __launch_bounds__(64) void k_rowblk(int nrows, unsigned *__restrict__ rowcnt, HeavyNext hn) {
+// k_rowblk: 16 waves per block, wave w of block b sums row block 16 b + w
+constexpr int kRowblkWaves = 16;
+constexpr unsigned kHeavyBlocks = 64;  // k_rowblk's extra blocks for the heavy-item listing (65 536 lanes)
+__global__ __launch_bounds__(64 * kRowblkWaves) void k_rowblk(int nrows, unsigned *__restrict__ rowcnt, HeavyNext hn) {
   // (K1b fused into the prefilter: the next detect's listed items here, on
-  // every lane of the grid -- the host adds kHeavyBlocks blocks past the nb
-  // row blocks for them, ~1 slot per lane at the 100k box)
+  // every lane of the grid -- the host adds kHeavyBlocks blocks past the
+  // row-block sums for them, ~1 slot per lane at the 100k box)
   if (hn.cost) heavy_next(hn);
-  const int nb = rank_blocks(nrows), b = blockIdx.x, lane = threadIdx.x;
+  const int nb = rank_blocks(nrows), b = blockIdx.x * kRowblkWaves + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (b >= nb) return;
   unsigned c = 0, l = 0;
 #pragma unroll
@@ -3224,7 +3244,9 @@ int detect_enqueue(Ctx *c, double rpz, double hpz, double tla, int flags, int64_
   }
   if (B) {
     const bool hl = fuse && hn.cost;  // the heavy-item listing moves here from K1b
-    hipLaunchKernelGGL(k_rowblk, dim3((unsigned)rank_blocks((int)nrows) + (hl ? kHeavyBlocks : 0u)), dim3(64), 0,
+    hipLaunchKernelGGL(k_rowblk, dim3((unsigned)((rank_blocks((int)nrows) + kRowblkWaves - 1) / kRowblkWaves) +
+                                          (hl ? kHeavyBlocks : 0u)),
+                       dim3(64 * kRowblkWaves), 0,
                        c->stream, (int)nrows, (unsigned *)c->rowcnt.p, hl ? hn : HeavyNext{});
     const RankLaunch rl{(unsigned)rank_blocks((int)nrows), (int)nrows, dcnt, cap, (unsigned *)c->rowoff.p,
                         (unsigned *)c->rowcnt.p, (const uint2 *)c->kbuck.p, B, (const double *)c->cpay.p, (int)rb,
