@@ -100,11 +100,19 @@ def show(fn):
                   (frac * 100, np.interp(frac, np.cumsum(np.sort(dur)[::-1]) / dur.sum(), np.sort(en)) if False else
                    en[np.argsort(en)][np.searchsorted(np.cumsum(dur[np.argsort(en)]) / dur.sum(), frac)]))
         listed = (rec[:, 0] >> np.uint64(63)).astype(bool)
+        work_all = subs > 0
         npc = ((rec[:, 0] >> np.uint64(48)) & np.uint64(0x7fff)).astype(np.int64)
         if listed.any():
             print('  listed units %d (pieces %s): max %.1f us; unlisted max %.1f us (sub-groups %d, pieces %d)' %
                   (listed.sum(), np.unique(npc[listed]).tolist(), dur[listed].max(), dur[~listed].max(),
                    subs[~listed][np.argmax(dur[~listed])], npc[~listed][np.argmax(dur[~listed])]))
+            for pc in np.unique(npc[listed]).tolist():
+                sel = listed & (npc == pc) & work_all
+                if sel.any():
+                    print('    listed with %d piece(s): %d units, us p50 %.1f max %.1f, sub-groups p50 %d max %d, '
+                          'start p90 %.1f' % (pc, sel.sum(), np.median(dur[sel]), dur[sel].max(),
+                                              int(np.median(subs[sel])), int(subs[sel].max()),
+                                              np.percentile(st[sel], 90)))
             long = dur > 0.6 * dur.max()
             print('  units above 60%% of the max: %d, listed %d; (pieces, sub-groups, us) of the 6 longest: %s' %
                   (long.sum(), (long & listed).sum(),
@@ -113,6 +121,16 @@ def show(fn):
             print('  no listed units')
         starts = np.sort(st)
         print('  item starts: first %.1f, 50%% by %.1f, last %.1f us' % (starts[0], starts[len(starts) // 2], starts[-1]))
+        work = subs > 0
+        edges = np.arange(0.0, span + 5.0, 5.0)
+        print('  units with work in flight per 5 us: %s' % [int(((st < e + 5) & (en > e) & work).sum()) for e in edges])
+        p90 = np.percentile(last, 90)
+        tl = (en > p90) & work
+        if tl.any():
+            print('  tail (units ending after the p90 wave end, %.1f us): %d, listed %d; start p10/p50/p90 %s; '
+                  'us p50 %.1f max %.1f; sub-groups p50 %d max %d' %
+                  (p90, tl.sum(), (tl & listed).sum(), np.round(np.percentile(st[tl], [10, 50, 90]), 1).tolist(),
+                   np.median(dur[tl]), dur[tl].max(), int(np.median(subs[tl])), int(subs[tl].max())))
         det += 1
 
 
