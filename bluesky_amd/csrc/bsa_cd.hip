@@ -755,7 +755,7 @@ struct PairResult {
 // replaces qdrdist_matrix, its metre distance handed over in nm (/ nm) so that
 // StateBasedCD.py:22's `* nm` restores metres -- the reference's own detect
 // with the geo function swapped (tools/make_golden.py captures exactly that).
-template <bool KWIK>
+template <bool KWIK, bool SC = true>
 __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c, double rpz,
                                                 double hpz, double tla) {
   PairResult o;
@@ -767,7 +767,7 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
     dist_nm = dist_m / kNM;
   } else {
     // geo.qdrdist_matrix (geo.py:118-160)
-    qdrdist_entry(r.lat, r.lon, r.sinlat, r.coslat, r.hemA, c.lat, c.lon, c.sinlat, c.coslat, c.hemA,
+    qdrdist_entry<SC>(r.lat, r.lon, r.sinlat, r.coslat, r.hemA, c.lat, c.lon, c.sinlat, c.coslat, c.hemA,
                   c.eps, qdr, dist_nm);
   }
 
@@ -775,7 +775,7 @@ __device__ __forceinline__ PairResult eval_pair(const RowRec &r, const ColRec &c
   const double dist = dist_nm * kNM + 0.0;
   const double qdrrad = qdr * kD2R;
   double sq, cq;
-  sincos(qdrrad, &sq, &cq);
+  sin_cos<SC>(qdrrad, &sq, &cq);
   const double dx = dist * sq;
   const double dy = dist * cq;
   const double du = c.u - r.u;  // own.u[j] - int.u[i]
@@ -868,7 +868,7 @@ __device__ __forceinline__ void fuse_exact_one(const ExactFuse &xf, uint2 p, uns
                                                Counters *__restrict__ cnt) {
   const unsigned oi = xf.perm_r ? xf.perm_r[p.x] : (unsigned)xf.rb + p.x, oj = xf.perm_c[p.y];
   if (xf.perm_r ? oi == oj : oi == p.y) return;  // an aircraft against itself (never a pair)
-  const PairResult o = eval_pair<false>(xf.R[p.x], xf.C[p.y], xf.rpz, xf.hpz, xf.tla);
+  const PairResult o = eval_pair<false, false>(xf.R[p.x], xf.C[p.y], xf.rpz, xf.hpz, xf.tla);  // (sin_cos)
   exact_bucket(o, (int)oi - xf.rb, oj, p.y, id, xf.nrows, xf.B, xf.cpay, xf.rowcnt, xf.kb, cnt);
 }
 

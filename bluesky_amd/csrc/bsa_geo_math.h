@@ -68,9 +68,24 @@ __device__ __forceinline__ double rwgs84_sc(double sinlat, double coslat) {
   const double bdbd = bd * bd;
   return sqrt((anan + bnbn) / (adad + bdbd));
 }
+// sin and cos of one argument: one sincos (SC; bit for bit the separate
+// calls, tools/sincos_check.hip), or the separate calls -- for the fused
+// prefilter's K1b, where sincos's result pointers raised the kernel's
+// register pressure (scratch 24 -> 56 B per lane, +8 MB of spill writes per
+// launch at the 100k box)
+template <bool SC>
+__device__ __forceinline__ void sin_cos(double x, double *s, double *c) {
+  if (SC) {
+    sincos(x, s, c);
+  } else {
+    *s = sin(x);
+    *c = cos(x);
+  }
+}
+template <bool SC = true>
 __device__ __forceinline__ double rwgs84(double latd) {
   double sinlat, coslat;
-  sincos(latd * kD2R, &sinlat, &coslat);  // (bit for bit sin / cos: tools/sincos_check.hip)
+  sin_cos<SC>(latd * kD2R, &sinlat, &coslat);
   return rwgs84_sc(sinlat, coslat);
 }
 
@@ -91,6 +106,7 @@ __device__ __forceinline__ GeoPt geo_pt(double lat, double lon) {
 // One entry [i, j] of geo.qdrdist_matrix (geo.py:117-160): point 1 = row i,
 // point 2 = column j, eps = (lat1[j] == 0.) * 1e-6 (geo.py:128, indexed by
 // the column).  qdr [deg], dist [nm].
+template <bool SC = true>
 __device__ __forceinline__ void qdrdist_entry(double lat1, double lon1, double sinlat1, double coslat1,
                                               double hemA1, double lat2, double lon2, double sinlat2,
                                               double coslat2, double hemA2, double eps, double &qdr,
@@ -101,12 +117,12 @@ __device__ __forceinline__ void qdrdist_entry(double lat1, double lon1, double s
     // different hemisphere (geo.py:125-128)
     rr = (0.5 * (hemA1 + hemA2)) / (fabs(lat1) + (fabs(lat2) + eps));
   } else {
-    rr = rwgs84(lat1 + lat2);  // geo.py:121: radius at the SUM of the latitudes
+    rr = rwgs84<SC>(lat1 + lat2);  // geo.py:121: radius at the SUM of the latitudes
   }
   const double sin1 = (lat2 - lat1) * kD2R;
   const double sin2 = (lon2 - lon1) * kD2R;
   double sin21, cos21;
-  sincos(sin2, &sin21, &cos21);
+  sin_cos<SC>(sin2, &sin21, &cos21);
   const double y = sin21 * coslat2;
   const double x1 = coslat1 * sinlat2;
   const double x2 = sinlat1 * coslat2;
